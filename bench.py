@@ -1,0 +1,261 @@
+#!/usr/bin/env python3
+"""Benchmark of the EVAM pre-process hot path on MI355X (BASELINE.json metric).
+
+Default workload (BASELINE.json configs[1], "C2"): a batch of 32 synthetic 1920x1080 NV12 frames,
+device-resident, -> 32x3x512x512 fp32 NCHW normalised (range [0,1], ImageNet mean/std in BGR order),
+one fused kernel launch per step. Other configs (--config c1|c3|c4|c5) are the remaining BASELINE
+workloads; the driver's headline line is c2.
+
+    python bench.py [--gpus N --steps K --warmup W] [--config c2] [--no-cpu-baseline]
+
+Multi-GPU: one process per GPU (torchrun); camera streams are partitioned s mod G, every rank runs its
+own batch (weak scaling), no collective touches the hot loop; after the timed region one all_reduce(MAX)
+of the elapsed time and one all_gather of per-rank stats run over RCCL.
+
+Output: ONE JSON line from rank 0 with value = frames/s over all ranks, plus `roofline` (algorithmic
+bytes per launch / mean launch time from HIP events on the launch stream) and `cpu_baseline` (the C
+oracle, OpenMP on the host cores, on a bounded sample — rank 0 at N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+METRIC = "pre-processed frames/sec (1080p NV12→512² NCHW fp32) 1–8 GPU; % HBM peak"
+BGR_MEAN = (0.406, 0.456, 0.485)
+BGR_STD = (0.225, 0.224, 0.229)
+
+WORKLOADS = {
+    "c1": dict(desc="C1: 768x432 NV12 -> 512x512 u8 BGR NCHW (no normalisation)", fourcc="NV12", src=(768, 432),
+               frames=32, dst=(512, 512), dtype="u8", norm=False, mode="no-aspect-ratio"),
+    "c2": dict(desc="C2: 32x 1920x1080 NV12 (pitch 1920, device-resident) -> 32x3x512x512 fp32 NCHW, "
+                    "range [0,1] + mean/std", fourcc="NV12", src=(1920, 1080), frames=32, dst=(512, 512),
+               dtype="f32", norm=True, mode="no-aspect-ratio"),
+    "c3": dict(desc="C3: 32x 1080p NV12 frames x 50 seed-0 ROIs (w 24..400, h 24..300) -> 1600x3x72x72 fp32",
+               fourcc="NV12", src=(1920, 1080), frames=32, dst=(72, 72), dtype="f32", norm=True,
+               mode="no-aspect-ratio", rois=50),
+    "c4": dict(desc="C4: 64 streams x 3840x2160 NV12 -> 640x640 fp32 letterbox (640x360 + fill)", fourcc="NV12",
+               src=(3840, 2160), frames=64, dst=(640, 640), dtype="f32", norm=True, mode="aspect-ratio"),
+    "c5": dict(desc="C5: 32 streams x 1080p NV12 -> aspect(max) 398x224 -> central crop 224x224 fp32, "
+                    "slot t%16 of a [32,16,3,224,224] clip ring", fourcc="NV12", src=(1920, 1080), frames=32,
+               dst=(224, 224), dtype="f32", norm=False, mode="aspect-ratio", crop="central", ring=16),
+}
+
+
+def seed_rois(n_per_frame, n_frames, W, H):
+    rng = np.random.default_rng(0)
+    rois = []
+    for f in range(n_frames):
+        for _ in range(n_per_frame):
+            w = int(rng.integers(24, 401))
+            h = int(rng.integers(24, 301))
+            x = int(rng.integers(0, W - w + 1))
+            y = int(rng.integers(0, H - h + 1))
+            rois.append((f, x, y, w, h))
+    return rois
+
+
+def make_info(evam, wl):
+    kw = {}
+    if wl["norm"]:
+        kw.update(range=(0.0, 1.0), mean=BGR_MEAN, std=BGR_STD)
+    if wl["mode"] == "aspect-ratio":
+        kw.update(resize="aspect-ratio", crop=wl.get("crop"))
+    return evam.PreProcInfo(**kw)
+
+
+def device_frames(evam, torch, wl, n, device, seed):
+    """n synthetic frames, i.i.d. uniform bytes from a seeded device generator (one surface each)."""
+    gen = torch.Generator(device=device)
+    gen.manual_seed(seed)
+    fc = evam.preproc.FOURCC_BY_NAME[wl["fourcc"]]
+    W, H = wl["src"]
+    imgs = []
+    for _ in range(n):
+        planes = [torch.randint(0, 256, (r, p), dtype=torch.uint8, device=device, generator=gen)
+                  for r, p in evam.plane_layout(fc, W, H, pitch_align=16)]
+        imgs.append(evam.Image(fc, W, H, planes))
+    return imgs
+
+
+def cpu_baseline(wl, budget_s: float):
+    """Time the C oracle (the CPU restatement, OpenMP over output rows) on the host cores."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O  # checker / baseline only
+
+    O.build_c_oracle()
+    c = O.COracle()
+    cores = len(os.sched_getaffinity(0))
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit():
+        cores = min(cores, int(env))
+    c.set_num_threads(cores)
+    rng = np.random.default_rng(0)
+    fc = {"NV12": O.NV12, "I420": O.I420, "BGRX": O.BGRX, "BGR": O.BGR}[wl["fourcc"]]
+    frame = O.random_frame(rng, fc, *wl["src"])
+    DW, DH = wl["dst"]
+    f32 = wl["dtype"] == "f32"
+    lut = O.np_norm_lut(3, (0.0, 1.0), BGR_MEAN, BGR_STD) if wl["norm"] else O.np_norm_lut(0)
+    mode = {"no-aspect-ratio": 0, "aspect-ratio": 2 if wl.get("crop") else 1}[wl["mode"]]
+    rois = seed_rois(wl["rois"], 1, *wl["src"]) if wl.get("rois") else [(0, 0, 0, 0, 0)]
+    out = np.zeros((len(rois), 3, DH, DW), np.float32 if f32 else np.uint8)
+    frames = 0
+    t0 = time.perf_counter()
+    while True:
+        for i, r in enumerate(rois):
+            c.preprocess_item(frame, r[1:], out, i, mode=mode, lut=lut if f32 else None)
+        frames += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s and frames >= 2:
+            break
+    return {"value": round(frames / el, 3), "unit": "frames/s", "cores": cores, "kind": "port",
+            "sample": f"{frames} frame(s) of {wl['desc'].split(':')[0]} through the C oracle "
+                      f"(oracle/evam_oracle.c, OpenMP {cores} threads) in {el:.1f} s"}
+
+
+def load_pmc_traffic(config_name: str, n_frames_per_launch: int):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary for this workload, if any."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        d = json.load(open(path))
+        e = d.get(config_name)
+        if e and e.get("frames_per_launch") == n_frames_per_launch:
+            return e.get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--config", default="c2", choices=sorted(WORKLOADS))
+    ap.add_argument("--frames", type=int, default=0, help="frames per rank per step (default: workload's)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU-baseline work")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    import __graft_entry__ as g
+
+    evam = g.import_package()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    device = torch.device(f"cuda:{local}")
+    torch.cuda.set_device(device)
+
+    wl = WORKLOADS[args.config]
+    n = args.frames or wl["frames"]
+    if args.config == "c4" and world > 1:
+        n = max(1, wl["frames"] // world)  # 64 streams partitioned s mod G (strong split of a fixed stream set)
+    imgs = device_frames(evam, torch, wl, n, device, seed=1234 + rank)
+    batch = evam.ImageBatch(imgs)
+    info = make_info(evam, wl)
+    DW, DH = wl["dst"]
+    rois = None
+    if wl.get("rois"):
+        rois = [evam.Roi(*r) for r in seed_rois(wl["rois"], n, *wl["src"])]
+    n_items = len(rois) if rois is not None else n
+    ring = wl.get("ring")
+    out_n = n * ring if ring else n_items
+    dtype = torch.float32 if wl["dtype"] == "f32" else torch.uint8
+    out = torch.empty((out_n, 3, DH, DW), dtype=dtype, device=device)
+    pp = evam.HipPreProcessor(device=local)
+
+    def step(t):
+        if ring:
+            pp.convert(batch, out, info, slot_offset=t % ring, slot_stride=ring)
+        else:
+            pp.convert(batch, out, info, rois=rois)
+
+    # algorithmic bytes per launch, from the library's own accounting
+    pp.set_option(evam.native.OPT_STATS, 1)
+    step(0)
+    torch.cuda.synchronize()
+    st = pp.stats()
+    alg_bytes = int(st.src_bytes + st.dst_bytes)
+    pp.set_option(evam.native.OPT_STATS, 0)
+
+    for t in range(args.warmup):
+        step(t)
+    stream = torch.cuda.current_stream(device)
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for t in range(args.steps):
+        step(t)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    kern_ms = e0.elapsed_time(e1) / args.steps  # one launch per step
+    el = torch.tensor([wall], dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        # optional stats all-gather (frames, bytes, ns) — after timing, never in the hot loop
+        mine = torch.tensor([n * args.steps, alg_bytes * args.steps, int(kern_ms * args.steps * 1e6)],
+                            dtype=torch.int64, device=device)
+        allst = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(allst, mine)
+    wall_max = float(el.item())
+    total_frames = n * world * args.steps
+    value = total_frames / wall_max
+    achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+    traffic = load_pmc_traffic(args.config, n)
+
+    if rank == 0:
+        res = {
+            "metric": METRIC if args.config == "c2" else f"{METRIC} [{args.config}]",
+            "value": round(value, 1),
+            "unit": "frames/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(wall_max / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8" if wl["dtype"] == "u8" else "u8->f32",
+            "data": "synthetic (seeded uniform u8 planes generated on device; no video decode)",
+            "config": {"workload": wl["desc"], "frames_per_gpu_per_step": n, "items_per_launch": n_items,
+                       "src": f"{wl['src'][0]}x{wl['src'][1]} {wl['fourcc']}", "dst": f"{DW}x{DH}",
+                       "parallelism": f"streams s mod {world}, one process per GPU, no hot-loop collective"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "algorithmic_bytes_per_launch": alg_bytes, "mean_launch_ms": round(kern_ms, 5)},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            res["cpu_baseline"] = cpu_baseline(wl, args.cpu_budget)
+        else:
+            res["cpu_baseline"] = None
+        print(json.dumps(res), flush=True)
+    pp.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

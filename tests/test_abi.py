@@ -1,0 +1,100 @@
+"""CPU tests of the C ABI boundary: the library loads, exports every symbol include/evam_pp.h declares,
+struct layouts match the header, and the host-side error paths behave (no GPU compute calls)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "evam_pp.h")
+
+
+def header_functions():
+    src = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:int|void|const char\*)\s+(evam_pp_\w+)\s*\(", src, re.M)))
+
+
+def test_library_exports_every_declared_symbol(evam):
+    lib = evam.load_library()
+    declared = header_functions()
+    assert declared, "no functions parsed from the header"
+    assert set(declared) == set(evam.native.EXPORTED_SYMBOLS)
+    for name in declared:
+        assert hasattr(lib, name), f"{name} not exported"
+    assert lib.evam_pp_abi_version() == evam.native.ABI_VERSION
+
+
+def test_struct_sizes_match_header(evam):
+    for cls, size in evam.native.STRUCT_SIZES.items():
+        assert ctypes.sizeof(cls) == size, cls.__name__
+
+
+def test_header_enums_match_python(evam):
+    src = open(HEADER).read()
+    vals = {k: int(v, 0) for k, v in re.findall(r"(EVAM_\w+)\s*=\s*(-?0x[0-9A-Fa-f]+|-?\d+)", src)}
+    N = evam.native
+    assert vals["EVAM_FOURCC_NV12"] == N.FOURCC_NV12 and vals["EVAM_FOURCC_I420"] == N.FOURCC_I420
+    assert vals["EVAM_FOURCC_BGRX"] == N.FOURCC_BGRX and vals["EVAM_FOURCC_BGR"] == N.FOURCC_BGR
+    assert vals["EVAM_PP_ERR_EMPTY_ROI"] == N.ERR_EMPTY_ROI and vals["EVAM_PP_ERR_ALIGNMENT"] == N.ERR_ALIGNMENT
+    assert vals["EVAM_RESIZE_ASPECT_CROP"] == N.RESIZE_ASPECT_CROP
+    # FourCC = a | b<<8 | c<<16 | d<<24 of the DL Streamer names
+    for name, v in (("NV12", N.FOURCC_NV12), ("I420", N.FOURCC_I420), ("BGRX", N.FOURCC_BGRX)):
+        assert v == int.from_bytes(name.encode(), "little")
+
+
+def test_null_arguments_rejected(evam):
+    lib = evam.load_library()
+    assert lib.evam_pp_run(None, None, 0, None, 0, None, None, None) == evam.native.ERR_INVALID_ARG
+    assert b"NULL" in lib.evam_pp_last_error()
+    assert lib.evam_pp_sync(None) == evam.native.ERR_INVALID_ARG
+    assert lib.evam_pp_create(0, None, None) == evam.native.ERR_INVALID_ARG
+    lib.evam_pp_destroy(None)  # no-op
+
+
+def test_create_without_gpu_reports_no_device(evam):
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    lib = evam.load_library()
+    h = ctypes.c_void_p()
+    assert lib.evam_pp_create(0, None, ctypes.byref(h)) == evam.native.ERR_NO_DEVICE
+    with pytest.raises(evam.PreProcError):
+        evam.HipPreProcessor(device=0)
+
+
+def test_model_proc_mapping(evam):
+    """In-tree model-procs: vehicle-detection-0202 (input_preproc [] -> defaults) and
+    action-recognition-0001 (BGR, resize aspect-ratio, crop central), restated inline
+    (models_list/vehicle-detection-0202.json:3, models_list/action-recognition-0001.json:3-13)."""
+    N = evam.native
+    d = evam.PreProcInfo.from_model_proc(None)
+    c = d.to_c(N.DTYPE_U8)
+    assert (c.resize_mode, c.color_order, c.norm_flags) == (N.RESIZE_NO_ASPECT, N.COLOR_BGR, 0)
+    a = evam.PreProcInfo.from_model_proc({"format": "image", "layer_name": "0",
+                                          "params": {"color_space": "BGR", "resize": "aspect-ratio",
+                                                     "crop": "central"}})
+    assert a.to_c(N.DTYPE_F32).resize_mode == N.RESIZE_ASPECT_CROP
+    n = evam.PreProcInfo.from_model_proc({"params": {"range": [0, 1], "mean": [0.1, 0.2, 0.3], "std": [1, 2, 3],
+                                                     "color_space": "RGB"}})
+    c = n.to_c(N.DTYPE_F32)
+    assert c.norm_flags == 3 and c.color_order == N.COLOR_RGB and list(c.std) == [1.0, 2.0, 3.0]
+    with pytest.raises(evam.PreProcError):
+        evam.PreProcInfo(resize="aspect-ratio", crop="top_left").to_c(N.DTYPE_U8)
+    with pytest.raises(evam.PreProcError):
+        evam.PreProcInfo(color_space="GRAYSCALE").to_c(N.DTYPE_U8)
+
+
+def test_backend_selection(evam):
+    with pytest.raises(evam.PreProcError):
+        evam.create_preprocessor("opencv")
+    with pytest.raises(evam.PreProcError):
+        evam.create_preprocessor("nonsense")
+
+
+def test_transform_inverse(evam):
+    t = evam.Transform(scale_x=640 / 3840, scale_y=360 / 2160, crop_x=0, crop_y=0, crop_w=3840, crop_h=2160,
+                       pad_x=0, pad_y=140, resized_w=640, resized_h=360)
+    x, y = t.tensor_to_source(320, 320)
+    assert abs(x - 1920) < 1e-6 and abs(y - 1080) < 1e-6

@@ -1,0 +1,317 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle, bit-exact.
+
+u8 outputs must be byte-identical; fp32 outputs are compared bitwise too (the kernel maps the u8 result
+through a host-built LUT computed in the reference's operation order, so the bar north_star states —
+1e-6 relative — is met with zero error). Sizes are small enough for the oracle to finish in seconds, plus
+the full BASELINE configs through size-independent properties.
+"""
+import zlib
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+FORMATS = ["NV12", "I420", "BGRX", "BGR"]
+
+
+def fc(O, name):
+    return {"NV12": O.NV12, "I420": O.I420, "BGRX": O.BGRX, "BGR": O.BGR}[name]
+
+
+def upload(evam, frames, device):
+    return [evam.Image.from_host(f.fourcc, f.width, f.height, f.planes, device=device) for f in frames]
+
+
+def run_hip(evam, torch, imgs, shape, dtype, info=None, rois=None, slot_offset=0, slot_stride=1,
+            want_transform=False, pp=None, init=None):
+    out = torch.full(shape, init if init is not None else 7, dtype=dtype, device=imgs[0].planes[0].device)
+    own = pp is None
+    pp = pp or evam.HipPreProcessor(device=0)
+    xf = pp.convert(imgs, out, info, rois=rois, slot_offset=slot_offset, slot_stride=slot_stride,
+                    want_transform=want_transform)
+    torch.cuda.synchronize()
+    if own:
+        pp.close()
+    return out.cpu().numpy(), xf
+
+
+def info_lut(O, info):
+    if info is None:
+        return None
+    flags = (1 if info.range is not None else 0) | (2 if (info.mean is not None or info.std is not None) else 0)
+    return O.np_norm_lut(flags, info.range or (0.0, 255.0), info.mean or (0, 0, 0), info.std or (1, 1, 1))
+
+
+def run_oracle(O, coracle, frames, shape, dtype, info=None, rois=None, slot_offset=0, slot_stride=1, init=7):
+    ref = np.full(shape, init, dtype=np.float32 if dtype == "f32" else np.uint8)
+    mode = placement = 0
+    rgb = False
+    fill = (0, 0, 0)
+    if info is not None:
+        mode = info.resize_mode()
+        placement = 1 if info.placement == "center" else 0
+        rgb = info.color_space == "RGB"
+        fill = info.fill
+    lut = info_lut(O, info) if dtype == "f32" else None
+    if dtype == "f32" and lut is None:
+        lut = O.np_norm_lut(0)
+    items = rois if rois is not None else [(i, 0, 0, 0, 0) for i in range(len(frames))]
+    geoms = []
+    for i, (si, x, y, w, h) in enumerate(items):
+        g = coracle.preprocess_item(frames[si], (x, y, w, h), ref, slot_offset + i * slot_stride, mode=mode,
+                                    placement=placement, color_rgb=rgb, lut=lut, fill=fill)
+        geoms.append(g)
+    return ref, geoms
+
+
+def assert_same(got, ref, what=""):
+    if got.dtype == np.float32:
+        same = (got.view(np.uint32) == ref.view(np.uint32))
+    else:
+        same = got == ref
+    if not same.all():
+        bad = np.argwhere(~same)
+        i = tuple(bad[0])
+        raise AssertionError(f"{what}: {len(bad)} mismatches of {got.size}; first at {i}: got {got[i]} ref {ref[i]}")
+
+
+@pytest.mark.parametrize("fmt", FORMATS)
+@pytest.mark.parametrize("src,dst", [((64, 48), (512, 512)), ((66, 50), (33, 17)), ((160, 90), (72, 72)),
+                                     ((320, 180), (160, 90)), ((96, 64), (96, 64)), ((200, 120), (300, 70))])
+@pytest.mark.parametrize("dtype", ["u8", "f32"])
+def test_full_frame(evam, O, coracle, gpu, fmt, src, dst, dtype):
+    import torch
+
+    rng = np.random.default_rng(zlib.crc32(repr((fmt, src, dst)).encode()))
+    frames = [O.random_frame(rng, fc(O, fmt), src[0], src[1], pattern=p) for p in ("uniform", "gradient")]
+    info = evam.PreProcInfo(range=(0.0, 1.0), mean=(0.406, 0.456, 0.485), std=(0.225, 0.224, 0.229)) \
+        if dtype == "f32" else None
+    shape = (2, 3, dst[1], dst[0])
+    got, _ = run_hip(evam, torch, upload(evam, frames, gpu), shape, torch.float32 if dtype == "f32" else torch.uint8,
+                     info)
+    ref, _ = run_oracle(O, coracle, frames, shape, dtype, info)
+    assert_same(got, ref, f"{fmt} {src}->{dst} {dtype}")
+
+
+def test_numpy_restatement_agrees(evam, O, coracle, gpu):
+    """Third leg: the GPU output also equals the independent numpy restatement."""
+    import torch
+
+    rng = np.random.default_rng(5)
+    f = O.random_frame(rng, O.NV12, 130, 74)
+    got, _ = run_hip(evam, torch, upload(evam, [f], gpu), (1, 3, 40, 56), torch.uint8)
+    ref = O.np_preprocess_item(f, None, 56, 40)
+    assert_same(got[0], ref, "numpy restatement")
+
+
+@pytest.mark.parametrize("fmt", FORMATS)
+def test_roi_batch(evam, O, coracle, gpu, fmt):
+    """gvaclassify: ~50 variable ROIs per frame, incl. frame-edge, odd and partially outside rects."""
+    import torch
+
+    rng = np.random.default_rng(11)
+    W, H = 320, 240
+    frames = [O.random_frame(rng, fc(O, fmt), W, H) for _ in range(2)]
+    rois = []
+    for si in range(2):
+        for _ in range(50):
+            w = int(rng.integers(3, 200))
+            h = int(rng.integers(3, 150))
+            x = int(rng.integers(-20, W - 2))
+            y = int(rng.integers(-20, H - 2))
+            w, h = max(w, 3 - x), max(h, 3 - y)  # keep at least a sliver inside the frame
+            rois.append((si, x, y, w, h))
+    rois += [(0, 0, 0, W, H), (1, W - 3, H - 3, 10, 10), (0, 1, 1, 1, 1), (1, 5, 7, 9, 11)]
+    info = evam.PreProcInfo(range=(0.0, 1.0))
+    shape = (len(rois), 3, 72, 72)
+    got, _ = run_hip(evam, torch, upload(evam, frames, gpu), shape, torch.float32, info,
+                     rois=[evam.Roi(*r) for r in rois])
+    ref, _ = run_oracle(O, coracle, frames, shape, "f32", info, rois=rois)
+    assert_same(got, ref, f"roi batch {fmt}")
+
+
+@pytest.mark.parametrize("placement", ["top_left", "center"])
+@pytest.mark.parametrize("fill", [(0, 0, 0), (114, 114, 114), (1, 2, 3)])
+def test_letterbox(evam, O, coracle, gpu, placement, fill):
+    import torch
+
+    rng = np.random.default_rng(3)
+    frames = [O.random_frame(rng, O.NV12, 384, 216), O.random_frame(rng, O.NV12, 216, 384)]
+    info = evam.PreProcInfo(resize="aspect-ratio", placement=placement, fill=fill)
+    shape = (2, 3, 160, 160)
+    got, xf = run_hip(evam, torch, upload(evam, frames, gpu), shape, torch.uint8, info, want_transform=True)
+    ref, geoms = run_oracle(O, coracle, frames, shape, "u8", info)
+    assert_same(got, ref, f"letterbox {placement} {fill}")
+    for t, g in zip(xf, geoms):
+        assert (t.crop_x, t.crop_y, t.crop_w, t.crop_h, t.resized_w, t.resized_h, t.pad_x, t.pad_y) == g
+
+
+@pytest.mark.parametrize("fmt,src", [("NV12", (1920, 1080)), ("BGRX", (768, 432)), ("I420", (640, 480))])
+def test_aspect_central_crop(evam, O, coracle, gpu, fmt, src):
+    """action-recognition-0001 model-proc: BGR, resize aspect-ratio, crop central, 224x224."""
+    import torch
+
+    rng = np.random.default_rng(4)
+    frames = [O.random_frame(rng, fc(O, fmt), *src)]
+    info = evam.PreProcInfo.from_model_proc({"format": "image", "layer_name": "0", "params": {
+        "color_space": "BGR", "resize": "aspect-ratio", "crop": "central"}})
+    shape = (1, 3, 224, 224)
+    got, xf = run_hip(evam, torch, upload(evam, frames, gpu), shape, torch.float32, info, want_transform=True)
+    ref, geoms = run_oracle(O, coracle, frames, shape, "f32", info)
+    assert_same(got, ref, f"aspect crop {fmt} {src}")
+    if src == (1920, 1080):
+        assert (xf[0].resized_w, xf[0].resized_h, xf[0].pad_x) == (398, 224, -87)
+
+
+def test_clip_ring_slots(evam, O, coracle, gpu):
+    """C5 packing: frame t of stream s goes to slot s*16 + t%16 of a [S*16,3,H,W] ring."""
+    import torch
+
+    rng = np.random.default_rng(8)
+    S = 3
+    shape = (S * 16, 3, 32, 32)
+    out = torch.zeros(shape, dtype=torch.float32, device=gpu)
+    ref = np.zeros(shape, np.float32)
+    pp = evam.HipPreProcessor(device=0)
+    info = evam.PreProcInfo(resize="aspect-ratio", crop="central")
+    lut = O.np_norm_lut(0)
+    for t in range(18):
+        frames = [O.random_frame(rng, O.BGRX, 96, 54) for _ in range(S)]
+        pp.convert(upload(evam, frames, gpu), out, info, slot_offset=t % 16, slot_stride=16)
+        for s, f in enumerate(frames):
+            coracle.preprocess_item(f, None, ref, s * 16 + t % 16, mode=2, lut=lut)
+    torch.cuda.synchronize()
+    assert_same(out.cpu().numpy(), ref, "clip ring")
+    pp.close()
+
+
+def test_rgb_order_and_mixed_formats(evam, O, coracle, gpu):
+    """color_space=RGB swaps planes; one call may mix source formats (one launch per format)."""
+    import torch
+
+    rng = np.random.default_rng(9)
+    frames = [O.random_frame(rng, fc(O, n), 120, 68) for n in FORMATS]
+    info = evam.PreProcInfo(color_space="RGB", range=(-1.0, 1.0), mean=(0.1, 0.2, 0.3), std=(0.5, 0.25, 2.0))
+    shape = (4, 3, 50, 70)
+    got, _ = run_hip(evam, torch, upload(evam, frames, gpu), shape, torch.float32, info)
+    ref, _ = run_oracle(O, coracle, frames, shape, "f32", info)
+    assert_same(got, ref, "rgb mixed formats")
+
+
+def test_reuse_handle_changing_inputs(evam, O, coracle, gpu):
+    """The descriptor block cache must re-upload when frames / config change between calls."""
+    import torch
+
+    rng = np.random.default_rng(10)
+    pp = evam.HipPreProcessor(device=0)
+    for k in range(4):
+        frames = [O.random_frame(rng, O.NV12, 64 + 16 * k, 48 + 8 * k) for _ in range(2)]
+        info = evam.PreProcInfo(range=(0.0, float(k + 1)))
+        shape = (2, 3, 40, 40)
+        got, _ = run_hip(evam, torch, upload(evam, frames, gpu), shape, torch.float32, info, pp=pp)
+        ref, _ = run_oracle(O, coracle, frames, shape, "f32", info)
+        assert_same(got, ref, f"iteration {k}")
+    pp.close()
+
+
+def test_pitch_variants(evam, O, coracle, gpu):
+    """1080p NV12 with pitch 1920 and 2048 (C2 variants)."""
+    import torch
+
+    rng = np.random.default_rng(12)
+    for align in (16, 256):
+        f = O.random_frame(rng, O.NV12, 1920, 1080, pitch_align=align)
+        assert f.planes[0].shape[1] == (1920 if align == 16 else 2048)
+        got, _ = run_hip(evam, torch, upload(evam, [f], gpu), (1, 3, 512, 512), torch.uint8)
+        ref, _ = run_oracle(O, coracle, [f], (1, 3, 512, 512), "u8")
+        assert_same(got, ref, f"pitch {f.planes[0].shape[1]}")
+
+
+def test_c2_full_size_parity_and_properties(evam, O, coracle, gpu):
+    """Headline config at full size: 1080p NV12 batch -> 512x512 fp32 normalised.
+    Bit-exact vs the oracle on 4 distinct frames, and slot independence on a 32-frame batch."""
+    import torch
+
+    rng = np.random.default_rng(0)
+    frames = [O.random_frame(rng, O.NV12, 1920, 1080, pattern=p) for p in ("uniform", "gradient") * 2]
+    info = evam.PreProcInfo(range=(0.0, 1.0), mean=(0.406, 0.456, 0.485), std=(0.225, 0.224, 0.229))
+    imgs = upload(evam, frames, gpu)
+    got, _ = run_hip(evam, torch, imgs, (4, 3, 512, 512), torch.float32, info)
+    ref, _ = run_oracle(O, coracle, frames, (4, 3, 512, 512), "f32", info)
+    assert_same(got, ref, "C2 full size")
+    # 32 slots = the 4 frames repeated: every slot equals its frame's slot, whatever its position.
+    batch = [imgs[i % 4] for i in range(32)]
+    got32, _ = run_hip(evam, torch, batch, (32, 3, 512, 512), torch.float32, info)
+    for i in range(32):
+        assert_same(got32[i], got[i % 4], f"slot {i}")
+
+
+def test_constant_frame_property(evam, O, gpu):
+    """Size-independent property at the C4 size: a constant-colour 4K frame letterboxed to 640x640 gives the
+    constant's BT.601 colour in the 640x360 image and the fill value in the padding."""
+    import torch
+
+    W, H = 3840, 2160
+    f = O.random_frame(np.random.default_rng(0), O.NV12, W, H)
+    f.planes[0][:] = 150
+    f.planes[1][:, 0::2] = 90
+    f.planes[1][:, 1::2] = 200
+    img = upload(evam, [f], gpu)
+    info = evam.PreProcInfo(resize="aspect-ratio", fill=(9, 9, 9))
+    got, xf = run_hip(evam, torch, img, (1, 3, 640, 640), torch.uint8, info, want_transform=True)
+    b, g, r = (int(v) for v in O.np_yuv_pixel(150, 90, 200))
+    assert (xf[0].resized_w, xf[0].resized_h) == (640, 360)
+    assert (got[0, 0, :360] == b).all() and (got[0, 1, :360] == g).all() and (got[0, 2, :360] == r).all()
+    assert (got[0, :, 360:] == 9).all()
+
+
+@pytest.mark.parametrize("case", ["empty_roi", "bad_fourcc", "misaligned_pitch", "slot_oob", "odd_yuv",
+                                  "bad_dtype", "src_index"])
+def test_errors(evam, O, gpu, case):
+    import torch
+
+    rng = np.random.default_rng(1)
+    f = O.random_frame(rng, O.NV12, 64, 48)
+    img = upload(evam, [f], gpu)[0]
+    out = torch.zeros((1, 3, 16, 16), dtype=torch.uint8, device=gpu)
+    rois = None
+    if case == "empty_roi":
+        rois = [evam.Roi(0, 100, 100, 10, 10)]
+    elif case == "bad_fourcc":
+        img = evam.Image(0x12345678, 64, 48, img.planes)
+    elif case == "misaligned_pitch":
+        p = torch.zeros((48, 72), dtype=torch.uint8, device=gpu)
+        img = evam.Image(O.NV12, 64, 48, [p, img.planes[1]])
+    elif case == "slot_oob":
+        rois = [evam.Roi(0, 0, 0, 0, 0), evam.Roi(0, 0, 0, 0, 0)]
+    elif case == "odd_yuv":
+        img = evam.Image(O.NV12, 63, 48, img.planes)
+    elif case == "bad_dtype":
+        out = torch.zeros((1, 3, 16, 16), dtype=torch.float16, device=gpu)
+    elif case == "src_index":
+        rois = [evam.Roi(3, 0, 0, 0, 0)]
+    pp = evam.HipPreProcessor(device=0)
+    with pytest.raises(evam.PreProcError) as ei:
+        pp.convert([img], out, rois=rois)
+    expected = {"empty_roi": -4, "bad_fourcc": -2, "misaligned_pitch": -3, "slot_oob": -1, "odd_yuv": -1,
+                "bad_dtype": -2, "src_index": -1}[case]
+    assert ei.value.status == expected, str(ei.value)
+    pp.close()
+
+
+def test_stats_and_timing(evam, O, gpu):
+    """Byte accounting of SURVEY §8(d) for C2: 6,148,608 algorithmic bytes per frame."""
+    import torch
+
+    f = O.random_frame(np.random.default_rng(0), O.NV12, 1920, 1080)
+    img = upload(evam, [f], gpu)
+    pp = evam.HipPreProcessor(device=0)
+    pp.set_option(evam.native.OPT_STATS, 1)
+    pp.set_option(evam.native.OPT_TIMING, 1)
+    out = torch.empty((2, 3, 512, 512), dtype=torch.float32, device=gpu)
+    pp.convert(img * 2, out, evam.PreProcInfo(range=(0.0, 1.0)))
+    st = pp.stats()
+    assert st.src_bytes == 2 * 3_002_880 and st.dst_bytes == 2 * 3_145_728
+    assert st.n_launches == 1 and st.last_kernel_ms > 0
+    pp.close()
