@@ -70,26 +70,39 @@ struct KParams {
     const float* lut;  // [3][256]
     void* dst;
     int DW, DH;
-    int TW, TH, tiles_x, tiles_per_item;
+    int TW, TH, tiles_x, tiles_per_item, n_tiles;
     uint32_t tw_magic;  // ceil(2^32 / TW)
-    int strideY, strideC;  // LDS bytes per staged row
-    int offRow, offSlot, offLut, offY, offC, offV;  // LDS carve (coltab at 0)
+    int tab_bytes;      // one table set: coltab | rowtab | slotY | slotC
+    int buf_bytes;      // one staging buffer (upper bound of a tile's packed footprint)
+    int offTab, offBuf; // LDS carve: LUT at 0 (fp32 out), 2 table sets at offTab, 2 buffers at offBuf
     int color_rgb;
-    uint32_t fill;  // packed u8 fill, output channel order
+    uint32_t fill;      // packed u8 fill, output channel order
 };
 
 struct ColEntry {  // 16 B, one per tile column
-    int16_t oY0, oY1;  // LDS byte offset of the two taps in a staged luma/packed row (-1: column not in image)
-    int16_t oC0, oC1;  // LDS byte offset in a staged chroma row (NV12: U of the UV pair)
+    int16_t oY0, oY1;  // byte offset of the two taps inside a staged luma/packed row (-1: not in image)
+    int16_t oC0, oC1;  // byte offset inside a staged chroma row (NV12: U of the UV pair)
     int16_t a0, a1;    // 11-bit horizontal weights
     int16_t pad0, pad1;
 };
 
 struct RowEntry {  // 32 B, one per tile row
-    int32_t y0, y1;   // LDS byte offsets of the two staged luma rows (-1: row not in image)
-    int32_t c0, c1;   // LDS byte offsets of the two staged chroma rows
+    int32_t y0, y1;   // buffer byte offsets of the two staged luma rows (-1: row not in image)
+    int32_t c0, c1;   // buffer byte offsets of the two staged chroma rows
     int32_t b0, b1;   // 11-bit vertical weights
     int32_t pad0, pad1;
+};
+
+// Per-tile values every lane holds (wave-uniform).
+struct TileInfo {
+    const uint8_t* plane[3];  // copied out of the descriptor during setup: no descriptor load may sit
+    int pitch[3];             // between the DMA issue and the compute (its vmcnt wait would drain the DMA)
+    int slot;
+    int X0, Y0, X1, Y1;
+    int active;        // the tile shows part of the resized image (else pure padding)
+    int fsY, cprY;     // luma/packed footprint: 16-B aligned start byte, 16-B chunks per row
+    int fsC, cprC;     // chroma footprint
+    int offC, offV;    // chroma / V plane offsets inside the staging buffer
 };
 
 // ------------------------------------------------------------------------------------------------
@@ -120,38 +133,40 @@ __device__ __forceinline__ uint32_t umulhi(uint32_t a, uint32_t b) { return __um
 
 __device__ __forceinline__ int clamp255(int v) { return min(max(v, 0), 255); }
 
-// BT.601 20-bit fixed point (OpenCV uvToRGBuv + yRGBuvToRGBA). Arguments are raw bytes.
+// BT.601 20-bit fixed point (OpenCV uvToRGBuv + yRGBuvToRGBA). Arguments are raw bytes; every
+// product fits the full-rate 24-bit multiplier.
 __device__ __forceinline__ void yuv_to_bgr(int Y, int U, int V, int& b, int& g, int& r) {
-    const int y = max(Y - 16, 0) * kCY;
-    const int ruv = kCVR * V + kKR;
-    const int guv = kCVG * V + kCUG * U + kKG;
-    const int buv = kCUB * U + kKB;
+    const int y = __mul24(max(Y - 16, 0), kCY);
+    const int ruv = __mul24(kCVR, V) + kKR;
+    const int guv = __mul24(kCVG, V) + __mul24(kCUG, U) + kKG;
+    const int buv = __mul24(kCUB, U) + kKB;
     b = clamp255((y + buv) >> 20);
     g = clamp255((y + guv) >> 20);
     r = clamp255((y + ruv) >> 20);
 }
 
 template <int FMT>
-__device__ __forceinline__ void tap(const uint8_t* __restrict__ lds, int yrow, int crow, int vrow, int oy,
+__device__ __forceinline__ void tap(const uint8_t* __restrict__ buf, int yrow, int crow, int vrow, int oy,
                                     int oc, int& b, int& g, int& r) {
     if constexpr (FMT == kNV12) {
-        const int Y = lds[yrow + oy];
-        const uint32_t uv = *reinterpret_cast<const uint16_t*>(lds + crow + oc);
+        const int Y = buf[yrow + oy];
+        const uint32_t uv = *reinterpret_cast<const uint16_t*>(buf + crow + oc);
         yuv_to_bgr(Y, uv & 0xFF, uv >> 8, b, g, r);
     } else if constexpr (FMT == kI420) {
-        const int Y = lds[yrow + oy];
-        yuv_to_bgr(Y, lds[crow + oc], lds[vrow + oc], b, g, r);
+        const int Y = buf[yrow + oy];
+        yuv_to_bgr(Y, buf[crow + oc], buf[vrow + oc], b, g, r);
     } else if constexpr (FMT == kBGRX) {
-        const uint32_t p = *reinterpret_cast<const uint32_t*>(lds + yrow + oy);
+        const uint32_t p = *reinterpret_cast<const uint32_t*>(buf + yrow + oy);
         b = p & 0xFF; g = (p >> 8) & 0xFF; r = (p >> 16) & 0xFF;
     } else {
-        b = lds[yrow + oy]; g = lds[yrow + oy + 1]; r = lds[yrow + oy + 2];
+        b = buf[yrow + oy]; g = buf[yrow + oy + 1]; r = buf[yrow + oy + 2];
     }
 }
 
-// VResizeLinear<uchar,int,short,FixedPtCast<int,uchar,22>,VResizeLinearVec_32s8u>
+// VResizeLinear<uchar,int,short,FixedPtCast<int,uchar,22>,VResizeLinearVec_32s8u>.
+// D >> 4 <= 32655 and |b| <= 2048, so both products are exact on the 24-bit multiplier.
 __device__ __forceinline__ int vresize(int D0, int D1, int b0, int b1) {
-    return (((b0 * (D0 >> 4)) >> 16) + ((b1 * (D1 >> 4)) >> 16) + 2) >> 2;
+    return ((__mul24(b0, D0 >> 4) >> 16) + (__mul24(b1, D1 >> 4) >> 16) + 2) >> 2;
 }
 
 template <int FMT>
@@ -160,23 +175,30 @@ struct FmtTraits {
     static constexpr int nchroma = FMT == kNV12 ? 1 : (FMT == kI420 ? 2 : 0);
 };
 
-// 128-bit row staging: n_slots rows of `bytes` bytes (multiple of 16) from global to LDS.
-__device__ __forceinline__ void stage_plane(uint8_t* __restrict__ lds, int lds_off, int stride,
-                                            const int32_t* __restrict__ slot_rows, int n_slots,
-                                            const uint8_t* __restrict__ plane, int pitch, int fs, int bytes,
-                                            int tid) {
-    const int cpr = bytes >> 4;
+// One 16-byte LDS-DMA load: global -> LDS at (wave-uniform lds_base + lane * 16).
+__device__ __forceinline__ void glds16(const uint8_t* g, uint8_t* lds_wave_base) {
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                     (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+}
+
+// Issue the LDS-DMA loads of one plane's staged rows. Rows are packed back to back in the buffer
+// (row slot s at s * cpr * 16), so chunk c of the flattened (slot, column) space lands at c * 16 and a
+// wave's 64 chunks form one contiguous 1 KiB LDS run, as LDS-DMA requires. Skipped slots (row < 0:
+// duplicate or invisible rows) issue nothing.
+__device__ __forceinline__ void issue_plane(uint8_t* lds_plane, const int32_t* __restrict__ slot_rows, int n_slots,
+                                            const uint8_t* __restrict__ plane, int pitch, int fs, int cpr, int tid) {
     if (cpr <= 0) return;
     const uint32_t magic = 0xFFFFFFFFu / (uint32_t)cpr + 1u;
     const int total = n_slots * cpr;
-#pragma unroll 4
-    for (int c = tid; c < total; c += kThreads) {
-        const int slot = (cpr & (cpr - 1)) == 0 ? (c >> __builtin_ctz(cpr)) : (int)umulhi((uint32_t)c, magic);
-        const int col = c - slot * cpr;
-        const int row = slot_rows[slot];
-        if (row >= 0) {
-            const uint4 v = *reinterpret_cast<const uint4*>(plane + (size_t)row * pitch + fs + col * 16);
-            *reinterpret_cast<uint4*>(lds + lds_off + slot * stride + col * 16) = v;
+    const int wave_off = tid & ~63;
+    for (int c0 = 0; c0 < total; c0 += kThreads) {
+        const int c = c0 + tid;
+        if (c < total) {
+            const int slot = (int)umulhi((uint32_t)c, magic);
+            const int col = c - slot * cpr;
+            const int row = slot_rows[slot];
+            if (row >= 0)
+                glds16(plane + (uint32_t)row * (uint32_t)pitch + fs + col * 16, lds_plane + (c0 + wave_off) * 16);
         }
     }
 }
@@ -197,81 +219,74 @@ __device__ __forceinline__ void store_px(const KParams& P, const float* __restri
     }
 }
 
-template <int FMT, int OUT>
-__global__ __launch_bounds__(kThreads) void evam_pp_kernel(const KParams P) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+// Tile geometry, footprint and coefficient tables (written to the table set `tab`).
+template <int FMT>
+__device__ __forceinline__ void setup_tile(const KParams& P, int t, uint8_t* tab, TileInfo& ti) {
     using T = FmtTraits<FMT>;
     const int tid = threadIdx.x;
-    const int item_idx = blockIdx.x / P.tiles_per_item;
-    const int tile = blockIdx.x - item_idx * P.tiles_per_item;
+    const int item = t / P.tiles_per_item;
+    const int tile = t - item * P.tiles_per_item;
     const int ty = tile / P.tiles_x;
     const int tx = tile - ty * P.tiles_x;
-    const ItemDesc& it = P.items[item_idx];
-
-    const int X0 = tx * P.TW, Y0 = ty * P.TH;
-    const int X1 = min(X0 + P.TW, P.DW), Y1 = min(Y0 + P.TH, P.DH);
-    const size_t plane = (size_t)P.DW * P.DH;
-    const size_t slot_base = (size_t)it.slot * 3 * plane;
-    const int npx = P.TW * P.TH;
-
-    float* lut_s = reinterpret_cast<float*>(smem + P.offLut);
-    if constexpr (OUT == 1) {
-        for (int i = tid; i < 768; i += kThreads) lut_s[i] = P.lut[i];
+    // Descriptors are read-only for the launch: read them through the constant address space so they
+    // become scalar (s_load, lgkmcnt) loads, which never wait behind the LDS-DMA on vmcnt.
+    const __attribute__((address_space(4))) ItemDesc* it =
+        (const __attribute__((address_space(4))) ItemDesc*)(P.items) + item;
+    for (int i = 0; i < 3; i++) {
+        ti.plane[i] = it->plane[i];
+        ti.pitch[i] = it->pitch[i];
     }
+    ti.slot = it->slot;
+    ti.X0 = tx * P.TW;
+    ti.Y0 = ty * P.TH;
+    ti.X1 = min(ti.X0 + P.TW, P.DW);
+    ti.Y1 = min(ti.Y0 + P.TH, P.DH);
+    const int ox = it->ox, oy = it->oy, rw = it->rw, rh = it->rh, cw = it->cw, ch = it->ch;
+    const int x0 = it->x0, y0 = it->y0;
+    const double scx = it->scale_x, scy = it->scale_y;
+    const int dx_lo = max(ti.X0 - ox, 0), dx_hi = min(ti.X1 - ox, rw) - 1;
+    const int dy_lo = max(ti.Y0 - oy, 0), dy_hi = min(ti.Y1 - oy, rh) - 1;
+    ti.active = dx_lo <= dx_hi && dy_lo <= dy_hi;
+    ti.fsY = ti.cprY = ti.fsC = ti.cprC = ti.offC = ti.offV = 0;
+    if (!ti.active) return;
 
-    // visible resized-image range inside this tile
-    const int dx_lo = max(X0 - it.ox, 0), dx_hi = min(X1 - it.ox, it.rw) - 1;
-    const int dy_lo = max(Y0 - it.oy, 0), dy_hi = min(Y1 - it.oy, it.rh) - 1;
-    const int f0 = P.fill & 0xFF, f1 = (P.fill >> 8) & 0xFF, f2 = (P.fill >> 16) & 0xFF;
-
-    if (dx_lo > dx_hi || dy_lo > dy_hi) {  // pure padding tile: no source traffic
-        if constexpr (OUT == 1) __syncthreads();
-        for (int p = tid; p < npx; p += kThreads) {
-            const int ly = (int)umulhi((uint32_t)p, P.tw_magic);
-            const int lx = p - ly * P.TW;
-            const int X = X0 + lx, Y = Y0 + ly;
-            if (X < X1 && Y < Y1) store_px<OUT>(P, lut_s, slot_base + (size_t)Y * P.DW + X, plane, f0, f1, f2);
-        }
-        return;
-    }
-
-    // ---- 1. coefficient tables for this tile, LDS offsets relative to the 16-B aligned footprint ----
-    int sxa, sxb, cdummy0, cdummy1;
-    linear_coef(dx_lo, it.scale_x, it.cw, true, sxa, cdummy0, cdummy1);
-    linear_coef(dx_hi, it.scale_x, it.cw, true, sxb, cdummy0, cdummy1);
-    const int xa = it.x0 + sxa;                        // first source column touched
-    const int xb = it.x0 + min(sxb + 1, it.cw - 1);    // last source column touched
-    const int fsY = (xa * T::bpp) & ~15;
-    const int feY = (xb * T::bpp + T::bpp + 15) & ~15;
-    int fsC = 0, feC = 0;
+    int sxa, sxb, cd0, cd1;
+    linear_coef(dx_lo, scx, cw, true, sxa, cd0, cd1);
+    linear_coef(dx_hi, scx, cw, true, sxb, cd0, cd1);
+    const int xa = x0 + sxa;                      // first source column touched
+    const int xb = x0 + min(sxb + 1, cw - 1);     // last source column touched
+    ti.fsY = (xa * T::bpp) & ~15;
+    ti.cprY = (((xb * T::bpp + T::bpp + 15) & ~15) - ti.fsY) >> 4;
     if constexpr (FMT == kNV12) {
-        fsC = (2 * (xa >> 1)) & ~15;
-        feC = (2 * (xb >> 1) + 2 + 15) & ~15;
+        ti.fsC = (2 * (xa >> 1)) & ~15;
+        ti.cprC = (((2 * (xb >> 1) + 2 + 15) & ~15) - ti.fsC) >> 4;
     } else if constexpr (FMT == kI420) {
-        fsC = (xa >> 1) & ~15;
-        feC = ((xb >> 1) + 1 + 15) & ~15;
+        ti.fsC = (xa >> 1) & ~15;
+        ti.cprC = ((((xb >> 1) + 1 + 15) & ~15) - ti.fsC) >> 4;
     }
+    const int fwY = ti.cprY * 16, fwC = ti.cprC * 16;
+    ti.offC = 2 * P.TH * fwY;
+    ti.offV = ti.offC + 2 * P.TH * fwC;
 
-    ColEntry* coltab = reinterpret_cast<ColEntry*>(smem);
-    RowEntry* rowtab = reinterpret_cast<RowEntry*>(smem + P.offRow);
-    int32_t* slotY = reinterpret_cast<int32_t*>(smem + P.offSlot);
+    ColEntry* coltab = reinterpret_cast<ColEntry*>(tab);
+    RowEntry* rowtab = reinterpret_cast<RowEntry*>(tab + P.TW * (int)sizeof(ColEntry));
+    int32_t* slotY = reinterpret_cast<int32_t*>(tab + P.TW * (int)sizeof(ColEntry) + P.TH * (int)sizeof(RowEntry));
     int32_t* slotC = slotY + 2 * P.TH;
-
     for (int lx = tid; lx < P.TW; lx += kThreads) {
         ColEntry e;
-        const int dx = X0 + lx - it.ox;
-        if (X0 + lx < X1 && dx >= 0 && dx < it.rw) {
+        const int dx = ti.X0 + lx - ox;
+        if (ti.X0 + lx < ti.X1 && dx >= 0 && dx < rw) {
             int sx, a0, a1;
-            linear_coef(dx, it.scale_x, it.cw, true, sx, a0, a1);
-            const int ca = it.x0 + sx, cb = it.x0 + min(sx + 1, it.cw - 1);
-            e.oY0 = (int16_t)(ca * T::bpp - fsY);
-            e.oY1 = (int16_t)(cb * T::bpp - fsY);
+            linear_coef(dx, scx, cw, true, sx, a0, a1);
+            const int ca = x0 + sx, cb = x0 + min(sx + 1, cw - 1);
+            e.oY0 = (int16_t)(ca * T::bpp - ti.fsY);
+            e.oY1 = (int16_t)(cb * T::bpp - ti.fsY);
             if constexpr (FMT == kNV12) {
-                e.oC0 = (int16_t)(2 * (ca >> 1) - fsC);
-                e.oC1 = (int16_t)(2 * (cb >> 1) - fsC);
+                e.oC0 = (int16_t)(2 * (ca >> 1) - ti.fsC);
+                e.oC1 = (int16_t)(2 * (cb >> 1) - ti.fsC);
             } else {
-                e.oC0 = (int16_t)((ca >> 1) - fsC);
-                e.oC1 = (int16_t)((cb >> 1) - fsC);
+                e.oC0 = (int16_t)((ca >> 1) - ti.fsC);
+                e.oC1 = (int16_t)((cb >> 1) - ti.fsC);
             }
             e.a0 = (int16_t)a0;
             e.a1 = (int16_t)a1;
@@ -283,25 +298,25 @@ __global__ __launch_bounds__(kThreads) void evam_pp_kernel(const KParams P) {
     }
     for (int ly = tid; ly < P.TH; ly += kThreads) {
         RowEntry e;
-        const int dy = Y0 + ly - it.oy;
+        const int dy = ti.Y0 + ly - oy;
         int ya = -1, yb = -1, ca = -1, cb = -1;
-        if (Y0 + ly < Y1 && dy >= 0 && dy < it.rh) {
+        if (ti.Y0 + ly < ti.Y1 && dy >= 0 && dy < rh) {
             int sy, b0, b1;
-            linear_coef(dy, it.scale_y, it.ch, false, sy, b0, b1);
-            ya = it.y0 + min(max(sy, 0), it.ch - 1);
-            yb = it.y0 + min(max(sy + 1, 0), it.ch - 1);
-            e.y0 = P.offY + (2 * ly) * P.strideY;
-            e.y1 = yb == ya ? e.y0 : P.offY + (2 * ly + 1) * P.strideY;
+            linear_coef(dy, scy, ch, false, sy, b0, b1);
+            ya = y0 + min(max(sy, 0), ch - 1);
+            yb = y0 + min(max(sy + 1, 0), ch - 1);
+            e.y0 = (2 * ly) * fwY;
+            e.y1 = yb == ya ? e.y0 : (2 * ly + 1) * fwY;
+            if (yb == ya) yb = -1;
             if constexpr (T::nchroma > 0) {
                 ca = ya >> 1;
-                cb = yb >> 1;
-                e.c0 = (2 * ly) * P.strideC;
-                e.c1 = cb == ca ? e.c0 : (2 * ly + 1) * P.strideC;
+                cb = (yb < 0 ? ya : yb) >> 1;
+                e.c0 = ti.offC + (2 * ly) * fwC;
+                e.c1 = cb == ca ? e.c0 : ti.offC + (2 * ly + 1) * fwC;
                 if (cb == ca) cb = -1;
             } else {
                 e.c0 = 0; e.c1 = 0;
             }
-            if (yb == ya) yb = -1;
             e.b0 = b0;
             e.b1 = b1;
         } else {
@@ -314,25 +329,43 @@ __global__ __launch_bounds__(kThreads) void evam_pp_kernel(const KParams P) {
         slotC[2 * ly] = ca;
         slotC[2 * ly + 1] = cb;
     }
-    __syncthreads();
+}
 
-    // ---- 2. stage the source footprint (HBM -> LDS, 16 B per lane) ----
-    stage_plane(smem, P.offY, P.strideY, slotY, 2 * P.TH, it.plane[0], it.pitch[0], fsY, feY - fsY, tid);
+template <int FMT>
+__device__ __forceinline__ void issue_tile(const KParams& P, const TileInfo& ti, const uint8_t* tab, uint8_t* buf) {
+    using T = FmtTraits<FMT>;
+    const int tid = threadIdx.x;
+    const int32_t* slotY = reinterpret_cast<const int32_t*>(tab + P.TW * (int)sizeof(ColEntry) + P.TH * (int)sizeof(RowEntry));
+    const int32_t* slotC = slotY + 2 * P.TH;
+    issue_plane(buf, slotY, 2 * P.TH, ti.plane[0], ti.pitch[0], ti.fsY, ti.cprY, tid);
     if constexpr (T::nchroma >= 1)
-        stage_plane(smem, P.offC, P.strideC, slotC, 2 * P.TH, it.plane[1], it.pitch[1], fsC, feC - fsC, tid);
+        issue_plane(buf + ti.offC, slotC, 2 * P.TH, ti.plane[1], ti.pitch[1], ti.fsC, ti.cprC, tid);
     if constexpr (T::nchroma == 2)
-        stage_plane(smem, P.offV, P.strideC, slotC, 2 * P.TH, it.plane[2], it.pitch[2], fsC, feC - fsC, tid);
-    __syncthreads();
+        issue_plane(buf + ti.offV, slotC, 2 * P.TH, ti.plane[2], ti.pitch[2], ti.fsC, ti.cprC, tid);
+}
 
-    // ---- 3. convert + resize + normalise + planar store ----
-    const int cbase = P.offC;
-    const int vdelta = P.offV - P.offC;
+// Convert + resize + normalise + planar store of one tile from its staged footprint.
+template <int FMT, int OUT>
+__device__ __forceinline__ void compute_tile(const KParams& P, const TileInfo& ti, const uint8_t* tab,
+                                             const uint8_t* buf, const float* lut_s) {
+    const int tid = threadIdx.x;
+    const size_t plane = (size_t)P.DW * P.DH;
+    const size_t slot_base = (size_t)ti.slot * 3 * plane;
+    const int npx = P.TW * P.TH;
+    const int f0 = P.fill & 0xFF, f1 = (P.fill >> 8) & 0xFF, f2 = (P.fill >> 16) & 0xFF;
+    const ColEntry* coltab = reinterpret_cast<const ColEntry*>(tab);
+    const RowEntry* rowtab = reinterpret_cast<const RowEntry*>(tab + P.TW * (int)sizeof(ColEntry));
+    const int vdelta = ti.offV - ti.offC;
     for (int p = tid; p < npx; p += kThreads) {
         const int ly = (int)umulhi((uint32_t)p, P.tw_magic);
         const int lx = p - ly * P.TW;
-        const int X = X0 + lx, Y = Y0 + ly;
-        if (X >= X1 || Y >= Y1) continue;
+        const int X = ti.X0 + lx, Y = ti.Y0 + ly;
+        if (X >= ti.X1 || Y >= ti.Y1) continue;
         const size_t base = slot_base + (size_t)Y * P.DW + X;
+        if (!ti.active) {
+            store_px<OUT>(P, lut_s, base, plane, f0, f1, f2);
+            continue;
+        }
         const ColEntry ce = coltab[lx];
         const RowEntry re = rowtab[ly];
         if (ce.oY0 < 0 || re.y0 < 0) {
@@ -340,18 +373,16 @@ __global__ __launch_bounds__(kThreads) void evam_pp_kernel(const KParams P) {
             continue;
         }
         int bA, gA, rA, bB, gB, rB;
-        // row 0
-        tap<FMT>(smem, re.y0, cbase + re.c0, cbase + re.c0 + vdelta, ce.oY0, ce.oC0, bA, gA, rA);
-        tap<FMT>(smem, re.y0, cbase + re.c0, cbase + re.c0 + vdelta, ce.oY1, ce.oC1, bB, gB, rB);
-        const int Db0 = bA * ce.a0 + bB * ce.a1;
-        const int Dg0 = gA * ce.a0 + gB * ce.a1;
-        const int Dr0 = rA * ce.a0 + rB * ce.a1;
-        // row 1
-        tap<FMT>(smem, re.y1, cbase + re.c1, cbase + re.c1 + vdelta, ce.oY0, ce.oC0, bA, gA, rA);
-        tap<FMT>(smem, re.y1, cbase + re.c1, cbase + re.c1 + vdelta, ce.oY1, ce.oC1, bB, gB, rB);
-        const int Db1 = bA * ce.a0 + bB * ce.a1;
-        const int Dg1 = gA * ce.a0 + gB * ce.a1;
-        const int Dr1 = rA * ce.a0 + rB * ce.a1;
+        tap<FMT>(buf, re.y0, re.c0, re.c0 + vdelta, ce.oY0, ce.oC0, bA, gA, rA);
+        tap<FMT>(buf, re.y0, re.c0, re.c0 + vdelta, ce.oY1, ce.oC1, bB, gB, rB);
+        const int Db0 = __mul24(bA, ce.a0) + __mul24(bB, ce.a1);
+        const int Dg0 = __mul24(gA, ce.a0) + __mul24(gB, ce.a1);
+        const int Dr0 = __mul24(rA, ce.a0) + __mul24(rB, ce.a1);
+        tap<FMT>(buf, re.y1, re.c1, re.c1 + vdelta, ce.oY0, ce.oC0, bA, gA, rA);
+        tap<FMT>(buf, re.y1, re.c1, re.c1 + vdelta, ce.oY1, ce.oC1, bB, gB, rB);
+        const int Db1 = __mul24(bA, ce.a0) + __mul24(bB, ce.a1);
+        const int Dg1 = __mul24(gA, ce.a0) + __mul24(gB, ce.a1);
+        const int Dr1 = __mul24(rA, ce.a0) + __mul24(rB, ce.a1);
         const int vb = vresize(Db0, Db1, re.b0, re.b1);
         const int vg = vresize(Dg0, Dg1, re.b0, re.b1);
         const int vr = vresize(Dr0, Dr1, re.b0, re.b1);
@@ -359,6 +390,54 @@ __global__ __launch_bounds__(kThreads) void evam_pp_kernel(const KParams P) {
             store_px<OUT>(P, lut_s, base, plane, vr, vg, vb);
         else
             store_px<OUT>(P, lut_s, base, plane, vb, vg, vr);
+    }
+}
+
+// Persistent, software-pipelined kernel: workgroup g processes tiles g, g + G, g + 2G, ... While it
+// converts tile t out of staging buffer b, the LDS-DMA loads of tile t + G are in flight into buffer
+// b ^ 1, and the next tables are computed before the wait. A grid of one workgroup per tile
+// (G = n_tiles) degenerates to load -> wait -> compute.
+template <int FMT, int OUT>
+__global__ __launch_bounds__(kThreads) void evam_pp_kernel(const KParams P) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const float* lut_s = reinterpret_cast<const float*>(smem);
+    if constexpr (OUT == 1) {
+        float* l = reinterpret_cast<float*>(smem);
+        for (int i = threadIdx.x; i < 768; i += kThreads) l[i] = P.lut[i];
+    }
+    int t = blockIdx.x;
+    if (t >= P.n_tiles) return;
+    uint8_t* const tab0 = smem + P.offTab;
+    uint8_t* const tab1 = tab0 + P.tab_bytes;
+    uint8_t* const buf0 = smem + P.offBuf;
+    uint8_t* const buf1 = buf0 + P.buf_bytes;
+
+    TileInfo cur;
+    setup_tile<FMT>(P, t, tab0, cur);
+    __syncthreads();
+    if (cur.active) issue_tile<FMT>(P, cur, tab0, buf0);
+    int b = 0;
+    for (;;) {
+        const int tn = t + (int)gridDim.x;
+        const bool has_next = tn < P.n_tiles;
+        uint8_t* tab_c = b ? tab1 : tab0;
+        uint8_t* buf_c = b ? buf1 : buf0;
+        uint8_t* tab_n = b ? tab0 : tab1;
+        uint8_t* buf_n = b ? buf0 : buf1;
+        TileInfo nxt;
+        if (has_next) setup_tile<FMT>(P, tn, tab_n, nxt);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA into buf_c has landed
+        __syncthreads();                                   // ... and every other wave's; tab_n visible
+        if (has_next && nxt.active) issue_tile<FMT>(P, nxt, tab_n, buf_n);
+        compute_tile<FMT, OUT>(P, cur, tab_c, buf_c, lut_s);
+        if (!has_next) break;
+        // WAR guard for tab_c / buf_c (rewritten next iteration). A raw barrier: the DMA into buf_n
+        // stays in flight across it.
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        t = tn;
+        cur = nxt;
+        b ^= 1;
     }
 }
 
@@ -489,38 +568,36 @@ int64_t item_src_bytes(int f, const Geom& g, int DW, int DH) {
 }
 
 struct TileCfg {
-    int TW, TH, strideY, strideC, lds, offRow, offSlot, offLut, offY, offC, offV;
+    int TW, TH, strideY, strideC, tab_bytes, buf_bytes, offTab, offBuf, lds;
 };
 
-// Tile shape: ~1024 output pixels per 256-thread workgroup, shrunk until the staged footprint fits.
+int env_int(const char* name, int dflt) {
+    const char* v = getenv(name);
+    return (v && *v) ? atoi(v) : dflt;
+}
+
+// Tile shape: TW x TH output pixels per 256-thread workgroup iteration (~512 by default), shrunk until
+// two table sets + two staging buffers fit the LDS budget. EVAM_PP_TW / EVAM_PP_TH override (tuning).
 TileCfg choose_tiles(int f, int DW, int DH, double max_ratio_x, int out_dtype) {
     TileCfg t{};
     if (DW <= 256) t.TW = DW;
     else if (DW % 128 == 0) t.TW = 128;
     else if (DW % 64 == 0) t.TW = 64;
     else t.TW = 128;
-    t.TH = std::max(1, std::min(DH, 1024 / t.TW));
+    t.TH = std::max(1, std::min(DH, 512 / t.TW));
+    t.TW = std::max(1, std::min(DW, env_int("EVAM_PP_TW", t.TW)));
+    t.TH = std::max(1, std::min(DH, env_int("EVAM_PP_TH", t.TH)));
     const int bpp = fmt_bpp(f);
+    const int nC = f == kNV12 ? 1 : (f == kI420 ? 2 : 0);
     for (;;) {
-        const int span = (int)std::ceil((t.TW - 1) * max_ratio_x) + 4;  // source columns
+        const int span = (int)std::ceil((t.TW - 1) * max_ratio_x) + 4;  // source columns touched, upper bound
         t.strideY = ((span * bpp + 32) + 15) & ~15;
         t.strideC = f == kNV12 ? ((span + 2 + 32 + 15) & ~15) : (f == kI420 ? ((span / 2 + 2 + 32 + 15) & ~15) : 0);
-        const int nC = f == kNV12 ? 1 : (f == kI420 ? 2 : 0);
-        int off = ((int)sizeof(ColEntry) * t.TW + 15) & ~15;
-        t.offRow = off;
-        off += (int)sizeof(RowEntry) * t.TH;
-        t.offSlot = off;
-        off += 4 * 4 * t.TH;
-        off = (off + 15) & ~15;
-        t.offLut = off;
-        if (out_dtype == EVAM_DTYPE_F32) off += kLutBytes;
-        t.offY = off;
-        off += 2 * t.TH * t.strideY;
-        t.offC = off;
-        off += 2 * t.TH * t.strideC;
-        t.offV = off;
-        if (nC == 2) off += 2 * t.TH * t.strideC;
-        t.lds = off;
+        t.tab_bytes = ((int)sizeof(ColEntry) * t.TW + (int)sizeof(RowEntry) * t.TH + 16 * t.TH + 15) & ~15;
+        t.buf_bytes = 2 * t.TH * (t.strideY + nC * t.strideC);
+        t.offTab = out_dtype == EVAM_DTYPE_F32 ? kLutBytes : 0;
+        t.offBuf = t.offTab + 2 * t.tab_bytes;
+        t.lds = t.offBuf + 2 * t.buf_bytes;
         if (t.lds <= kLdsBudget) break;
         if (t.TH > 1) t.TH = std::max(1, t.TH / 2);
         else if (t.TW > 16) t.TW = std::max(16, t.TW / 2);
@@ -552,6 +629,7 @@ hipError_t launch(int f, int out, const KParams& p, int grid, int lds, hipStream
 
 struct evam_pp {
     int device = 0;
+    int n_cu = 256;
     hipStream_t stream = nullptr;
     int opt_stats = 0, opt_timing = 0;
     evam_pp_stats stats{};
@@ -581,6 +659,8 @@ int evam_pp_create(int hip_device, void* hip_stream, evam_pp** out) {
     evam_pp* h = new (std::nothrow) evam_pp();
     if (!h) return fail(EVAM_PP_ERR_OOM, "evam_pp_create: out of host memory");
     h->device = hip_device;
+    if (hipDeviceGetAttribute(&h->n_cu, hipDeviceAttributeMultiprocessorCount, hip_device) != hipSuccess || h->n_cu <= 0)
+        h->n_cu = 256;
     h->stream = reinterpret_cast<hipStream_t>(hip_stream);
     if (hipEventCreate(&h->ev0) != hipSuccess || hipEventCreate(&h->ev1) != hipSuccess) {
         delete h;
@@ -782,14 +862,18 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
         p.tiles_x = (DW + t.TW - 1) / t.TW;
         const int tiles_y = (DH + t.TH - 1) / t.TH;
         p.tiles_per_item = p.tiles_x * tiles_y;
+        const int64_t n_tiles = (int64_t)count[f] * p.tiles_per_item;
+        if (n_tiles > 0x7FFFFFFF) return fail(EVAM_PP_ERR_INVALID_ARG, "evam_pp_run: too many tiles");
+        p.n_tiles = (int)n_tiles;
         p.tw_magic = (uint32_t)(0xFFFFFFFFu / (uint32_t)t.TW) + 1u;
-        p.strideY = t.strideY; p.strideC = t.strideC;
-        p.offRow = t.offRow; p.offSlot = t.offSlot; p.offLut = t.offLut;
-        p.offY = t.offY; p.offC = t.offC; p.offV = t.offV;
+        p.tab_bytes = t.tab_bytes; p.buf_bytes = t.buf_bytes;
+        p.offTab = t.offTab; p.offBuf = t.offBuf;
         p.color_rgb = cfg->color_order == EVAM_COLOR_RGB;
         p.fill = (uint32_t)cfg->fill[0] | ((uint32_t)cfg->fill[1] << 8) | ((uint32_t)cfg->fill[2] << 16);
-        const int64_t grid = (int64_t)count[f] * p.tiles_per_item;
-        if (grid > 0x7FFFFFFF) return fail(EVAM_PP_ERR_INVALID_ARG, "evam_pp_run: grid too large");
+        // Persistent grid: every resident workgroup slot gets a strided share of the tiles.
+        // EVAM_PP_WGS_PER_CU=0 launches one workgroup per tile instead (no cross-tile prefetch).
+        const int per_cu = env_int("EVAM_PP_WGS_PER_CU", std::max(1, std::min(8, (160 * 1024) / std::max(t.lds, 1))));
+        int64_t grid = per_cu > 0 ? std::min<int64_t>(n_tiles, (int64_t)h->n_cu * per_cu) : n_tiles;
         if (t.lds > 64 * 1024) {
             hipError_t e = hipSuccess;
             switch (f * 2 + cfg->out_dtype) {
