@@ -38,7 +38,9 @@ namespace {
 // ------------------------------------------------------------------------------------------------
 // constants
 // ------------------------------------------------------------------------------------------------
-constexpr int kThreads = 256;
+constexpr int kLoaderThreads = 64;   // wave 0: tables + LDS-DMA
+constexpr int kConsumers = 256;      // waves 1..4: convert + store
+constexpr int kBlock = kLoaderThreads + kConsumers;
 constexpr int kLutBytes = 3 * 256 * 4;
 constexpr int kLdsBudget = 48 * 1024;
 
@@ -77,6 +79,7 @@ struct KParams {
     int offTab, offBuf; // LDS carve: LUT at 0 (fp32 out), 2 table sets at offTab, 2 buffers at offBuf
     int color_rgb;
     uint32_t fill;      // packed u8 fill, output channel order
+    int ablate;         // diagnostics only (EVAM_PP_ABLATE bits): 1 no DMA, 2 no pixel math, 4 no stores
 };
 
 struct ColEntry {  // 16 B, one per tile column
@@ -186,15 +189,20 @@ __device__ __forceinline__ void glds16(const uint8_t* g, uint8_t* lds_wave_base)
 // wave's 64 chunks form one contiguous 1 KiB LDS run, as LDS-DMA requires. Skipped slots (row < 0:
 // duplicate or invisible rows) issue nothing.
 __device__ __forceinline__ void issue_plane(uint8_t* lds_plane, const int32_t* __restrict__ slot_rows, int n_slots,
-                                            const uint8_t* __restrict__ plane, int pitch, int fs, int cpr, int tid) {
+                                            const uint8_t* __restrict__ plane, int pitch, int fs, int cpr, int tid,
+                                            int nthr) {
     if (cpr <= 0) return;
-    const uint32_t magic = 0xFFFFFFFFu / (uint32_t)cpr + 1u;
+    // c / cpr: shift for powers of two (cpr == 1 included: its magic number would overflow to 0),
+    // else the round-up reciprocal (exact for c * cpr < 2^32).
+    const bool pow2 = (cpr & (cpr - 1)) == 0;
+    const int sh = __builtin_ctz((unsigned)cpr);
+    const uint32_t magic = pow2 ? 0u : 0xFFFFFFFFu / (uint32_t)cpr + 1u;
     const int total = n_slots * cpr;
     const int wave_off = tid & ~63;
-    for (int c0 = 0; c0 < total; c0 += kThreads) {
+    for (int c0 = 0; c0 < total; c0 += nthr) {
         const int c = c0 + tid;
         if (c < total) {
-            const int slot = (int)umulhi((uint32_t)c, magic);
+            const int slot = pow2 ? (c >> sh) : (int)umulhi((uint32_t)c, magic);
             const int col = c - slot * cpr;
             const int row = slot_rows[slot];
             if (row >= 0)
@@ -219,11 +227,25 @@ __device__ __forceinline__ void store_px(const KParams& P, const float* __restri
     }
 }
 
-// Tile geometry, footprint and coefficient tables (written to the table set `tab`).
+// Per-tile values the consumer waves read from the table set header (written by the loader).
+struct TileHdr {
+    int X0, Y0, X1, Y1;
+    int active, offC, offV, slot;
+};
+constexpr int kHdrBytes = (int)sizeof(TileHdr);
+
+__device__ __forceinline__ ColEntry* tab_cols(uint8_t* tab) { return reinterpret_cast<ColEntry*>(tab + kHdrBytes); }
+__device__ __forceinline__ RowEntry* tab_rows(uint8_t* tab, const KParams& P) {
+    return reinterpret_cast<RowEntry*>(tab + kHdrBytes + P.TW * (int)sizeof(ColEntry));
+}
+__device__ __forceinline__ int32_t* tab_slots(uint8_t* tab, const KParams& P) {
+    return reinterpret_cast<int32_t*>(tab + kHdrBytes + P.TW * (int)sizeof(ColEntry) + P.TH * (int)sizeof(RowEntry));
+}
+
+// Tile geometry, footprint and coefficient tables, written to the table set `tab` by `nthr` threads.
 template <int FMT>
-__device__ __forceinline__ void setup_tile(const KParams& P, int t, uint8_t* tab, TileInfo& ti) {
+__device__ __forceinline__ void setup_tile(const KParams& P, int t, uint8_t* tab, TileInfo& ti, int tid, int nthr) {
     using T = FmtTraits<FMT>;
-    const int tid = threadIdx.x;
     const int item = t / P.tiles_per_item;
     const int tile = t - item * P.tiles_per_item;
     const int ty = tile / P.tiles_x;
@@ -248,31 +270,37 @@ __device__ __forceinline__ void setup_tile(const KParams& P, int t, uint8_t* tab
     const int dy_lo = max(ti.Y0 - oy, 0), dy_hi = min(ti.Y1 - oy, rh) - 1;
     ti.active = dx_lo <= dx_hi && dy_lo <= dy_hi;
     ti.fsY = ti.cprY = ti.fsC = ti.cprC = ti.offC = ti.offV = 0;
-    if (!ti.active) return;
-
-    int sxa, sxb, cd0, cd1;
-    linear_coef(dx_lo, scx, cw, true, sxa, cd0, cd1);
-    linear_coef(dx_hi, scx, cw, true, sxb, cd0, cd1);
-    const int xa = x0 + sxa;                      // first source column touched
-    const int xb = x0 + min(sxb + 1, cw - 1);     // last source column touched
-    ti.fsY = (xa * T::bpp) & ~15;
-    ti.cprY = (((xb * T::bpp + T::bpp + 15) & ~15) - ti.fsY) >> 4;
-    if constexpr (FMT == kNV12) {
-        ti.fsC = (2 * (xa >> 1)) & ~15;
-        ti.cprC = (((2 * (xb >> 1) + 2 + 15) & ~15) - ti.fsC) >> 4;
-    } else if constexpr (FMT == kI420) {
-        ti.fsC = (xa >> 1) & ~15;
-        ti.cprC = ((((xb >> 1) + 1 + 15) & ~15) - ti.fsC) >> 4;
+    if (ti.active) {
+        int sxa, sxb, cd0, cd1;
+        linear_coef(dx_lo, scx, cw, true, sxa, cd0, cd1);
+        linear_coef(dx_hi, scx, cw, true, sxb, cd0, cd1);
+        const int xa = x0 + sxa;                      // first source column touched
+        const int xb = x0 + min(sxb + 1, cw - 1);     // last source column touched
+        ti.fsY = (xa * T::bpp) & ~15;
+        ti.cprY = (((xb * T::bpp + T::bpp + 15) & ~15) - ti.fsY) >> 4;
+        if constexpr (FMT == kNV12) {
+            ti.fsC = (2 * (xa >> 1)) & ~15;
+            ti.cprC = (((2 * (xb >> 1) + 2 + 15) & ~15) - ti.fsC) >> 4;
+        } else if constexpr (FMT == kI420) {
+            ti.fsC = (xa >> 1) & ~15;
+            ti.cprC = ((((xb >> 1) + 1 + 15) & ~15) - ti.fsC) >> 4;
+        }
+        ti.offC = 2 * P.TH * ti.cprY * 16;
+        ti.offV = ti.offC + 2 * P.TH * ti.cprC * 16;
     }
+    if (tid == 0) {
+        TileHdr h;
+        h.X0 = ti.X0; h.Y0 = ti.Y0; h.X1 = ti.X1; h.Y1 = ti.Y1;
+        h.active = ti.active; h.offC = ti.offC; h.offV = ti.offV; h.slot = ti.slot;
+        *reinterpret_cast<TileHdr*>(tab) = h;
+    }
+    if (!ti.active) return;
     const int fwY = ti.cprY * 16, fwC = ti.cprC * 16;
-    ti.offC = 2 * P.TH * fwY;
-    ti.offV = ti.offC + 2 * P.TH * fwC;
-
-    ColEntry* coltab = reinterpret_cast<ColEntry*>(tab);
-    RowEntry* rowtab = reinterpret_cast<RowEntry*>(tab + P.TW * (int)sizeof(ColEntry));
-    int32_t* slotY = reinterpret_cast<int32_t*>(tab + P.TW * (int)sizeof(ColEntry) + P.TH * (int)sizeof(RowEntry));
+    ColEntry* coltab = tab_cols(tab);
+    RowEntry* rowtab = tab_rows(tab, P);
+    int32_t* slotY = tab_slots(tab, P);
     int32_t* slotC = slotY + 2 * P.TH;
-    for (int lx = tid; lx < P.TW; lx += kThreads) {
+    for (int lx = tid; lx < P.TW; lx += nthr) {
         ColEntry e;
         const int dx = ti.X0 + lx - ox;
         if (ti.X0 + lx < ti.X1 && dx >= 0 && dx < rw) {
@@ -296,7 +324,7 @@ __device__ __forceinline__ void setup_tile(const KParams& P, int t, uint8_t* tab
         e.pad0 = 0; e.pad1 = 0;
         coltab[lx] = e;
     }
-    for (int ly = tid; ly < P.TH; ly += kThreads) {
+    for (int ly = tid; ly < P.TH; ly += nthr) {
         RowEntry e;
         const int dy = ti.Y0 + ly - oy;
         int ya = -1, yb = -1, ca = -1, cb = -1;
@@ -332,38 +360,38 @@ __device__ __forceinline__ void setup_tile(const KParams& P, int t, uint8_t* tab
 }
 
 template <int FMT>
-__device__ __forceinline__ void issue_tile(const KParams& P, const TileInfo& ti, const uint8_t* tab, uint8_t* buf) {
+__device__ __forceinline__ void issue_tile(const KParams& P, const TileInfo& ti, uint8_t* tab, uint8_t* buf,
+                                           int tid, int nthr) {
     using T = FmtTraits<FMT>;
-    const int tid = threadIdx.x;
-    const int32_t* slotY = reinterpret_cast<const int32_t*>(tab + P.TW * (int)sizeof(ColEntry) + P.TH * (int)sizeof(RowEntry));
+    const int32_t* slotY = tab_slots(tab, P);
     const int32_t* slotC = slotY + 2 * P.TH;
-    issue_plane(buf, slotY, 2 * P.TH, ti.plane[0], ti.pitch[0], ti.fsY, ti.cprY, tid);
+    issue_plane(buf, slotY, 2 * P.TH, ti.plane[0], ti.pitch[0], ti.fsY, ti.cprY, tid, nthr);
     if constexpr (T::nchroma >= 1)
-        issue_plane(buf + ti.offC, slotC, 2 * P.TH, ti.plane[1], ti.pitch[1], ti.fsC, ti.cprC, tid);
+        issue_plane(buf + ti.offC, slotC, 2 * P.TH, ti.plane[1], ti.pitch[1], ti.fsC, ti.cprC, tid, nthr);
     if constexpr (T::nchroma == 2)
-        issue_plane(buf + ti.offV, slotC, 2 * P.TH, ti.plane[2], ti.pitch[2], ti.fsC, ti.cprC, tid);
+        issue_plane(buf + ti.offV, slotC, 2 * P.TH, ti.plane[2], ti.pitch[2], ti.fsC, ti.cprC, tid, nthr);
 }
 
-// Convert + resize + normalise + planar store of one tile from its staged footprint.
+// Convert + resize + normalise + planar store of one tile from its staged footprint (kConsumers threads).
 template <int FMT, int OUT>
-__device__ __forceinline__ void compute_tile(const KParams& P, const TileInfo& ti, const uint8_t* tab,
-                                             const uint8_t* buf, const float* lut_s) {
-    const int tid = threadIdx.x;
+__device__ __forceinline__ void compute_tile(const KParams& P, uint8_t* tab, const uint8_t* buf,
+                                             const float* lut_s, int tid) {
+    const TileHdr hd = *reinterpret_cast<const TileHdr*>(tab);
     const size_t plane = (size_t)P.DW * P.DH;
-    const size_t slot_base = (size_t)ti.slot * 3 * plane;
+    const size_t slot_base = (size_t)hd.slot * 3 * plane;
     const int npx = P.TW * P.TH;
     const int f0 = P.fill & 0xFF, f1 = (P.fill >> 8) & 0xFF, f2 = (P.fill >> 16) & 0xFF;
-    const ColEntry* coltab = reinterpret_cast<const ColEntry*>(tab);
-    const RowEntry* rowtab = reinterpret_cast<const RowEntry*>(tab + P.TW * (int)sizeof(ColEntry));
-    const int vdelta = ti.offV - ti.offC;
-    for (int p = tid; p < npx; p += kThreads) {
-        const int ly = (int)umulhi((uint32_t)p, P.tw_magic);
+    const ColEntry* coltab = tab_cols(tab);
+    const RowEntry* rowtab = tab_rows(tab, P);
+    const int vdelta = hd.offV - hd.offC;
+    for (int p = tid; p < npx; p += kConsumers) {
+        const int ly = P.TW == 1 ? p : (int)umulhi((uint32_t)p, P.tw_magic);  // p / TW
         const int lx = p - ly * P.TW;
-        const int X = ti.X0 + lx, Y = ti.Y0 + ly;
-        if (X >= ti.X1 || Y >= ti.Y1) continue;
+        const int X = hd.X0 + lx, Y = hd.Y0 + ly;
+        if (X >= hd.X1 || Y >= hd.Y1) continue;
         const size_t base = slot_base + (size_t)Y * P.DW + X;
-        if (!ti.active) {
-            store_px<OUT>(P, lut_s, base, plane, f0, f1, f2);
+        if (!hd.active || (P.ablate & 2)) {
+            if (!(P.ablate & 4)) store_px<OUT>(P, lut_s, base, plane, f0, f1, f2);
             continue;
         }
         const ColEntry ce = coltab[lx];
@@ -386,6 +414,10 @@ __device__ __forceinline__ void compute_tile(const KParams& P, const TileInfo& t
         const int vb = vresize(Db0, Db1, re.b0, re.b1);
         const int vg = vresize(Dg0, Dg1, re.b0, re.b1);
         const int vr = vresize(Dr0, Dr1, re.b0, re.b1);
+        if (P.ablate & 4) {
+            asm volatile("" :: "v"(vb), "v"(vg), "v"(vr));  // keep the math alive
+            continue;
+        }
         if (P.color_rgb)
             store_px<OUT>(P, lut_s, base, plane, vr, vg, vb);
         else
@@ -393,50 +425,56 @@ __device__ __forceinline__ void compute_tile(const KParams& P, const TileInfo& t
     }
 }
 
-// Persistent, software-pipelined kernel: workgroup g processes tiles g, g + G, g + 2G, ... While it
-// converts tile t out of staging buffer b, the LDS-DMA loads of tile t + G are in flight into buffer
-// b ^ 1, and the next tables are computed before the wait. A grid of one workgroup per tile
-// (G = n_tiles) degenerates to load -> wait -> compute.
+// Persistent loader/consumer kernel. Wave 0 is the loader: it builds the tables of tile t + G and
+// streams its source footprint into the other staging buffer by LDS-DMA, then waits only for its own
+// DMA (it never stores). Waves 1..4 are consumers: they convert tile t and store it, and never wait for
+// their stores. One raw s_barrier per tile hands buffer and tables over. Workgroup g processes tiles
+// g, g + G, g + 2G, ...; a grid of one workgroup per tile degenerates to load -> barrier -> compute.
 template <int FMT, int OUT>
-__global__ __launch_bounds__(kThreads) void evam_pp_kernel(const KParams P) {
+__global__ __launch_bounds__(kBlock) void evam_pp_kernel(const KParams P) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int tid = threadIdx.x;
+    const bool loader = __builtin_amdgcn_readfirstlane(tid >> 6) == 0;  // wave 0, provably wave-uniform
     const float* lut_s = reinterpret_cast<const float*>(smem);
-    if constexpr (OUT == 1) {
-        float* l = reinterpret_cast<float*>(smem);
-        for (int i = threadIdx.x; i < 768; i += kThreads) l[i] = P.lut[i];
-    }
     int t = blockIdx.x;
     if (t >= P.n_tiles) return;
     uint8_t* const tab0 = smem + P.offTab;
     uint8_t* const tab1 = tab0 + P.tab_bytes;
     uint8_t* const buf0 = smem + P.offBuf;
     uint8_t* const buf1 = buf0 + P.buf_bytes;
-
-    TileInfo cur;
-    setup_tile<FMT>(P, t, tab0, cur);
-    __syncthreads();
-    if (cur.active) issue_tile<FMT>(P, cur, tab0, buf0);
+    if (loader) {
+        TileInfo ti;
+        setup_tile<FMT>(P, t, tab0, ti, tid, kLoaderThreads);
+        if (ti.active && !(P.ablate & 1)) issue_tile<FMT>(P, ti, tab0, buf0, tid, kLoaderThreads);
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    } else {
+        if constexpr (OUT == 1) {
+            float* l = reinterpret_cast<float*>(smem);
+            for (int i = tid - kLoaderThreads; i < 768; i += kConsumers) l[i] = P.lut[i];
+        }
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
     int b = 0;
     for (;;) {
         const int tn = t + (int)gridDim.x;
         const bool has_next = tn < P.n_tiles;
-        uint8_t* tab_c = b ? tab1 : tab0;
-        uint8_t* buf_c = b ? buf1 : buf0;
-        uint8_t* tab_n = b ? tab0 : tab1;
-        uint8_t* buf_n = b ? buf0 : buf1;
-        TileInfo nxt;
-        if (has_next) setup_tile<FMT>(P, tn, tab_n, nxt);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA into buf_c has landed
-        __syncthreads();                                   // ... and every other wave's; tab_n visible
-        if (has_next && nxt.active) issue_tile<FMT>(P, nxt, tab_n, buf_n);
-        compute_tile<FMT, OUT>(P, cur, tab_c, buf_c, lut_s);
+        if (loader) {
+            if (has_next) {
+                uint8_t* tab_n = b ? tab0 : tab1;
+                uint8_t* buf_n = b ? buf0 : buf1;
+                TileInfo ti;
+                setup_tile<FMT>(P, tn, tab_n, ti, tid, kLoaderThreads);
+                if (ti.active && !(P.ablate & 1)) issue_tile<FMT>(P, ti, tab_n, buf_n, tid, kLoaderThreads);
+                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // own DMA + table writes
+            }
+        } else {
+            compute_tile<FMT, OUT>(P, b ? tab1 : tab0, b ? buf1 : buf0, lut_s, tid - kLoaderThreads);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads of tab/buf done; stores stay in flight
+        }
         if (!has_next) break;
-        // WAR guard for tab_c / buf_c (rewritten next iteration). A raw barrier: the DMA into buf_n
-        // stays in flight across it.
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         t = tn;
-        cur = nxt;
         b ^= 1;
     }
 }
@@ -593,7 +631,7 @@ TileCfg choose_tiles(int f, int DW, int DH, double max_ratio_x, int out_dtype) {
         const int span = (int)std::ceil((t.TW - 1) * max_ratio_x) + 4;  // source columns touched, upper bound
         t.strideY = ((span * bpp + 32) + 15) & ~15;
         t.strideC = f == kNV12 ? ((span + 2 + 32 + 15) & ~15) : (f == kI420 ? ((span / 2 + 2 + 32 + 15) & ~15) : 0);
-        t.tab_bytes = ((int)sizeof(ColEntry) * t.TW + (int)sizeof(RowEntry) * t.TH + 16 * t.TH + 15) & ~15;
+        t.tab_bytes = (32 + (int)sizeof(ColEntry) * t.TW + (int)sizeof(RowEntry) * t.TH + 16 * t.TH + 15) & ~15;
         t.buf_bytes = 2 * t.TH * (t.strideY + nC * t.strideC);
         t.offTab = out_dtype == EVAM_DTYPE_F32 ? kLutBytes : 0;
         t.offBuf = t.offTab + 2 * t.tab_bytes;
@@ -608,7 +646,7 @@ TileCfg choose_tiles(int f, int DW, int DH, double max_ratio_x, int out_dtype) {
 
 template <int FMT, int OUT>
 hipError_t launch_t(const KParams& p, int grid, int lds, hipStream_t s) {
-    hipLaunchKernelGGL((evam_pp_kernel<FMT, OUT>), dim3(grid), dim3(kThreads), lds, s, p);
+    hipLaunchKernelGGL((evam_pp_kernel<FMT, OUT>), dim3(grid), dim3(kBlock), lds, s, p);
     return hipGetLastError();
 }
 
@@ -865,26 +903,36 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
         const int64_t n_tiles = (int64_t)count[f] * p.tiles_per_item;
         if (n_tiles > 0x7FFFFFFF) return fail(EVAM_PP_ERR_INVALID_ARG, "evam_pp_run: too many tiles");
         p.n_tiles = (int)n_tiles;
-        p.tw_magic = (uint32_t)(0xFFFFFFFFu / (uint32_t)t.TW) + 1u;
+        p.tw_magic = t.TW > 1 ? (uint32_t)(0xFFFFFFFFu / (uint32_t)t.TW) + 1u : 0u;
         p.tab_bytes = t.tab_bytes; p.buf_bytes = t.buf_bytes;
         p.offTab = t.offTab; p.offBuf = t.offBuf;
         p.color_rgb = cfg->color_order == EVAM_COLOR_RGB;
+        p.ablate = env_int("EVAM_PP_ABLATE", 0);
         p.fill = (uint32_t)cfg->fill[0] | ((uint32_t)cfg->fill[1] << 8) | ((uint32_t)cfg->fill[2] << 16);
         // Persistent grid: every resident workgroup slot gets a strided share of the tiles.
         // EVAM_PP_WGS_PER_CU=0 launches one workgroup per tile instead (no cross-tile prefetch).
-        const int per_cu = env_int("EVAM_PP_WGS_PER_CU", std::max(1, std::min(8, (160 * 1024) / std::max(t.lds, 1))));
+        // Default: persistent, as many workgroups per CU as LDS and the 32-wave limit allow.
+        const int per_cu = env_int("EVAM_PP_WGS_PER_CU",
+                                   std::max(1, std::min(32 / (kBlock / 64), (160 * 1024) / std::max(t.lds, 1))));
         int64_t grid = per_cu > 0 ? std::min<int64_t>(n_tiles, (int64_t)h->n_cu * per_cu) : n_tiles;
-        if (t.lds > 64 * 1024) {
+        int lds = t.lds;
+        if (grid == n_tiles) {
+            // One tile per workgroup: no prefetch, so one table set + one buffer; the smaller LDS
+            // footprint buys occupancy (latency hiding across workgroups instead of inside one).
+            p.offBuf = t.offTab + t.tab_bytes;
+            lds = p.offBuf + t.buf_bytes;
+        }
+        if (lds > 64 * 1024) {
             hipError_t e = hipSuccess;
             switch (f * 2 + cfg->out_dtype) {
-#define SETATTR(F, O) case F * 2 + O: e = hipFuncSetAttribute((const void*)evam_pp_kernel<F, O>, hipFuncAttributeMaxDynamicSharedMemorySize, t.lds); break;
+#define SETATTR(F, O) case F * 2 + O: e = hipFuncSetAttribute((const void*)evam_pp_kernel<F, O>, hipFuncAttributeMaxDynamicSharedMemorySize, lds); break;
                 SETATTR(kNV12, 0) SETATTR(kNV12, 1) SETATTR(kI420, 0) SETATTR(kI420, 1)
                 SETATTR(kBGRX, 0) SETATTR(kBGRX, 1) SETATTR(kBGR, 0) SETATTR(kBGR, 1)
 #undef SETATTR
             }
             if (e != hipSuccess) return fail(EVAM_PP_ERR_HIP, "hipFuncSetAttribute: %s", hipGetErrorString(e));
         }
-        hipError_t e = launch(f, cfg->out_dtype, p, (int)grid, t.lds, h->stream);
+        hipError_t e = launch(f, cfg->out_dtype, p, (int)grid, lds, h->stream);
         if (e != hipSuccess) return fail(EVAM_PP_ERR_HIP, "kernel launch failed: %s", hipGetErrorString(e));
         launches++;
     }

@@ -78,7 +78,8 @@ def assert_same(got, ref, what=""):
 
 @pytest.mark.parametrize("fmt", FORMATS)
 @pytest.mark.parametrize("src,dst", [((64, 48), (512, 512)), ((66, 50), (33, 17)), ((160, 90), (72, 72)),
-                                     ((320, 180), (160, 90)), ((96, 64), (96, 64)), ((200, 120), (300, 70))])
+                                     ((320, 180), (160, 90)), ((96, 64), (96, 64)), ((200, 120), (300, 70)),
+                                     ((64, 48), (1, 1)), ((64, 48), (1, 37)), ((2, 2), (40, 3)), ((1920, 1080), (3, 2))])
 @pytest.mark.parametrize("dtype", ["u8", "f32"])
 def test_full_frame(evam, O, coracle, gpu, fmt, src, dst, dtype):
     import torch
