@@ -129,7 +129,7 @@ def load_library(path: str | None = None) -> ctypes.CDLL:
         return _LIB
     import torch  # noqa: F401  (binds the library to torch's HIP runtime; see module docstring)
 
-    p = path or LIB_PATH
+    p = path or os.environ.get("EVAM_PP_LIB") or LIB_PATH  # EVAM_PP_LIB: A/B a variant build
     if not os.path.exists(p):
         raise RuntimeError(
             f"{LIB_NAME} is not built at {p}: run `python -c 'import __graft_entry__ as g; g.build()'` "

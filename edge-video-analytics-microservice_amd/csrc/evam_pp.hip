@@ -38,11 +38,12 @@ namespace {
 // ------------------------------------------------------------------------------------------------
 // constants
 // ------------------------------------------------------------------------------------------------
-constexpr int kLoaderThreads = 64;   // wave 0: tables + LDS-DMA
-constexpr int kConsumers = 256;      // waves 1..4: convert + store
-constexpr int kBlock = kLoaderThreads + kConsumers;
+constexpr int kThreads = 256;
+#ifndef EVAM_PP_UNROLL
+#define EVAM_PP_UNROLL 1
+#endif
+constexpr int kUnroll = EVAM_PP_UNROLL;  // pixels per lane whose loads are issued together
 constexpr int kLutBytes = 3 * 256 * 4;
-constexpr int kLdsBudget = 48 * 1024;
 
 // OpenCV color_yuv.simd.hpp ITUR_BT_601_*; the -128 chroma bias is folded into the constants.
 constexpr int kCY = 1220542, kCUB = 2116026, kCUG = -409993, kCVG = -852492, kCVR = 1673527;
@@ -73,39 +74,25 @@ struct KParams {
     void* dst;
     int DW, DH;
     int TW, TH, tiles_x, tiles_per_item, n_tiles;
-    uint32_t tw_magic;  // ceil(2^32 / TW)
-    int tab_bytes;      // one table set: coltab | rowtab | slotY | slotC
-    int buf_bytes;      // one staging buffer (upper bound of a tile's packed footprint)
-    int offTab, offBuf; // LDS carve: LUT at 0 (fp32 out), 2 table sets at offTab, 2 buffers at offBuf
+    uint32_t tw_magic;  // ceil(2^32 / TW) (TW > 1)
+    int offCol, offRow; // LDS carve: LUT at 0 (fp32 out), column table, row table
     int color_rgb;
     uint32_t fill;      // packed u8 fill, output channel order
-    int ablate;         // diagnostics only (EVAM_PP_ABLATE bits): 1 no DMA, 2 no pixel math, 4 no stores
+    int ablate;         // diagnostics only (EVAM_PP_ABLATE bits): 2 no pixel math, 4 no stores
 };
 
-struct ColEntry {  // 16 B, one per tile column
-    int16_t oY0, oY1;  // byte offset of the two taps inside a staged luma/packed row (-1: not in image)
-    int16_t oC0, oC1;  // byte offset inside a staged chroma row (NV12: U of the UV pair)
-    int16_t a0, a1;    // 11-bit horizontal weights
-    int16_t pad0, pad1;
+// Per output column of a tile: absolute byte offsets of the two horizontal taps inside a source row.
+struct alignas(16) ColEntry {  // 16 B
+    int32_t oY0, oY1;  // luma / packed-pixel byte offsets of tap 0 / tap 1 (-1 in oY0: column shows padding)
+    int32_t oC0;       // chroma byte offset of tap 0 (NV12: U of the UV pair; I420: U/V plane column)
+    uint16_t a0, a1;   // 11-bit horizontal weights << 4 (see vresize)
 };
-
-struct RowEntry {  // 32 B, one per tile row
-    int32_t y0, y1;   // buffer byte offsets of the two staged luma rows (-1: row not in image)
-    int32_t c0, c1;   // buffer byte offsets of the two staged chroma rows
-    int32_t b0, b1;   // 11-bit vertical weights
+// Per output row of a tile: byte offsets of the two vertical taps' rows inside the planes.
+struct alignas(16) RowEntry {  // 32 B
+    int32_t y0, y1;   // row offsets in the luma / packed plane (-1 in y0: row shows padding)
+    int32_t c0, c1;   // row offsets in the chroma plane(s) (I420: same offset for U and V)
+    int32_t b0, b1;   // 11-bit vertical weights << 8 (see vresize)
     int32_t pad0, pad1;
-};
-
-// Per-tile values every lane holds (wave-uniform).
-struct TileInfo {
-    const uint8_t* plane[3];  // copied out of the descriptor during setup: no descriptor load may sit
-    int pitch[3];             // between the DMA issue and the compute (its vmcnt wait would drain the DMA)
-    int slot;
-    int X0, Y0, X1, Y1;
-    int active;        // the tile shows part of the resized image (else pure padding)
-    int fsY, cprY;     // luma/packed footprint: 16-B aligned start byte, 16-B chunks per row
-    int fsC, cprC;     // chroma footprint
-    int offC, offV;    // chroma / V plane offsets inside the staging buffer
 };
 
 // ------------------------------------------------------------------------------------------------
@@ -148,28 +135,17 @@ __device__ __forceinline__ void yuv_to_bgr(int Y, int U, int V, int& b, int& g, 
     r = clamp255((y + ruv) >> 20);
 }
 
-template <int FMT>
-__device__ __forceinline__ void tap(const uint8_t* __restrict__ buf, int yrow, int crow, int vrow, int oy,
-                                    int oc, int& b, int& g, int& r) {
-    if constexpr (FMT == kNV12) {
-        const int Y = buf[yrow + oy];
-        const uint32_t uv = *reinterpret_cast<const uint16_t*>(buf + crow + oc);
-        yuv_to_bgr(Y, uv & 0xFF, uv >> 8, b, g, r);
-    } else if constexpr (FMT == kI420) {
-        const int Y = buf[yrow + oy];
-        yuv_to_bgr(Y, buf[crow + oc], buf[vrow + oc], b, g, r);
-    } else if constexpr (FMT == kBGRX) {
-        const uint32_t p = *reinterpret_cast<const uint32_t*>(buf + yrow + oy);
-        b = p & 0xFF; g = (p >> 8) & 0xFF; r = (p >> 16) & 0xFF;
-    } else {
-        b = buf[yrow + oy]; g = buf[yrow + oy + 1]; r = buf[yrow + oy + 2];
-    }
+// VResizeLinear<uchar,int,short,FixedPtCast<int,uchar,22>,VResizeLinearVec_32s8u>:
+//   dst = (((b0 * (D0 >> 4)) >> 16) + ((b1 * (D1 >> 4)) >> 16) + 2) >> 2
+// evaluated on the full-rate 24-bit multiplier. The column table holds a' = a << 4 and the row table
+// b' = b << 8, so the horizontal pass yields D' = D << 4 (< 2^23) and
+//   (b * (D >> 4)) >> 16 == mulhi_u24(b', D' & ~0xFF)
+// exactly (b' * ((D >> 4) << 8) = b * (D >> 4) * 2^16).
+__device__ __forceinline__ uint32_t mulhi_u24(uint32_t a, uint32_t b) {
+    return (uint32_t)(((uint64_t)(a & 0xFFFFFFu) * (uint64_t)(b & 0xFFFFFFu)) >> 32);
 }
-
-// VResizeLinear<uchar,int,short,FixedPtCast<int,uchar,22>,VResizeLinearVec_32s8u>.
-// D >> 4 <= 32655 and |b| <= 2048, so both products are exact on the 24-bit multiplier.
-__device__ __forceinline__ int vresize(int D0, int D1, int b0, int b1) {
-    return ((__mul24(b0, D0 >> 4) >> 16) + (__mul24(b1, D1 >> 4) >> 16) + 2) >> 2;
+__device__ __forceinline__ int vresize(uint32_t D0s, uint32_t D1s, uint32_t b0s, uint32_t b1s) {
+    return (int)((mulhi_u24(b0s, D0s & 0xFFFF00u) + mulhi_u24(b1s, D1s & 0xFFFF00u) + 2u) >> 2);
 }
 
 template <int FMT>
@@ -178,304 +154,211 @@ struct FmtTraits {
     static constexpr int nchroma = FMT == kNV12 ? 1 : (FMT == kI420 ? 2 : 0);
 };
 
-// One 16-byte LDS-DMA load: global -> LDS at (wave-uniform lds_base + lane * 16).
-__device__ __forceinline__ void glds16(const uint8_t* g, uint8_t* lds_wave_base) {
-    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
-                                     (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
-}
-
-// Issue the LDS-DMA loads of one plane's staged rows. Rows are packed back to back in the buffer
-// (row slot s at s * cpr * 16), so chunk c of the flattened (slot, column) space lands at c * 16 and a
-// wave's 64 chunks form one contiguous 1 KiB LDS run, as LDS-DMA requires. Skipped slots (row < 0:
-// duplicate or invisible rows) issue nothing.
-__device__ __forceinline__ void issue_plane(uint8_t* lds_plane, const int32_t* __restrict__ slot_rows, int n_slots,
-                                            const uint8_t* __restrict__ plane, int pitch, int fs, int cpr, int tid,
-                                            int nthr) {
-    if (cpr <= 0) return;
-    // c / cpr: shift for powers of two (cpr == 1 included: its magic number would overflow to 0),
-    // else the round-up reciprocal (exact for c * cpr < 2^32).
-    const bool pow2 = (cpr & (cpr - 1)) == 0;
-    const int sh = __builtin_ctz((unsigned)cpr);
-    const uint32_t magic = pow2 ? 0u : 0xFFFFFFFFu / (uint32_t)cpr + 1u;
-    const int total = n_slots * cpr;
-    const int wave_off = tid & ~63;
-    for (int c0 = 0; c0 < total; c0 += nthr) {
-        const int c = c0 + tid;
-        if (c < total) {
-            const int slot = pow2 ? (c >> sh) : (int)umulhi((uint32_t)c, magic);
-            const int col = c - slot * cpr;
-            const int row = slot_rows[slot];
-            if (row >= 0)
-                glds16(plane + (uint32_t)row * (uint32_t)pitch + fs + col * 16, lds_plane + (c0 + wave_off) * 16);
-        }
-    }
-}
-
-template <int OUT>
-__device__ __forceinline__ void store_px(const KParams& P, const float* __restrict__ lut, size_t base,
-                                         size_t plane, int v0, int v1, int v2) {
-    if constexpr (OUT == 0) {
-        uint8_t* d = reinterpret_cast<uint8_t*>(P.dst);
-        d[base] = (uint8_t)v0;
-        d[base + plane] = (uint8_t)v1;
-        d[base + 2 * plane] = (uint8_t)v2;
-    } else {
-        float* d = reinterpret_cast<float*>(P.dst);
-        d[base] = lut[v0];
-        d[base + plane] = lut[256 + v1];
-        d[base + 2 * plane] = lut[512 + v2];
-    }
-}
-
-// Per-tile values the consumer waves read from the table set header (written by the loader).
-struct TileHdr {
-    int X0, Y0, X1, Y1;
-    int active, offC, offV, slot;
-};
-constexpr int kHdrBytes = (int)sizeof(TileHdr);
-
-__device__ __forceinline__ ColEntry* tab_cols(uint8_t* tab) { return reinterpret_cast<ColEntry*>(tab + kHdrBytes); }
-__device__ __forceinline__ RowEntry* tab_rows(uint8_t* tab, const KParams& P) {
-    return reinterpret_cast<RowEntry*>(tab + kHdrBytes + P.TW * (int)sizeof(ColEntry));
-}
-__device__ __forceinline__ int32_t* tab_slots(uint8_t* tab, const KParams& P) {
-    return reinterpret_cast<int32_t*>(tab + kHdrBytes + P.TW * (int)sizeof(ColEntry) + P.TH * (int)sizeof(RowEntry));
-}
-
-// Tile geometry, footprint and coefficient tables, written to the table set `tab` by `nthr` threads.
+// Raw bytes of one source pixel, read straight from the frame (global memory, through L1/L2).
+// Plane bases are wave-uniform (SGPR) and offsets 32-bit, so each load is one saddr-form instruction.
 template <int FMT>
-__device__ __forceinline__ void setup_tile(const KParams& P, int t, uint8_t* tab, TileInfo& ti, int tid, int nthr) {
+__device__ __forceinline__ void load_tap(const uint8_t* __restrict__ p0, const uint8_t* __restrict__ p1,
+                                         const uint8_t* __restrict__ p2, uint32_t oy, uint32_t oc, uint32_t (&v)[3]) {
+    if constexpr (FMT == kNV12) {
+        v[0] = p0[oy];
+        v[1] = *reinterpret_cast<const uint16_t*>(p1 + oc);
+    } else if constexpr (FMT == kI420) {
+        v[0] = p0[oy];
+        v[1] = p1[oc];
+        v[2] = p2[oc];
+    } else if constexpr (FMT == kBGRX) {
+        v[0] = *reinterpret_cast<const uint32_t*>(p0 + oy);
+    } else {
+        v[0] = p0[oy];
+        v[1] = p0[oy + 1];
+        v[2] = p0[oy + 2];
+    }
+}
+
+template <int FMT>
+__device__ __forceinline__ void to_bgr(const uint32_t (&v)[3], int& b, int& g, int& r) {
+    if constexpr (FMT == kNV12) {
+        yuv_to_bgr((int)v[0], (int)(v[1] & 0xFF), (int)(v[1] >> 8), b, g, r);
+    } else if constexpr (FMT == kI420) {
+        yuv_to_bgr((int)v[0], (int)v[1], (int)v[2], b, g, r);
+    } else if constexpr (FMT == kBGRX) {
+        b = v[0] & 0xFF; g = (v[0] >> 8) & 0xFF; r = (v[0] >> 16) & 0xFF;
+    } else {
+        b = (int)v[0]; g = (int)v[1]; r = (int)v[2];
+    }
+}
+
+// Planar stores of one pixel. Plane bases are wave-uniform (SGPR) and the offset is a 32-bit byte
+// offset, so every store is one saddr-form instruction with no 64-bit address arithmetic.
+template <int OUT>
+__device__ __forceinline__ void store_px(uint8_t* d0, uint8_t* d1, uint8_t* d2, const float* __restrict__ lut,
+                                         uint32_t o, int v0, int v1, int v2) {
+    if constexpr (OUT == 0) {
+        d0[o] = (uint8_t)v0;
+        d1[o] = (uint8_t)v1;
+        d2[o] = (uint8_t)v2;
+    } else {
+        const uint32_t ob = o << 2;
+        *reinterpret_cast<float*>(d0 + ob) = lut[v0];
+        *reinterpret_cast<float*>(d1 + ob) = lut[256 + v1];
+        *reinterpret_cast<float*>(d2 + ob) = lut[512 + v2];
+    }
+}
+
+// One workgroup per output tile (TW x TH pixels of one item). The workgroup builds the OpenCV
+// coefficient tables of its columns and rows in LDS (device-side, exact double/float sequence), then
+// every lane gathers the four taps of its pixels directly from the frame in HBM — luma and chroma
+// bytes through L1, adjacent lanes sharing cache lines — converts them to BGR, runs both resize passes,
+// maps the u8 result through the normalisation LUT and stores the three planes. No staging, no barrier
+// after the tables: the memory pipeline overlaps loads of many pixels and many waves.
+template <int FMT, int OUT>
+__global__ __launch_bounds__(kThreads) void evam_pp_kernel(const KParams P) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     using T = FmtTraits<FMT>;
+    const int tid = threadIdx.x;
+    const int t = blockIdx.x;
     const int item = t / P.tiles_per_item;
     const int tile = t - item * P.tiles_per_item;
     const int ty = tile / P.tiles_x;
     const int tx = tile - ty * P.tiles_x;
-    // Descriptors are read-only for the launch: read them through the constant address space so they
-    // become scalar (s_load, lgkmcnt) loads, which never wait behind the LDS-DMA on vmcnt.
+    // Descriptors are read-only for the launch: the constant address space makes them scalar loads.
     const __attribute__((address_space(4))) ItemDesc* it =
         (const __attribute__((address_space(4))) ItemDesc*)(P.items) + item;
-    for (int i = 0; i < 3; i++) {
-        ti.plane[i] = it->plane[i];
-        ti.pitch[i] = it->pitch[i];
-    }
-    ti.slot = it->slot;
-    ti.X0 = tx * P.TW;
-    ti.Y0 = ty * P.TH;
-    ti.X1 = min(ti.X0 + P.TW, P.DW);
-    ti.Y1 = min(ti.Y0 + P.TH, P.DH);
-    const int ox = it->ox, oy = it->oy, rw = it->rw, rh = it->rh, cw = it->cw, ch = it->ch;
-    const int x0 = it->x0, y0 = it->y0;
+    const uint8_t* __restrict__ p0 = it->plane[0];
+    const uint8_t* __restrict__ p1 = it->plane[1];
+    const uint8_t* __restrict__ p2 = it->plane[2];
+    const int pitch0 = it->pitch[0], pitch1 = it->pitch[1];
+    const int x0 = it->x0, y0 = it->y0, cw = it->cw, ch = it->ch;
+    const int rw = it->rw, rh = it->rh, ox = it->ox, oy = it->oy;
     const double scx = it->scale_x, scy = it->scale_y;
-    const int dx_lo = max(ti.X0 - ox, 0), dx_hi = min(ti.X1 - ox, rw) - 1;
-    const int dy_lo = max(ti.Y0 - oy, 0), dy_hi = min(ti.Y1 - oy, rh) - 1;
-    ti.active = dx_lo <= dx_hi && dy_lo <= dy_hi;
-    ti.fsY = ti.cprY = ti.fsC = ti.cprC = ti.offC = ti.offV = 0;
-    if (ti.active) {
-        int sxa, sxb, cd0, cd1;
-        linear_coef(dx_lo, scx, cw, true, sxa, cd0, cd1);
-        linear_coef(dx_hi, scx, cw, true, sxb, cd0, cd1);
-        const int xa = x0 + sxa;                      // first source column touched
-        const int xb = x0 + min(sxb + 1, cw - 1);     // last source column touched
-        ti.fsY = (xa * T::bpp) & ~15;
-        ti.cprY = (((xb * T::bpp + T::bpp + 15) & ~15) - ti.fsY) >> 4;
-        if constexpr (FMT == kNV12) {
-            ti.fsC = (2 * (xa >> 1)) & ~15;
-            ti.cprC = (((2 * (xb >> 1) + 2 + 15) & ~15) - ti.fsC) >> 4;
-        } else if constexpr (FMT == kI420) {
-            ti.fsC = (xa >> 1) & ~15;
-            ti.cprC = ((((xb >> 1) + 1 + 15) & ~15) - ti.fsC) >> 4;
-        }
-        ti.offC = 2 * P.TH * ti.cprY * 16;
-        ti.offV = ti.offC + 2 * P.TH * ti.cprC * 16;
+    const int X0 = tx * P.TW, Y0 = ty * P.TH;
+    const int X1 = min(X0 + P.TW, P.DW), Y1 = min(Y0 + P.TH, P.DH);
+    const size_t plane = (size_t)P.DW * P.DH;
+    const size_t esz = OUT == 1 ? 4 : 1;
+    uint8_t* const d0 = reinterpret_cast<uint8_t*>(P.dst) + (size_t)it->slot * 3 * plane * esz;
+    uint8_t* const d1 = d0 + plane * esz;
+    uint8_t* const d2 = d1 + plane * esz;
+
+    float* lut_s = reinterpret_cast<float*>(smem);
+    if constexpr (OUT == 1) {
+        for (int i = tid; i < 768; i += kThreads) lut_s[i] = P.lut[i];
     }
-    if (tid == 0) {
-        TileHdr h;
-        h.X0 = ti.X0; h.Y0 = ti.Y0; h.X1 = ti.X1; h.Y1 = ti.Y1;
-        h.active = ti.active; h.offC = ti.offC; h.offV = ti.offV; h.slot = ti.slot;
-        *reinterpret_cast<TileHdr*>(tab) = h;
-    }
-    if (!ti.active) return;
-    const int fwY = ti.cprY * 16, fwC = ti.cprC * 16;
-    ColEntry* coltab = tab_cols(tab);
-    RowEntry* rowtab = tab_rows(tab, P);
-    int32_t* slotY = tab_slots(tab, P);
-    int32_t* slotC = slotY + 2 * P.TH;
-    for (int lx = tid; lx < P.TW; lx += nthr) {
+    ColEntry* coltab = reinterpret_cast<ColEntry*>(smem + P.offCol);
+    RowEntry* rowtab = reinterpret_cast<RowEntry*>(smem + P.offRow);
+    for (int lx = tid; lx < P.TW; lx += kThreads) {
         ColEntry e;
-        const int dx = ti.X0 + lx - ox;
-        if (ti.X0 + lx < ti.X1 && dx >= 0 && dx < rw) {
+        const int dx = X0 + lx - ox;
+        if (X0 + lx < X1 && dx >= 0 && dx < rw) {
             int sx, a0, a1;
             linear_coef(dx, scx, cw, true, sx, a0, a1);
             const int ca = x0 + sx, cb = x0 + min(sx + 1, cw - 1);
-            e.oY0 = (int16_t)(ca * T::bpp - ti.fsY);
-            e.oY1 = (int16_t)(cb * T::bpp - ti.fsY);
-            if constexpr (FMT == kNV12) {
-                e.oC0 = (int16_t)(2 * (ca >> 1) - ti.fsC);
-                e.oC1 = (int16_t)(2 * (cb >> 1) - ti.fsC);
-            } else {
-                e.oC0 = (int16_t)((ca >> 1) - ti.fsC);
-                e.oC1 = (int16_t)((cb >> 1) - ti.fsC);
-            }
-            e.a0 = (int16_t)a0;
-            e.a1 = (int16_t)a1;
+            e.oY0 = ca * T::bpp;
+            e.oY1 = cb * T::bpp;
+            e.oC0 = FMT == kNV12 ? 2 * (ca >> 1) : (ca >> 1);
+            e.a0 = (uint16_t)(a0 << 4);
+            e.a1 = (uint16_t)(a1 << 4);
         } else {
-            e.oY0 = -1; e.oY1 = -1; e.oC0 = 0; e.oC1 = 0; e.a0 = 0; e.a1 = 0;
+            e.oY0 = -1; e.oY1 = 0; e.oC0 = 0; e.a0 = 0; e.a1 = 0;
         }
-        e.pad0 = 0; e.pad1 = 0;
         coltab[lx] = e;
     }
-    for (int ly = tid; ly < P.TH; ly += nthr) {
+    for (int ly = tid; ly < P.TH; ly += kThreads) {
         RowEntry e;
-        const int dy = ti.Y0 + ly - oy;
-        int ya = -1, yb = -1, ca = -1, cb = -1;
-        if (ti.Y0 + ly < ti.Y1 && dy >= 0 && dy < rh) {
+        const int dy = Y0 + ly - oy;
+        if (Y0 + ly < Y1 && dy >= 0 && dy < rh) {
             int sy, b0, b1;
             linear_coef(dy, scy, ch, false, sy, b0, b1);
-            ya = y0 + min(max(sy, 0), ch - 1);
-            yb = y0 + min(max(sy + 1, 0), ch - 1);
-            e.y0 = (2 * ly) * fwY;
-            e.y1 = yb == ya ? e.y0 : (2 * ly + 1) * fwY;
-            if (yb == ya) yb = -1;
-            if constexpr (T::nchroma > 0) {
-                ca = ya >> 1;
-                cb = (yb < 0 ? ya : yb) >> 1;
-                e.c0 = ti.offC + (2 * ly) * fwC;
-                e.c1 = cb == ca ? e.c0 : ti.offC + (2 * ly + 1) * fwC;
-                if (cb == ca) cb = -1;
-            } else {
-                e.c0 = 0; e.c1 = 0;
-            }
-            e.b0 = b0;
-            e.b1 = b1;
+            const int ya = y0 + min(max(sy, 0), ch - 1);
+            const int yb = y0 + min(max(sy + 1, 0), ch - 1);
+            e.y0 = ya * pitch0;
+            e.y1 = yb * pitch0;
+            e.c0 = (ya >> 1) * pitch1;
+            e.c1 = (yb >> 1) * pitch1;
+            e.b0 = b0 << 8;
+            e.b1 = b1 << 8;
         } else {
-            e.y0 = -1; e.y1 = -1; e.c0 = 0; e.c1 = 0; e.b0 = 0; e.b1 = 0;
+            e.y0 = -1; e.y1 = 0; e.c0 = 0; e.c1 = 0; e.b0 = 0; e.b1 = 0;
         }
         e.pad0 = 0; e.pad1 = 0;
         rowtab[ly] = e;
-        slotY[2 * ly] = ya;
-        slotY[2 * ly + 1] = yb;
-        slotC[2 * ly] = ca;
-        slotC[2 * ly + 1] = cb;
     }
-}
+    __syncthreads();
 
-template <int FMT>
-__device__ __forceinline__ void issue_tile(const KParams& P, const TileInfo& ti, uint8_t* tab, uint8_t* buf,
-                                           int tid, int nthr) {
-    using T = FmtTraits<FMT>;
-    const int32_t* slotY = tab_slots(tab, P);
-    const int32_t* slotC = slotY + 2 * P.TH;
-    issue_plane(buf, slotY, 2 * P.TH, ti.plane[0], ti.pitch[0], ti.fsY, ti.cprY, tid, nthr);
-    if constexpr (T::nchroma >= 1)
-        issue_plane(buf + ti.offC, slotC, 2 * P.TH, ti.plane[1], ti.pitch[1], ti.fsC, ti.cprC, tid, nthr);
-    if constexpr (T::nchroma == 2)
-        issue_plane(buf + ti.offV, slotC, 2 * P.TH, ti.plane[2], ti.pitch[2], ti.fsC, ti.cprC, tid, nthr);
-}
-
-// Convert + resize + normalise + planar store of one tile from its staged footprint (kConsumers threads).
-template <int FMT, int OUT>
-__device__ __forceinline__ void compute_tile(const KParams& P, uint8_t* tab, const uint8_t* buf,
-                                             const float* lut_s, int tid) {
-    const TileHdr hd = *reinterpret_cast<const TileHdr*>(tab);
-    const size_t plane = (size_t)P.DW * P.DH;
-    const size_t slot_base = (size_t)hd.slot * 3 * plane;
-    const int npx = P.TW * P.TH;
     const int f0 = P.fill & 0xFF, f1 = (P.fill >> 8) & 0xFF, f2 = (P.fill >> 16) & 0xFF;
-    const ColEntry* coltab = tab_cols(tab);
-    const RowEntry* rowtab = tab_rows(tab, P);
-    const int vdelta = hd.offV - hd.offC;
-    for (int p = tid; p < npx; p += kConsumers) {
-        const int ly = P.TW == 1 ? p : (int)umulhi((uint32_t)p, P.tw_magic);  // p / TW
-        const int lx = p - ly * P.TW;
-        const int X = hd.X0 + lx, Y = hd.Y0 + ly;
-        if (X >= hd.X1 || Y >= hd.Y1) continue;
-        const size_t base = slot_base + (size_t)Y * P.DW + X;
-        if (!hd.active || (P.ablate & 2)) {
-            if (!(P.ablate & 4)) store_px<OUT>(P, lut_s, base, plane, f0, f1, f2);
-            continue;
+    const int npx = P.TW * P.TH;
+    // (lx, ly) of pixel p = tid + k * 256, advanced incrementally (no per-pixel division).
+    const int qstep = kThreads / P.TW, rstep = kThreads - qstep * P.TW;
+    int ly = tid / P.TW;
+    int lx = tid - ly * P.TW;
+    const uint32_t o_tile = (uint32_t)(Y0 * P.DW + X0);
+    // kUnroll pixels per lane per step: all their tap loads are issued before any of them is used,
+    // so every wave keeps kUnroll x (4..12) independent loads in flight.
+    for (int pb = tid; pb < npx; pb += kThreads * kUnroll) {
+        uint32_t raw[kUnroll][4][3];
+        uint32_t o[kUnroll], wa[kUnroll], wb0[kUnroll], wb1[kUnroll];
+        int mode[kUnroll];  // 0: outside the tile, 1: padding / fill, 2: image pixel
+#pragma unroll
+        for (int u = 0; u < kUnroll; u++) {
+            const int cx = lx, cy = ly;
+            lx += rstep;
+            ly += qstep;
+            if (lx >= P.TW) { lx -= P.TW; ly++; }
+            const bool in_tile = pb + u * kThreads < npx && X0 + cx < X1 && Y0 + cy < Y1;
+            const ColEntry ce = coltab[in_tile ? cx : 0];
+            const RowEntry re = rowtab[in_tile ? cy : 0];
+            const bool img = in_tile && ce.oY0 >= 0 && re.y0 >= 0 && !(P.ablate & 2);
+            mode[u] = !in_tile ? 0 : (img ? 2 : 1);
+            o[u] = o_tile + __umul24((uint32_t)cy, (uint32_t)P.DW) + (uint32_t)cx;
+            wa[u] = (uint32_t)ce.a0 | ((uint32_t)ce.a1 << 16);
+            wb0[u] = (uint32_t)re.b0;
+            wb1[u] = (uint32_t)re.b1;
+            // padding / out-of-tile lanes load from offset 0 (always valid) and discard the bytes
+            const uint32_t oyA = img ? (uint32_t)(re.y0 + ce.oY0) : 0u;
+            const uint32_t oyB = img ? (uint32_t)(re.y0 + ce.oY1) : 0u;
+            const uint32_t oyC = img ? (uint32_t)(re.y1 + ce.oY0) : 0u;
+            const uint32_t oyD = img ? (uint32_t)(re.y1 + ce.oY1) : 0u;
+            const uint32_t oc0 = (uint32_t)ce.oC0;
+            const uint32_t oc1 = FMT == kNV12 ? ((uint32_t)ce.oY1 & ~1u) : ((uint32_t)ce.oY1 >> 1);
+            const uint32_t ocA = img ? (uint32_t)re.c0 + oc0 : 0u;
+            const uint32_t ocB = img ? (uint32_t)re.c0 + oc1 : 0u;
+            const uint32_t ocC = img ? (uint32_t)re.c1 + oc0 : 0u;
+            const uint32_t ocD = img ? (uint32_t)re.c1 + oc1 : 0u;
+            load_tap<FMT>(p0, p1, p2, oyA, ocA, raw[u][0]);
+            load_tap<FMT>(p0, p1, p2, oyB, ocB, raw[u][1]);
+            load_tap<FMT>(p0, p1, p2, oyC, ocC, raw[u][2]);
+            load_tap<FMT>(p0, p1, p2, oyD, ocD, raw[u][3]);
         }
-        const ColEntry ce = coltab[lx];
-        const RowEntry re = rowtab[ly];
-        if (ce.oY0 < 0 || re.y0 < 0) {
-            store_px<OUT>(P, lut_s, base, plane, f0, f1, f2);
-            continue;
-        }
-        int bA, gA, rA, bB, gB, rB;
-        tap<FMT>(buf, re.y0, re.c0, re.c0 + vdelta, ce.oY0, ce.oC0, bA, gA, rA);
-        tap<FMT>(buf, re.y0, re.c0, re.c0 + vdelta, ce.oY1, ce.oC1, bB, gB, rB);
-        const int Db0 = __mul24(bA, ce.a0) + __mul24(bB, ce.a1);
-        const int Dg0 = __mul24(gA, ce.a0) + __mul24(gB, ce.a1);
-        const int Dr0 = __mul24(rA, ce.a0) + __mul24(rB, ce.a1);
-        tap<FMT>(buf, re.y1, re.c1, re.c1 + vdelta, ce.oY0, ce.oC0, bA, gA, rA);
-        tap<FMT>(buf, re.y1, re.c1, re.c1 + vdelta, ce.oY1, ce.oC1, bB, gB, rB);
-        const int Db1 = __mul24(bA, ce.a0) + __mul24(bB, ce.a1);
-        const int Dg1 = __mul24(gA, ce.a0) + __mul24(gB, ce.a1);
-        const int Dr1 = __mul24(rA, ce.a0) + __mul24(rB, ce.a1);
-        const int vb = vresize(Db0, Db1, re.b0, re.b1);
-        const int vg = vresize(Dg0, Dg1, re.b0, re.b1);
-        const int vr = vresize(Dr0, Dr1, re.b0, re.b1);
-        if (P.ablate & 4) {
-            asm volatile("" :: "v"(vb), "v"(vg), "v"(vr));  // keep the math alive
-            continue;
-        }
-        if (P.color_rgb)
-            store_px<OUT>(P, lut_s, base, plane, vr, vg, vb);
-        else
-            store_px<OUT>(P, lut_s, base, plane, vb, vg, vr);
-    }
-}
-
-// Persistent loader/consumer kernel. Wave 0 is the loader: it builds the tables of tile t + G and
-// streams its source footprint into the other staging buffer by LDS-DMA, then waits only for its own
-// DMA (it never stores). Waves 1..4 are consumers: they convert tile t and store it, and never wait for
-// their stores. One raw s_barrier per tile hands buffer and tables over. Workgroup g processes tiles
-// g, g + G, g + 2G, ...; a grid of one workgroup per tile degenerates to load -> barrier -> compute.
-template <int FMT, int OUT>
-__global__ __launch_bounds__(kBlock) void evam_pp_kernel(const KParams P) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const int tid = threadIdx.x;
-    const bool loader = __builtin_amdgcn_readfirstlane(tid >> 6) == 0;  // wave 0, provably wave-uniform
-    const float* lut_s = reinterpret_cast<const float*>(smem);
-    int t = blockIdx.x;
-    if (t >= P.n_tiles) return;
-    uint8_t* const tab0 = smem + P.offTab;
-    uint8_t* const tab1 = tab0 + P.tab_bytes;
-    uint8_t* const buf0 = smem + P.offBuf;
-    uint8_t* const buf1 = buf0 + P.buf_bytes;
-    if (loader) {
-        TileInfo ti;
-        setup_tile<FMT>(P, t, tab0, ti, tid, kLoaderThreads);
-        if (ti.active && !(P.ablate & 1)) issue_tile<FMT>(P, ti, tab0, buf0, tid, kLoaderThreads);
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    } else {
-        if constexpr (OUT == 1) {
-            float* l = reinterpret_cast<float*>(smem);
-            for (int i = tid - kLoaderThreads; i < 768; i += kConsumers) l[i] = P.lut[i];
-        }
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_s_barrier();
-    int b = 0;
-    for (;;) {
-        const int tn = t + (int)gridDim.x;
-        const bool has_next = tn < P.n_tiles;
-        if (loader) {
-            if (has_next) {
-                uint8_t* tab_n = b ? tab0 : tab1;
-                uint8_t* buf_n = b ? buf0 : buf1;
-                TileInfo ti;
-                setup_tile<FMT>(P, tn, tab_n, ti, tid, kLoaderThreads);
-                if (ti.active && !(P.ablate & 1)) issue_tile<FMT>(P, ti, tab_n, buf_n, tid, kLoaderThreads);
-                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // own DMA + table writes
+#pragma unroll
+        for (int u = 0; u < kUnroll; u++) {
+            if (mode[u] == 0) continue;
+            if (mode[u] == 1) {
+                if (!(P.ablate & 4)) store_px<OUT>(d0, d1, d2, lut_s, o[u], f0, f1, f2);
+                continue;
             }
-        } else {
-            compute_tile<FMT, OUT>(P, b ? tab1 : tab0, b ? buf1 : buf0, lut_s, tid - kLoaderThreads);
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads of tab/buf done; stores stay in flight
+            const uint32_t a0 = wa[u] & 0xFFFF, a1 = wa[u] >> 16;  // 15-bit
+            int bA, gA, rA, bB, gB, rB;
+            to_bgr<FMT>(raw[u][0], bA, gA, rA);
+            to_bgr<FMT>(raw[u][1], bB, gB, rB);
+            const uint32_t Db0 = __umul24(bA, a0) + __umul24(bB, a1);
+            const uint32_t Dg0 = __umul24(gA, a0) + __umul24(gB, a1);
+            const uint32_t Dr0 = __umul24(rA, a0) + __umul24(rB, a1);
+            to_bgr<FMT>(raw[u][2], bA, gA, rA);
+            to_bgr<FMT>(raw[u][3], bB, gB, rB);
+            const uint32_t Db1 = __umul24(bA, a0) + __umul24(bB, a1);
+            const uint32_t Dg1 = __umul24(gA, a0) + __umul24(gB, a1);
+            const uint32_t Dr1 = __umul24(rA, a0) + __umul24(rB, a1);
+            const int vb = vresize(Db0, Db1, wb0[u], wb1[u]);
+            const int vg = vresize(Dg0, Dg1, wb0[u], wb1[u]);
+            const int vr = vresize(Dr0, Dr1, wb0[u], wb1[u]);
+            if (P.ablate & 4) {
+                asm volatile("" :: "v"(vb), "v"(vg), "v"(vr));  // keep the math alive
+                continue;
+            }
+            if (P.color_rgb)
+                store_px<OUT>(d0, d1, d2, lut_s, o[u], vr, vg, vb);
+            else
+                store_px<OUT>(d0, d1, d2, lut_s, o[u], vb, vg, vr);
         }
-        if (!has_next) break;
-        __builtin_amdgcn_s_barrier();
-        t = tn;
-        b ^= 1;
     }
 }
 
@@ -606,7 +489,7 @@ int64_t item_src_bytes(int f, const Geom& g, int DW, int DH) {
 }
 
 struct TileCfg {
-    int TW, TH, strideY, strideC, tab_bytes, buf_bytes, offTab, offBuf, lds;
+    int TW, TH, offCol, offRow, lds;
 };
 
 int env_int(const char* name, int dflt) {
@@ -614,39 +497,24 @@ int env_int(const char* name, int dflt) {
     return (v && *v) ? atoi(v) : dflt;
 }
 
-// Tile shape: TW x TH output pixels per 256-thread workgroup iteration (~512 by default), shrunk until
-// two table sets + two staging buffers fit the LDS budget. EVAM_PP_TW / EVAM_PP_TH override (tuning).
-TileCfg choose_tiles(int f, int DW, int DH, double max_ratio_x, int out_dtype) {
+// Tile shape: up to 512 columns (a whole model-input row when it fits) x enough rows for ~4096 output
+// pixels per 256-thread workgroup, so the per-tile table setup is amortised over ~16 pixels per lane.
+// EVAM_PP_TW / EVAM_PP_TH override (tuning).
+TileCfg choose_tiles(int DW, int DH, int out_dtype) {
     TileCfg t{};
-    if (DW <= 256) t.TW = DW;
-    else if (DW % 128 == 0) t.TW = 128;
-    else if (DW % 64 == 0) t.TW = 64;
-    else t.TW = 128;
-    t.TH = std::max(1, std::min(DH, 512 / t.TW));
+    t.TW = std::min(DW, 512);
+    t.TH = std::max(1, std::min(DH, 4096 / t.TW));
     t.TW = std::max(1, std::min(DW, env_int("EVAM_PP_TW", t.TW)));
     t.TH = std::max(1, std::min(DH, env_int("EVAM_PP_TH", t.TH)));
-    const int bpp = fmt_bpp(f);
-    const int nC = f == kNV12 ? 1 : (f == kI420 ? 2 : 0);
-    for (;;) {
-        const int span = (int)std::ceil((t.TW - 1) * max_ratio_x) + 4;  // source columns touched, upper bound
-        t.strideY = ((span * bpp + 32) + 15) & ~15;
-        t.strideC = f == kNV12 ? ((span + 2 + 32 + 15) & ~15) : (f == kI420 ? ((span / 2 + 2 + 32 + 15) & ~15) : 0);
-        t.tab_bytes = (32 + (int)sizeof(ColEntry) * t.TW + (int)sizeof(RowEntry) * t.TH + 16 * t.TH + 15) & ~15;
-        t.buf_bytes = 2 * t.TH * (t.strideY + nC * t.strideC);
-        t.offTab = out_dtype == EVAM_DTYPE_F32 ? kLutBytes : 0;
-        t.offBuf = t.offTab + 2 * t.tab_bytes;
-        t.lds = t.offBuf + 2 * t.buf_bytes;
-        if (t.lds <= kLdsBudget) break;
-        if (t.TH > 1) t.TH = std::max(1, t.TH / 2);
-        else if (t.TW > 16) t.TW = std::max(16, t.TW / 2);
-        else break;
-    }
+    t.offCol = out_dtype == EVAM_DTYPE_F32 ? kLutBytes : 0;
+    t.offRow = t.offCol + (int)sizeof(ColEntry) * t.TW;
+    t.lds = t.offRow + (int)sizeof(RowEntry) * t.TH;
     return t;
 }
 
 template <int FMT, int OUT>
 hipError_t launch_t(const KParams& p, int grid, int lds, hipStream_t s) {
-    hipLaunchKernelGGL((evam_pp_kernel<FMT, OUT>), dim3(grid), dim3(kBlock), lds, s, p);
+    hipLaunchKernelGGL((evam_pp_kernel<FMT, OUT>), dim3(grid), dim3(kThreads), lds, s, p);
     return hipGetLastError();
 }
 
@@ -888,9 +756,7 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
     int launches = 0;
     for (int f = 0; f < 4; f++) {
         if (!count[f]) continue;
-        const TileCfg t = choose_tiles(f, DW, DH, max_ratio[f], cfg->out_dtype);
-        if (t.lds > 160 * 1024 || t.strideY >= 32768 || t.strideC >= 32768)
-            return fail(EVAM_PP_ERR_UNSUPPORTED, "evam_pp_run: source footprint too wide (%.1fx downscale)", max_ratio[f]);
+        const TileCfg t = choose_tiles(DW, DH, cfg->out_dtype);
         KParams p{};
         p.items = reinterpret_cast<const ItemDesc*>(h->d_block + kLutBytes) + first[f];
         p.lut = reinterpret_cast<const float*>(h->d_block);
@@ -904,24 +770,12 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
         if (n_tiles > 0x7FFFFFFF) return fail(EVAM_PP_ERR_INVALID_ARG, "evam_pp_run: too many tiles");
         p.n_tiles = (int)n_tiles;
         p.tw_magic = t.TW > 1 ? (uint32_t)(0xFFFFFFFFu / (uint32_t)t.TW) + 1u : 0u;
-        p.tab_bytes = t.tab_bytes; p.buf_bytes = t.buf_bytes;
-        p.offTab = t.offTab; p.offBuf = t.offBuf;
+        p.offCol = t.offCol; p.offRow = t.offRow;
         p.color_rgb = cfg->color_order == EVAM_COLOR_RGB;
-        p.ablate = env_int("EVAM_PP_ABLATE", 0);
         p.fill = (uint32_t)cfg->fill[0] | ((uint32_t)cfg->fill[1] << 8) | ((uint32_t)cfg->fill[2] << 16);
-        // Persistent grid: every resident workgroup slot gets a strided share of the tiles.
-        // EVAM_PP_WGS_PER_CU=0 launches one workgroup per tile instead (no cross-tile prefetch).
-        // Default: persistent, as many workgroups per CU as LDS and the 32-wave limit allow.
-        const int per_cu = env_int("EVAM_PP_WGS_PER_CU",
-                                   std::max(1, std::min(32 / (kBlock / 64), (160 * 1024) / std::max(t.lds, 1))));
-        int64_t grid = per_cu > 0 ? std::min<int64_t>(n_tiles, (int64_t)h->n_cu * per_cu) : n_tiles;
-        int lds = t.lds;
-        if (grid == n_tiles) {
-            // One tile per workgroup: no prefetch, so one table set + one buffer; the smaller LDS
-            // footprint buys occupancy (latency hiding across workgroups instead of inside one).
-            p.offBuf = t.offTab + t.tab_bytes;
-            lds = p.offBuf + t.buf_bytes;
-        }
+        p.ablate = env_int("EVAM_PP_ABLATE", 0);
+        const int64_t grid = n_tiles;
+        const int lds = t.lds;
         if (lds > 64 * 1024) {
             hipError_t e = hipSuccess;
             switch (f * 2 + cfg->out_dtype) {
