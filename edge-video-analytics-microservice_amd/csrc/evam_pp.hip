@@ -39,18 +39,14 @@ namespace {
 // constants
 // ------------------------------------------------------------------------------------------------
 constexpr int kThreads = 256;
-#ifndef EVAM_PP_UNROLL
-#define EVAM_PP_UNROLL 1
-#endif
-constexpr int kUnroll = EVAM_PP_UNROLL;  // pixels per lane whose loads are issued together
 constexpr int kLutBytes = 3 * 256 * 4;
 
 // OpenCV color_yuv.simd.hpp ITUR_BT_601_*; the -128 chroma bias is folded into the constants.
 constexpr int kCY = 1220542, kCUB = 2116026, kCUG = -409993, kCVG = -852492, kCVR = 1673527;
 constexpr int kHalf = 1 << 19;
-constexpr int kKR = kHalf - 128 * kCVR;
-constexpr int kKG = kHalf - 128 * kCVG - 128 * kCUG;
-constexpr int kKB = kHalf - 128 * kCUB;
+constexpr int kKR = kHalf - 128 * kCVR - 16 * kCY;  // the luma term is max(Y,16)*CY (see yuv_to_bgr)
+constexpr int kKG = kHalf - 128 * kCVG - 128 * kCUG - 16 * kCY;
+constexpr int kKB = kHalf - 128 * kCUB - 16 * kCY;
 
 enum FmtId { kNV12 = 0, kI420 = 1, kBGRX = 2, kBGR = 3 };
 
@@ -78,20 +74,20 @@ struct KParams {
     int offCol, offRow; // LDS carve: LUT at 0 (fp32 out), column table, row table
     int color_rgb;
     uint32_t fill;      // packed u8 fill, output channel order
-    int ablate;         // diagnostics only (EVAM_PP_ABLATE bits): 2 no pixel math, 4 no stores
+    int ablate;         // diagnostics only (EVAM_PP_ABLATE bits): 2 no pixel math, 4 no stores, 8 loads only, 16 no loads
 };
 
 // Per output column of a tile: absolute byte offsets of the two horizontal taps inside a source row.
 struct alignas(16) ColEntry {  // 16 B
-    int32_t oY0, oY1;  // luma / packed-pixel byte offsets of tap 0 / tap 1 (-1 in oY0: column shows padding)
+    int32_t oY0, oY1;  // luma / packed-pixel byte offsets of tap 0 / tap 1 (always valid addresses)
     int32_t oC0;       // chroma byte offset of tap 0 (NV12: U of the UV pair; I420: U/V plane column)
-    uint16_t a0, a1;   // 11-bit horizontal weights << 4 (see vresize)
+    uint16_t a0, a1;   // 11-bit horizontal weights << 4 (see vresize); both 0: the column shows padding
 };
 // Per output row of a tile: byte offsets of the two vertical taps' rows inside the planes.
 struct alignas(16) RowEntry {  // 32 B
-    int32_t y0, y1;   // row offsets in the luma / packed plane (-1 in y0: row shows padding)
+    int32_t y0, y1;   // row offsets in the luma / packed plane (always valid addresses)
     int32_t c0, c1;   // row offsets in the chroma plane(s) (I420: same offset for U and V)
-    int32_t b0, b1;   // 11-bit vertical weights << 8 (see vresize)
+    int32_t b0, b1;   // 11-bit vertical weights << 8 (see vresize); both 0: the row shows padding
     int32_t pad0, pad1;
 };
 
@@ -126,7 +122,7 @@ __device__ __forceinline__ int clamp255(int v) { return min(max(v, 0), 255); }
 // BT.601 20-bit fixed point (OpenCV uvToRGBuv + yRGBuvToRGBA). Arguments are raw bytes; every
 // product fits the full-rate 24-bit multiplier.
 __device__ __forceinline__ void yuv_to_bgr(int Y, int U, int V, int& b, int& g, int& r) {
-    const int y = __mul24(max(Y - 16, 0), kCY);
+    const int y = __mul24(max(Y, 16), kCY);  // max(Y-16,0)*CY + 16*CY; the 16*CY is folded into kK*
     const int ruv = __mul24(kCVR, V) + kKR;
     const int guv = __mul24(kCVG, V) + __mul24(kCUG, U) + kKG;
     const int buv = __mul24(kCUB, U) + kKB;
@@ -258,7 +254,7 @@ __global__ __launch_bounds__(kThreads) void evam_pp_kernel(const KParams P) {
             e.a0 = (uint16_t)(a0 << 4);
             e.a1 = (uint16_t)(a1 << 4);
         } else {
-            e.oY0 = -1; e.oY1 = 0; e.oC0 = 0; e.a0 = 0; e.a1 = 0;
+            e.oY0 = 0; e.oY1 = 0; e.oC0 = 0; e.a0 = 0; e.a1 = 0;
         }
         coltab[lx] = e;
     }
@@ -277,7 +273,7 @@ __global__ __launch_bounds__(kThreads) void evam_pp_kernel(const KParams P) {
             e.b0 = b0 << 8;
             e.b1 = b1 << 8;
         } else {
-            e.y0 = -1; e.y1 = 0; e.c0 = 0; e.c1 = 0; e.b0 = 0; e.b1 = 0;
+            e.y0 = 0; e.y1 = 0; e.c0 = 0; e.c1 = 0; e.b0 = 0; e.b1 = 0;
         }
         e.pad0 = 0; e.pad1 = 0;
         rowtab[ly] = e;
@@ -291,75 +287,84 @@ __global__ __launch_bounds__(kThreads) void evam_pp_kernel(const KParams P) {
     int ly = tid / P.TW;
     int lx = tid - ly * P.TW;
     const uint32_t o_tile = (uint32_t)(Y0 * P.DW + X0);
-    // kUnroll pixels per lane per step: all their tap loads are issued before any of them is used,
-    // so every wave keeps kUnroll x (4..12) independent loads in flight.
-    for (int pb = tid; pb < npx; pb += kThreads * kUnroll) {
-        uint32_t raw[kUnroll][4][3];
-        uint32_t o[kUnroll], wa[kUnroll], wb0[kUnroll], wb1[kUnroll];
-        int mode[kUnroll];  // 0: outside the tile, 1: padding / fill, 2: image pixel
-#pragma unroll
-        for (int u = 0; u < kUnroll; u++) {
-            const int cx = lx, cy = ly;
-            lx += rstep;
-            ly += qstep;
-            if (lx >= P.TW) { lx -= P.TW; ly++; }
-            const bool in_tile = pb + u * kThreads < npx && X0 + cx < X1 && Y0 + cy < Y1;
-            const ColEntry ce = coltab[in_tile ? cx : 0];
-            const RowEntry re = rowtab[in_tile ? cy : 0];
-            const bool img = in_tile && ce.oY0 >= 0 && re.y0 >= 0 && !(P.ablate & 2);
-            mode[u] = !in_tile ? 0 : (img ? 2 : 1);
-            o[u] = o_tile + __umul24((uint32_t)cy, (uint32_t)P.DW) + (uint32_t)cx;
-            wa[u] = (uint32_t)ce.a0 | ((uint32_t)ce.a1 << 16);
-            wb0[u] = (uint32_t)re.b0;
-            wb1[u] = (uint32_t)re.b1;
-            // padding / out-of-tile lanes load from offset 0 (always valid) and discard the bytes
-            const uint32_t oyA = img ? (uint32_t)(re.y0 + ce.oY0) : 0u;
-            const uint32_t oyB = img ? (uint32_t)(re.y0 + ce.oY1) : 0u;
-            const uint32_t oyC = img ? (uint32_t)(re.y1 + ce.oY0) : 0u;
-            const uint32_t oyD = img ? (uint32_t)(re.y1 + ce.oY1) : 0u;
-            const uint32_t oc0 = (uint32_t)ce.oC0;
-            const uint32_t oc1 = FMT == kNV12 ? ((uint32_t)ce.oY1 & ~1u) : ((uint32_t)ce.oY1 >> 1);
-            const uint32_t ocA = img ? (uint32_t)re.c0 + oc0 : 0u;
-            const uint32_t ocB = img ? (uint32_t)re.c0 + oc1 : 0u;
-            const uint32_t ocC = img ? (uint32_t)re.c1 + oc0 : 0u;
-            const uint32_t ocD = img ? (uint32_t)re.c1 + oc1 : 0u;
-            load_tap<FMT>(p0, p1, p2, oyA, ocA, raw[u][0]);
-            load_tap<FMT>(p0, p1, p2, oyB, ocB, raw[u][1]);
-            load_tap<FMT>(p0, p1, p2, oyC, ocC, raw[u][2]);
-            load_tap<FMT>(p0, p1, p2, oyD, ocD, raw[u][3]);
+
+    // Software pipeline, one pixel deep: the tap loads of pixel k+1 are issued before pixel k is
+    // converted, so every wave always has a pixel's loads in flight while it computes.
+    struct Px {
+        uint32_t raw[4][3];
+        uint32_t o, wa, wb0, wb1;
+        int mode;  // 0: outside the tile, 1: padding / fill, 2: image pixel
+    };
+    auto gather = [&](int p, Px& x) {
+        const int cx = lx, cy = ly;
+        lx += rstep;
+        ly += qstep;
+        if (lx >= P.TW) { lx -= P.TW; ly++; }
+        const bool in_tile = p < npx && X0 + cx < X1 && Y0 + cy < Y1;
+        const ColEntry ce = coltab[in_tile ? cx : 0];
+        const RowEntry re = rowtab[in_tile ? cy : 0];
+        x.wa = (uint32_t)ce.a0 | ((uint32_t)ce.a1 << 16);
+        x.wb0 = (uint32_t)re.b0;
+        x.wb1 = (uint32_t)re.b1;
+        const bool img = in_tile && x.wa != 0 && (x.wb0 | x.wb1) != 0 && !(P.ablate & 2);
+        x.mode = !in_tile ? 0 : (img ? 2 : 1);
+        x.o = o_tile + __umul24((uint32_t)cy, (uint32_t)P.DW) + (uint32_t)cx;
+        if (P.ablate & 16) {  // diagnostics: no loads, math on synthetic bytes
+            for (int k = 0; k < 4; k++) { x.raw[k][0] = (ce.oY0 + k) & 255; x.raw[k][1] = (re.y0 + ce.oC0 * k) & 0xFFFF; x.raw[k][2] = k; }
+            return;
         }
-#pragma unroll
-        for (int u = 0; u < kUnroll; u++) {
-            if (mode[u] == 0) continue;
-            if (mode[u] == 1) {
-                if (!(P.ablate & 4)) store_px<OUT>(d0, d1, d2, lut_s, o[u], f0, f1, f2);
-                continue;
-            }
-            const uint32_t a0 = wa[u] & 0xFFFF, a1 = wa[u] >> 16;  // 15-bit
-            int bA, gA, rA, bB, gB, rB;
-            to_bgr<FMT>(raw[u][0], bA, gA, rA);
-            to_bgr<FMT>(raw[u][1], bB, gB, rB);
-            const uint32_t Db0 = __umul24(bA, a0) + __umul24(bB, a1);
-            const uint32_t Dg0 = __umul24(gA, a0) + __umul24(gB, a1);
-            const uint32_t Dr0 = __umul24(rA, a0) + __umul24(rB, a1);
-            to_bgr<FMT>(raw[u][2], bA, gA, rA);
-            to_bgr<FMT>(raw[u][3], bB, gB, rB);
-            const uint32_t Db1 = __umul24(bA, a0) + __umul24(bB, a1);
-            const uint32_t Dg1 = __umul24(gA, a0) + __umul24(gB, a1);
-            const uint32_t Dr1 = __umul24(rA, a0) + __umul24(rB, a1);
-            const int vb = vresize(Db0, Db1, wb0[u], wb1[u]);
-            const int vg = vresize(Dg0, Dg1, wb0[u], wb1[u]);
-            const int vr = vresize(Dr0, Dr1, wb0[u], wb1[u]);
-            if (P.ablate & 4) {
-                asm volatile("" :: "v"(vb), "v"(vg), "v"(vr));  // keep the math alive
-                continue;
-            }
-            if (P.color_rgb)
-                store_px<OUT>(d0, d1, d2, lut_s, o[u], vr, vg, vb);
-            else
-                store_px<OUT>(d0, d1, d2, lut_s, o[u], vb, vg, vr);
+        // Table offsets are valid addresses even for padding / out-of-tile lanes: no selects here.
+        const uint32_t oc1 = FMT == kNV12 ? ((uint32_t)ce.oY1 & ~1u) : ((uint32_t)ce.oY1 >> 1);  // tap-1 chroma
+        load_tap<FMT>(p0, p1, p2, (uint32_t)(re.y0 + ce.oY0), (uint32_t)(re.c0 + ce.oC0), x.raw[0]);
+        load_tap<FMT>(p0, p1, p2, (uint32_t)(re.y0 + ce.oY1), (uint32_t)re.c0 + oc1, x.raw[1]);
+        load_tap<FMT>(p0, p1, p2, (uint32_t)(re.y1 + ce.oY0), (uint32_t)(re.c1 + ce.oC0), x.raw[2]);
+        load_tap<FMT>(p0, p1, p2, (uint32_t)(re.y1 + ce.oY1), (uint32_t)re.c1 + oc1, x.raw[3]);
+    };
+    auto finish = [&](const Px& x) {
+        if (x.mode == 0) return;
+        if (x.mode == 1) {
+            if (!(P.ablate & 4)) store_px<OUT>(d0, d1, d2, lut_s, x.o, f0, f1, f2);
+            return;
         }
+        if (P.ablate & 8) {  // diagnostics: loads only, trivial math
+            uint32_t acc = 0;
+            for (int k = 0; k < 4; k++) acc += x.raw[k][0] + x.raw[k][1] + x.raw[k][2];
+            asm volatile("" :: "v"(acc));
+            return;
+        }
+        const uint32_t a0 = x.wa & 0xFFFF, a1 = x.wa >> 16;  // 15-bit
+        int bA, gA, rA, bB, gB, rB;
+        to_bgr<FMT>(x.raw[0], bA, gA, rA);
+        to_bgr<FMT>(x.raw[1], bB, gB, rB);
+        const uint32_t Db0 = __umul24(bA, a0) + __umul24(bB, a1);
+        const uint32_t Dg0 = __umul24(gA, a0) + __umul24(gB, a1);
+        const uint32_t Dr0 = __umul24(rA, a0) + __umul24(rB, a1);
+        to_bgr<FMT>(x.raw[2], bA, gA, rA);
+        to_bgr<FMT>(x.raw[3], bB, gB, rB);
+        const uint32_t Db1 = __umul24(bA, a0) + __umul24(bB, a1);
+        const uint32_t Dg1 = __umul24(gA, a0) + __umul24(gB, a1);
+        const uint32_t Dr1 = __umul24(rA, a0) + __umul24(rB, a1);
+        const int vb = vresize(Db0, Db1, x.wb0, x.wb1);
+        const int vg = vresize(Dg0, Dg1, x.wb0, x.wb1);
+        const int vr = vresize(Dr0, Dr1, x.wb0, x.wb1);
+        if (P.ablate & 4) {
+            asm volatile("" :: "v"(vb), "v"(vg), "v"(vr));  // keep the math alive
+            return;
+        }
+        if (P.color_rgb)
+            store_px<OUT>(d0, d1, d2, lut_s, x.o, vr, vg, vb);
+        else
+            store_px<OUT>(d0, d1, d2, lut_s, x.o, vb, vg, vr);
+    };
+    if (tid >= npx) return;
+    Px cur, nxt;
+    gather(tid, cur);
+    for (int p = tid + kThreads; p < npx; p += kThreads) {
+        gather(p, nxt);
+        finish(cur);
+        cur = nxt;
     }
+    finish(cur);
 }
 
 // ------------------------------------------------------------------------------------------------
