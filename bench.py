@@ -140,8 +140,8 @@ def load_pmc_traffic(config_name: str, n_frames_per_launch: int):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=500)
+    ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--config", default="c2", choices=sorted(WORKLOADS))
     ap.add_argument("--frames", type=int, default=0, help="frames per rank per step (default: workload's)")
     ap.add_argument("--no-cpu-baseline", action="store_true")

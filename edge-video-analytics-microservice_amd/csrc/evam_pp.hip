@@ -29,6 +29,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/evam_pp.h"
@@ -89,6 +90,53 @@ struct alignas(16) RowEntry {  // 32 B
     int32_t c0, c1;   // row offsets in the chroma plane(s) (I420: same offset for U and V)
     int32_t b0, b1;   // 11-bit vertical weights << 8 (see vresize); both 0: the row shows padding
     int32_t pad0, pad1;
+};
+
+// Row-kernel (uniform geometry) tables, built on the host once per geometry and cached in the
+// descriptor block. Indexed by output column X / output row Y of the DW x DH plane.
+struct alignas(16) XTab {  // 16 B
+    int32_t s0, s1;      // source columns of the two taps, relative to the crop (s1 = min(s0+1, cw-1))
+    uint16_t a0, a1;     // 11-bit weights << 4; both 0: column shows padding
+    int32_t pad;
+};
+struct alignas(16) YTab {  // 16 B
+    int32_t r0, r1;      // source rows of the two taps, relative to the crop (clamped)
+    int32_t b0, b1;      // 11-bit weights << 8; both 0: row shows padding
+};
+
+struct RParams {
+    const ItemDesc* items;
+    const float* lut;    // [3][256]
+    const XTab* xtab;    // [DW]
+    const YTab* ytab;    // [DH]
+    void* dst;
+    int DW, DH;
+    int TW, TH, tiles_x, tiles_per_item;
+    int nsegx;           // TW / 64 column segments per tile row
+    int color_rgb;
+    uint32_t fill;
+    int ablate;
+};
+
+#ifndef EVAM_PP_STAGE_ROWS
+#define EVAM_PP_STAGE_ROWS 2
+#endif
+constexpr int kStageRows = EVAM_PP_STAGE_ROWS;  // output rows per staged group (R)
+constexpr int kSlot = 1024;  // bytes of one staged source-row segment = one wave-wide 16 B/lane LDS-DMA
+
+struct SParams {
+    const ItemDesc* items;
+    const float* lut;    // [3][256]
+    const XTab* xtab;    // [DW]
+    const YTab* ytab;    // [DH]
+    void* dst;
+    int DW, DH;
+    int TH, tiles_x, tiles_per_item;
+    int offBuf;          // LDS offset of staging buffer 0 (after the LUT)
+    int buf_bytes;       // one staging buffer: slots x kSlot
+    int color_rgb;
+    uint32_t fill;
+    int ablate;
 };
 
 // ------------------------------------------------------------------------------------------------
@@ -367,6 +415,458 @@ __global__ __launch_bounds__(kThreads) void evam_pp_kernel(const KParams P) {
     finish(cur);
 }
 
+// BT.601 split into the chroma part (per chroma sample) and the per-luma part, so a chroma sample
+// shared by two taps is converted once. Same integers as yuv_to_bgr.
+struct UV3 { int b, g, r; };
+__device__ __forceinline__ UV3 uv_terms(int U, int V) {
+    return UV3{__mul24(kCUB, U) + kKB, __mul24(kCVG, V) + __mul24(kCUG, U) + kKG, __mul24(kCVR, V) + kKR};
+}
+__device__ __forceinline__ void y_plus_uv(int Y, const UV3& t, int& b, int& g, int& r) {
+    const int y = __mul24(max(Y, 16), kCY);
+    b = clamp255((y + t.b) >> 20);
+    g = clamp255((y + t.g) >> 20);
+    r = clamp255((y + t.r) >> 20);
+}
+
+template <int FMT>
+struct Chroma {  // raw chroma of one tap: NV12 packed UV (u16), I420 U and V bytes
+    uint32_t u, v;
+};
+template <int FMT>
+__device__ __forceinline__ UV3 chroma_terms(const Chroma<FMT>& c) {
+    if constexpr (FMT == kNV12) return uv_terms((int)(c.u & 0xFF), (int)(c.u >> 8));
+    else return uv_terms((int)c.u, (int)c.v);
+}
+
+// Uniform-geometry kernel: every item of the launch has the same crop size, resized size and
+// placement, so the coefficient tables come precomputed from the host (XTab / YTab, L2-resident) and
+// each wave walks whole 64-pixel row segments. Row pointers, vertical weights and the destination row
+// are wave-uniform SGPR values; column offsets and horizontal weights are per-lane registers loaded
+// once per workgroup. The inner loop therefore spends its VALU slots on the arithmetic alone. When
+// both vertical taps read the same chroma row (4:2:0, ~half the rows) their chroma is loaded and
+// converted once.
+template <int FMT, int OUT>
+__global__ __launch_bounds__(kThreads) void evam_pp_rows(const RParams P) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    using T = FmtTraits<FMT>;
+    constexpr bool kYUV = FMT == kNV12 || FMT == kI420;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int t = blockIdx.x;
+    const int item = t / P.tiles_per_item;
+    const int tile = t - item * P.tiles_per_item;
+    const int ty = tile / P.tiles_x;
+    const int tx = tile - ty * P.tiles_x;
+    const __attribute__((address_space(4))) ItemDesc* it =
+        (const __attribute__((address_space(4))) ItemDesc*)(P.items) + item;
+    const __attribute__((address_space(4))) YTab* ytab = (const __attribute__((address_space(4))) YTab*)(P.ytab);
+    const uint8_t* __restrict__ p0 = it->plane[0];
+    const uint8_t* __restrict__ p1 = it->plane[1];
+    const uint8_t* __restrict__ p2 = it->plane[2];
+    const int pitch0 = it->pitch[0], pitch1 = it->pitch[1], pitch2 = it->pitch[2];
+    const int x0 = it->x0, y0 = it->y0;
+    const size_t plane = (size_t)P.DW * P.DH;
+    const size_t esz = OUT == 1 ? 4 : 1;
+    uint8_t* const d0 = reinterpret_cast<uint8_t*>(P.dst) + (size_t)it->slot * 3 * plane * esz;
+    uint8_t* const d1 = d0 + plane * esz;
+    uint8_t* const d2 = d1 + plane * esz;
+    // Buffer resources (wave-uniform). Offsets are always in range by construction, so the range
+    // check is set wide open.
+    const __amdgpu_buffer_rsrc_t rsY = __builtin_amdgcn_make_buffer_rsrc((void*)p0, (short)0, 0x7FFFFFFF, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsC = __builtin_amdgcn_make_buffer_rsrc((void*)(p1 ? p1 : p0), (short)0, 0x7FFFFFFF, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsV = __builtin_amdgcn_make_buffer_rsrc((void*)(p2 ? p2 : p0), (short)0, 0x7FFFFFFF, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsD0 = __builtin_amdgcn_make_buffer_rsrc((void*)d0, (short)0, 0x7FFFFFFF, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsD1 = __builtin_amdgcn_make_buffer_rsrc((void*)d1, (short)0, 0x7FFFFFFF, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsD2 = __builtin_amdgcn_make_buffer_rsrc((void*)d2, (short)0, 0x7FFFFFFF, 0x00020000);
+
+    float* lut_s = reinterpret_cast<float*>(smem);
+    if constexpr (OUT == 1) {
+        for (int i = tid; i < 768; i += kThreads) lut_s[i] = P.lut[i];
+        __syncthreads();
+    }
+    const int f0 = P.fill & 0xFF, f1 = (P.fill >> 8) & 0xFF, f2 = (P.fill >> 16) & 0xFF;
+
+    // Which 64-pixel column segments and which rows of the tile this wave owns.
+    const int X0 = tx * P.TW, Y0 = ty * P.TH, Y1 = min(Y0 + P.TH, P.DH);
+    int seg0, seg_step, nseg, row0, row_step;
+    if (P.nsegx >= 4) { seg0 = wave; seg_step = 4; nseg = P.nsegx >> 2; row0 = 0; row_step = 1; }
+    else { seg0 = wave % P.nsegx; seg_step = 0; nseg = 1; row0 = wave / P.nsegx; row_step = 4 / P.nsegx; }
+
+    // Per-lane column state, up to two segments per wave.
+    uint32_t oY0[2], oY1[2], oC0[2], oC1[2], wa[2], xo[2];
+    bool xin[2];
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+        const int X = X0 + (seg0 + j * seg_step) * 64 + lane;
+        xin[j] = j < nseg && X < P.DW;
+        const XTab xt = P.xtab[xin[j] ? X : 0];
+        const int ca = x0 + xt.s0, cb = x0 + xt.s1;
+        oY0[j] = (uint32_t)(ca * T::bpp);
+        oY1[j] = (uint32_t)(cb * T::bpp);
+        oC0[j] = FMT == kNV12 ? (uint32_t)(2 * (ca >> 1)) : (uint32_t)(ca >> 1);
+        oC1[j] = FMT == kNV12 ? (uint32_t)(2 * (cb >> 1)) : (uint32_t)(cb >> 1);
+        wa[j] = (uint32_t)xt.a0 | ((uint32_t)xt.a1 << 16);
+        xo[j] = (uint32_t)(xin[j] ? X : 0);
+    }
+
+    for (int Y = Y0 + row0; Y < Y1; Y += row_step) {
+        const int yr0 = ytab[Y].r0, yr1 = ytab[Y].r1, yb0 = ytab[Y].b0, yb1 = ytab[Y].b1;  // scalar loads
+        const uint32_t orow = (uint32_t)(Y * P.DW);
+        if ((yb0 | yb1) == 0 || (P.ablate & 2)) {  // padding row (letterbox)
+#pragma unroll
+            for (int j = 0; j < 2; j++)
+                if (xin[j] && !(P.ablate & 4)) store_px<OUT>(d0, d1, d2, lut_s, orow + xo[j], f0, f1, f2);
+            continue;
+        }
+        const int ya = y0 + yr0, yb = y0 + yr1;
+        // Wave-uniform row offsets go in the buffer instructions' SGPR offset; the per-lane column
+        // offsets are the VGPR offsets: no per-tap address arithmetic at all.
+        const int sY0 = ya * pitch0, sY1 = yb * pitch0;
+        const int sC0 = (ya >> 1) * pitch1, sC1 = (yb >> 1) * pitch1;
+        const int sV0 = (ya >> 1) * pitch2, sV1 = (yb >> 1) * pitch2;
+        const uint32_t wb0 = (uint32_t)yb0, wb1 = (uint32_t)yb1;
+        const int sO = (int)(orow * (uint32_t)esz);
+
+        auto run = [&](auto share_tag) {
+            constexpr bool kShare = decltype(share_tag)::value;
+            // ---- gather: every tap of every owned segment, before any arithmetic ----
+            uint32_t q[2][4][3];
+            Chroma<FMT> ch[2][4];
+            if (P.ablate & 16) {  // diagnostics: no loads, arithmetic on synthetic bytes
+#pragma unroll
+                for (int j = 0; j < 2; j++)
+#pragma unroll
+                    for (int k = 0; k < 4; k++) {
+                        q[j][k][0] = (oY0[j] + 37 * k) & 255; q[j][k][1] = (oY1[j] + k) & 255; q[j][k][2] = (oC0[j] + k) & 255;
+                        ch[j][k].u = (oC1[j] * (k + 1)) & 0xFFFF; ch[j][k].v = (oC0[j] ^ k) & 255;
+                    }
+            } else
+#pragma unroll
+            for (int j = 0; j < 2; j++) {
+                if constexpr (kYUV) {
+                    q[j][0][0] = __builtin_amdgcn_raw_buffer_load_b8(rsY, oY0[j], sY0, 0);
+                    q[j][1][0] = __builtin_amdgcn_raw_buffer_load_b8(rsY, oY1[j], sY0, 0);
+                    q[j][2][0] = __builtin_amdgcn_raw_buffer_load_b8(rsY, oY0[j], sY1, 0);
+                    q[j][3][0] = __builtin_amdgcn_raw_buffer_load_b8(rsY, oY1[j], sY1, 0);
+                    if constexpr (FMT == kNV12) {
+                        ch[j][0].u = __builtin_amdgcn_raw_buffer_load_b16(rsC, oC0[j], sC0, 0);
+                        ch[j][1].u = __builtin_amdgcn_raw_buffer_load_b16(rsC, oC1[j], sC0, 0);
+                        if constexpr (!kShare) {
+                            ch[j][2].u = __builtin_amdgcn_raw_buffer_load_b16(rsC, oC0[j], sC1, 0);
+                            ch[j][3].u = __builtin_amdgcn_raw_buffer_load_b16(rsC, oC1[j], sC1, 0);
+                        }
+                    } else {
+                        ch[j][0].u = __builtin_amdgcn_raw_buffer_load_b8(rsC, oC0[j], sC0, 0);
+                        ch[j][0].v = __builtin_amdgcn_raw_buffer_load_b8(rsV, oC0[j], sV0, 0);
+                        ch[j][1].u = __builtin_amdgcn_raw_buffer_load_b8(rsC, oC1[j], sC0, 0);
+                        ch[j][1].v = __builtin_amdgcn_raw_buffer_load_b8(rsV, oC1[j], sV0, 0);
+                        if constexpr (!kShare) {
+                            ch[j][2].u = __builtin_amdgcn_raw_buffer_load_b8(rsC, oC0[j], sC1, 0);
+                            ch[j][2].v = __builtin_amdgcn_raw_buffer_load_b8(rsV, oC0[j], sV1, 0);
+                            ch[j][3].u = __builtin_amdgcn_raw_buffer_load_b8(rsC, oC1[j], sC1, 0);
+                            ch[j][3].v = __builtin_amdgcn_raw_buffer_load_b8(rsV, oC1[j], sV1, 0);
+                        }
+                    }
+                } else {
+#pragma unroll
+                    for (int k = 0; k < 4; k++) {
+                        const int sr = (k >> 1) ? sY1 : sY0;
+                        const uint32_t o = (k & 1) ? oY1[j] : oY0[j];
+                        if constexpr (FMT == kBGRX) {
+                            q[j][k][0] = __builtin_amdgcn_raw_buffer_load_b32(rsY, o, sr, 0);
+                        } else {
+                            q[j][k][0] = __builtin_amdgcn_raw_buffer_load_b8(rsY, o, sr, 0);
+                            q[j][k][1] = __builtin_amdgcn_raw_buffer_load_b8(rsY, o + 1, sr, 0);
+                            q[j][k][2] = __builtin_amdgcn_raw_buffer_load_b8(rsY, o + 2, sr, 0);
+                        }
+                    }
+                }
+                if (j + 1 >= nseg) break;
+            }
+            // ---- arithmetic + stores ----
+#pragma unroll
+            for (int j = 0; j < 2; j++) {
+                if (j < nseg && xin[j]) {
+                    if (P.ablate & 8) {  // diagnostics: loads only
+                        uint32_t acc = ch[j][0].u + ch[j][1].u + (kShare ? 0u : ch[j][2].u + ch[j][3].u);
+#pragma unroll
+                        for (int k = 0; k < 4; k++) acc += q[j][k][0];
+                        asm volatile("" :: "v"(acc));
+                        continue;
+                    }
+                    const uint32_t a0 = wa[j] & 0xFFFF, a1 = wa[j] >> 16;  // 15-bit
+                    int c[4][3];
+                    if constexpr (kYUV) {
+                        const UV3 tA = chroma_terms<FMT>(ch[j][0]);
+                        const UV3 tB = chroma_terms<FMT>(ch[j][1]);
+                        const UV3 tC = kShare ? tA : chroma_terms<FMT>(ch[j][2]);
+                        const UV3 tD = kShare ? tB : chroma_terms<FMT>(ch[j][3]);
+                        y_plus_uv((int)q[j][0][0], tA, c[0][0], c[0][1], c[0][2]);
+                        y_plus_uv((int)q[j][1][0], tB, c[1][0], c[1][1], c[1][2]);
+                        y_plus_uv((int)q[j][2][0], tC, c[2][0], c[2][1], c[2][2]);
+                        y_plus_uv((int)q[j][3][0], tD, c[3][0], c[3][1], c[3][2]);
+                    } else {
+#pragma unroll
+                        for (int k = 0; k < 4; k++) {
+                            if constexpr (FMT == kBGRX) {
+                                c[k][0] = q[j][k][0] & 0xFF; c[k][1] = (q[j][k][0] >> 8) & 0xFF; c[k][2] = (q[j][k][0] >> 16) & 0xFF;
+                            } else {
+                                c[k][0] = (int)q[j][k][0]; c[k][1] = (int)q[j][k][1]; c[k][2] = (int)q[j][k][2];
+                            }
+                        }
+                    }
+                    int v[3];
+#pragma unroll
+                    for (int ch3 = 0; ch3 < 3; ch3++) {
+                        const uint32_t D0 = __umul24(c[0][ch3], a0) + __umul24(c[1][ch3], a1);
+                        const uint32_t D1 = __umul24(c[2][ch3], a0) + __umul24(c[3][ch3], a1);
+                        v[ch3] = vresize(D0, D1, wb0, wb1);
+                    }
+                    if (P.ablate & 4) {
+                        asm volatile("" :: "v"(v[0]), "v"(v[1]), "v"(v[2]));
+                    } else {
+                        if (P.color_rgb) { const int tmp = v[0]; v[0] = v[2]; v[2] = tmp; }
+                        const uint32_t vo = xo[j] * (uint32_t)esz;
+                        if constexpr (OUT == 1) {
+                            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lut_s[v[0]]), rsD0, vo, sO, 0);
+                            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lut_s[256 + v[1]]), rsD1, vo, sO, 0);
+                            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lut_s[512 + v[2]]), rsD2, vo, sO, 0);
+                        } else {
+                            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v[0], rsD0, vo, sO, 0);
+                            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v[1], rsD1, vo, sO, 0);
+                            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v[2], rsD2, vo, sO, 0);
+                        }
+                    }
+                }
+            }
+        };
+        if constexpr (kYUV) {
+            if ((ya >> 1) == (yb >> 1)) run(std::true_type{});
+            else run(std::false_type{});
+        } else {
+            run(std::false_type{});
+        }
+    }
+}
+
+// Staged uniform-geometry kernel. A workgroup owns a TW x TH tile (TW = 64 x NSEGX) and walks it in
+// groups of R output rows. For each group the source row segments its taps need (two luma rows and
+// two chroma rows per output row, each at most kSlot bytes wide) are brought into LDS by LDS-DMA —
+// one 16 B/lane buffer_load ... lds per row segment, the row offset in the SGPR offset — while the
+// previous group is being converted out of the other staging buffer. Taps are then LDS byte reads
+// with immediate slot offsets, so neither the staging nor the gather costs VALU address arithmetic,
+// and VMEM carries only wide loads and the planar stores. Only the stores and the DMA use vmcnt; the
+// wait for group g+1 is vmcnt(stores issued after it), so the stores are never drained in the loop.
+template <int FMT, int OUT, int R, int NSEGX>
+__global__ __launch_bounds__(kThreads) void evam_pp_staged(const SParams P) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    using T = FmtTraits<FMT>;
+    constexpr bool kYUV = FMT == kNV12 || FMT == kI420;
+    constexpr int NP = FMT == kI420 ? 3 : (FMT == kNV12 ? 2 : 1);  // staged planes
+    constexpr int NS = 2 * R * NP;                                   // slots per staging buffer
+    constexpr int RSTEP = 4 / NSEGX;                                 // waves sharing a column segment
+    constexpr int RPW = R / RSTEP;                                   // rows per wave per group
+    constexpr int kStores = 3 * RPW;                                 // stores per wave per full group
+    static_assert(R % RSTEP == 0, "R must be a multiple of 4 / NSEGX");
+    constexpr int TW = 64 * NSEGX;
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int t = blockIdx.x;
+    const int item = t / P.tiles_per_item;
+    const int tile = t - item * P.tiles_per_item;
+    const int ty = tile / P.tiles_x;
+    const int tx = tile - ty * P.tiles_x;
+    const __attribute__((address_space(4))) ItemDesc* it =
+        (const __attribute__((address_space(4))) ItemDesc*)(P.items) + item;
+    const __attribute__((address_space(4))) YTab* ytab = (const __attribute__((address_space(4))) YTab*)(P.ytab);
+    const __attribute__((address_space(4))) XTab* xtab_s = (const __attribute__((address_space(4))) XTab*)(P.xtab);
+    const uint8_t* p0 = it->plane[0];
+    const uint8_t* p1 = it->plane[1];
+    const uint8_t* p2 = it->plane[2];
+    const int pitch0 = it->pitch[0], pitch1 = it->pitch[1], pitch2 = it->pitch[2];
+    const int x0 = it->x0, y0 = it->y0, ox = it->ox, rw = it->rw;
+    const size_t plane = (size_t)P.DW * P.DH;
+    const size_t esz = OUT == 1 ? 4 : 1;
+    uint8_t* const d0 = reinterpret_cast<uint8_t*>(P.dst) + (size_t)it->slot * 3 * plane * esz;
+    uint8_t* const d1 = d0 + plane * esz;
+    uint8_t* const d2 = d1 + plane * esz;
+    const __amdgpu_buffer_rsrc_t rsY = __builtin_amdgcn_make_buffer_rsrc((void*)p0, (short)0, 0x7FFFFFFF, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsC = __builtin_amdgcn_make_buffer_rsrc((void*)(p1 ? p1 : p0), (short)0, 0x7FFFFFFF, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsV = __builtin_amdgcn_make_buffer_rsrc((void*)(p2 ? p2 : p0), (short)0, 0x7FFFFFFF, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsD0 = __builtin_amdgcn_make_buffer_rsrc((void*)d0, (short)0, 0x7FFFFFFF, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsD1 = __builtin_amdgcn_make_buffer_rsrc((void*)d1, (short)0, 0x7FFFFFFF, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsD2 = __builtin_amdgcn_make_buffer_rsrc((void*)d2, (short)0, 0x7FFFFFFF, 0x00020000);
+
+    float* lut_s = reinterpret_cast<float*>(smem);
+    if constexpr (OUT == 1) {
+        for (int i = tid; i < 768; i += kThreads) lut_s[i] = P.lut[i];
+    }
+    const int f0 = P.fill & 0xFF, f1 = (P.fill >> 8) & 0xFF, f2 = (P.fill >> 16) & 0xFF;
+
+    const int X0 = tx * TW, Y0 = ty * P.TH, Y1 = min(Y0 + P.TH, P.DH);
+    const int seg = wave % NSEGX, rph = wave / NSEGX;
+    // visible (non-padding) columns of the tile -> source footprint (wave-uniform)
+    const int Xv0 = max(X0, ox), Xv1 = min(min(X0 + TW, P.DW), ox + rw) - 1;
+    const bool cols = Xv0 <= Xv1;
+    int fsY = 0, nY = 0, fsC = 0, nC = 0;
+    if (cols) {
+        const int xa = x0 + xtab_s[Xv0].s0, xb = x0 + xtab_s[Xv1].s1;
+        fsY = (xa * T::bpp) & ~15;
+        nY = (((xb * T::bpp + T::bpp + 15) & ~15) - fsY) >> 4;
+        if constexpr (FMT == kNV12) {
+            fsC = (2 * (xa >> 1)) & ~15;
+            nC = (((2 * (xb >> 1) + 2 + 15) & ~15) - fsC) >> 4;
+        } else if constexpr (FMT == kI420) {
+            fsC = (xa >> 1) & ~15;
+            nC = ((((xb >> 1) + 1 + 15) & ~15) - fsC) >> 4;
+        }
+    }
+    // per-lane column state: LDS byte offsets of the taps inside a slot, weights
+    const int X = X0 + seg * 64 + lane;
+    const bool xin = X < P.DW;
+    uint32_t lY0 = 0, lY1 = 0, lC0 = 0, lC1 = 0, wa = 0;
+    {
+        const XTab xt = P.xtab[xin ? X : 0];
+        wa = (uint32_t)xt.a0 | ((uint32_t)xt.a1 << 16);
+        if (xin && wa != 0) {
+            const int ca = x0 + xt.s0, cb = x0 + xt.s1;
+            lY0 = (uint32_t)(ca * T::bpp - fsY);
+            lY1 = (uint32_t)(cb * T::bpp - fsY);
+            lC0 = FMT == kNV12 ? (uint32_t)(2 * (ca >> 1) - fsC) : (uint32_t)((ca >> 1) - fsC);
+            lC1 = FMT == kNV12 ? (uint32_t)(2 * (cb >> 1) - fsC) : (uint32_t)((cb >> 1) - fsC);
+        }
+    }
+    const uint32_t xo = (uint32_t)(xin ? X : 0) * (uint32_t)esz;
+    const bool wave_stores = X0 + seg * 64 < P.DW;  // some lane of this wave stores (wave-uniform)
+    const int rows = Y1 - Y0;
+    const int ngroups = (rows + R - 1) / R;
+
+    // ---- LDS-DMA of group g into buffer `buf` (slot s = plane * 2R + 2 * row + tap) ----
+    auto issue = [&](int g, uint8_t* buf) {
+        if (!cols) return;
+#pragma unroll
+        for (int s0 = 0; s0 < NS; s0 += 4) {
+            const int s = s0 + wave;
+            const int pl = s / (2 * R), loc = s - pl * 2 * R, r = loc >> 1, tap = loc & 1;
+            const int Y = Y0 + g * R + r;
+            if (Y >= Y1) continue;
+            const int b0 = ytab[Y].b0, b1 = ytab[Y].b1;
+            if ((b0 | b1) == 0) continue;  // padding row: nothing to stage
+            const int ya = y0 + ytab[Y].r0, yb = y0 + ytab[Y].r1;
+            const int yr = tap ? yb : ya;
+            if (pl > 0 && tap && (ya >> 1) == (yb >> 1)) continue;  // chroma row shared by both taps
+            const int nck = pl == 0 ? nY : nC;
+            if (lane < nck) {
+                __attribute__((address_space(3))) void* dstl =
+                    (__attribute__((address_space(3))) void*)(buf + s * kSlot);
+                if (pl == 0)
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsY, dstl, 16, lane * 16, yr * pitch0 + fsY, 0, 0);
+                else if (pl == 1)
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsC, dstl, 16, lane * 16, (yr >> 1) * pitch1 + fsC, 0, 0);
+                else
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsV, dstl, 16, lane * 16, (yr >> 1) * pitch2 + fsC, 0, 0);
+            }
+        }
+    };
+
+    // ---- convert + resize + normalise + store the rows of group g owned by this wave ----
+    auto compute = [&](int g, const uint8_t* buf) {
+#pragma unroll
+        for (int k = 0; k < RPW; k++) {
+            const int r = rph + k * RSTEP;
+            const int Y = Y0 + g * R + r;
+            if (Y >= Y1) continue;
+            const int b0 = ytab[Y].b0, b1 = ytab[Y].b1;
+            const int sO = (int)((uint32_t)(Y * P.DW) * (uint32_t)esz);
+            int v[3];
+            if ((b0 | b1) == 0 || wa == 0 || (P.ablate & 2)) {  // padding row / column
+                v[0] = f0; v[1] = f1; v[2] = f2;
+            } else {
+                const uint32_t a0 = wa & 0xFFFF, a1 = wa >> 16;  // 15-bit
+                const uint32_t wb0 = (uint32_t)b0, wb1 = (uint32_t)b1;
+                const uint8_t* sy0 = buf + (2 * r) * kSlot;
+                const uint8_t* sy1 = sy0 + kSlot;
+                const uint8_t* sc0 = buf + (2 * R + 2 * r) * kSlot;
+                int c[4][3];
+                if constexpr (kYUV) {
+                    const int ya = y0 + ytab[Y].r0, yb = y0 + ytab[Y].r1;
+                    const bool share = (ya >> 1) == (yb >> 1);
+                    const uint8_t* sc1 = share ? sc0 : sc0 + kSlot;
+                    Chroma<FMT> cA, cB, cC, cD;
+                    if constexpr (FMT == kNV12) {
+                        cA.u = *reinterpret_cast<const uint16_t*>(sc0 + lC0);
+                        cB.u = *reinterpret_cast<const uint16_t*>(sc0 + lC1);
+                        cC.u = *reinterpret_cast<const uint16_t*>(sc1 + lC0);
+                        cD.u = *reinterpret_cast<const uint16_t*>(sc1 + lC1);
+                    } else {
+                        const uint8_t* sv0 = sc0 + 2 * R * kSlot;
+                        const uint8_t* sv1 = sc1 + 2 * R * kSlot;
+                        cA.u = sc0[lC0]; cA.v = sv0[lC0];
+                        cB.u = sc0[lC1]; cB.v = sv0[lC1];
+                        cC.u = sc1[lC0]; cC.v = sv1[lC0];
+                        cD.u = sc1[lC1]; cD.v = sv1[lC1];
+                    }
+                    const UV3 tA = chroma_terms<FMT>(cA);
+                    const UV3 tB = chroma_terms<FMT>(cB);
+                    const UV3 tC = chroma_terms<FMT>(cC);
+                    const UV3 tD = chroma_terms<FMT>(cD);
+                    y_plus_uv((int)sy0[lY0], tA, c[0][0], c[0][1], c[0][2]);
+                    y_plus_uv((int)sy0[lY1], tB, c[1][0], c[1][1], c[1][2]);
+                    y_plus_uv((int)sy1[lY0], tC, c[2][0], c[2][1], c[2][2]);
+                    y_plus_uv((int)sy1[lY1], tD, c[3][0], c[3][1], c[3][2]);
+                } else {
+                    const uint8_t* rowp[2] = {sy0, sy1};
+#pragma unroll
+                    for (int q = 0; q < 4; q++) {
+                        const uint8_t* sp = rowp[q >> 1] + ((q & 1) ? lY1 : lY0);
+                        if constexpr (FMT == kBGRX) {
+                            const uint32_t px = *reinterpret_cast<const uint32_t*>(sp);
+                            c[q][0] = px & 0xFF; c[q][1] = (px >> 8) & 0xFF; c[q][2] = (px >> 16) & 0xFF;
+                        } else {
+                            c[q][0] = sp[0]; c[q][1] = sp[1]; c[q][2] = sp[2];
+                        }
+                    }
+                }
+#pragma unroll
+                for (int ch3 = 0; ch3 < 3; ch3++) {
+                    const uint32_t D0 = __umul24(c[0][ch3], a0) + __umul24(c[1][ch3], a1);
+                    const uint32_t D1 = __umul24(c[2][ch3], a0) + __umul24(c[3][ch3], a1);
+                    v[ch3] = vresize(D0, D1, wb0, wb1);
+                }
+                if (P.color_rgb) { const int tmp = v[0]; v[0] = v[2]; v[2] = tmp; }
+            }
+            if (!xin) continue;
+            if constexpr (OUT == 1) {
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lut_s[v[0]]), rsD0, xo, sO, 0);
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lut_s[256 + v[1]]), rsD1, xo, sO, 0);
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lut_s[512 + v[2]]), rsD2, xo, sO, 0);
+            } else {
+                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v[0], rsD0, xo, sO, 0);
+                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v[1], rsD1, xo, sO, 0);
+                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v[2], rsD2, xo, sO, 0);
+            }
+        }
+    };
+
+    uint8_t* const buf0 = smem + P.offBuf;
+    uint8_t* const buf1 = buf0 + P.buf_bytes;
+    issue(0, buf0);
+    for (int g = 0; g < ngroups; g++) {
+        // DMA of group g landed (this wave's share), while the previous group's stores stay in flight
+        // — unless that group was partial or its lanes skipped stores: then drain everything.
+        const bool prev_full = g > 0 && (g * R <= rows) && wave_stores;
+        if (prev_full) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(kStores) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();  // every wave's DMA for g landed; every wave done reading g-1
+        if (g + 1 < ngroups) issue(g + 1, (g & 1) ? buf0 : buf1);
+        compute(g, (g & 1) ? buf1 : buf0);
+    }
+}
+
 // ------------------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------------------
@@ -517,6 +1017,129 @@ TileCfg choose_tiles(int DW, int DH, int out_dtype) {
     return t;
 }
 
+struct TabCache {
+    int key[8] = {-1, -1, -1, -1, -1, -1, -1, -1};
+    std::vector<XTab> x;
+    std::vector<YTab> y;
+};
+
+// OpenCV coefficient tables for the uniform-geometry kernel, indexed by output column / row of the
+// DW x DH plane (padding columns / rows get zero weights). Cached: rebuilt only when the geometry changes.
+void build_tables(const Geom& g, int DW, int DH, TabCache& c, XTab* xt, YTab* yt) {
+    const int key[8] = {g.cw, g.ch, g.rw, g.rh, g.ox, g.oy, DW, DH};
+    if (memcmp(key, c.key, sizeof(key)) != 0) {
+        c.x.assign(DW, XTab{});
+        c.y.assign(DH, YTab{});
+        const double scx = 1. / ((double)g.rw / g.cw), scy = 1. / ((double)g.rh / g.ch);
+        for (int X = 0; X < DW; X++) {
+            const int dx = X - g.ox;
+            if (dx < 0 || dx >= g.rw) continue;  // padding: s0 = s1 = 0, weights 0
+            int sx, a0, a1;
+            linear_coef(dx, scx, g.cw, true, sx, a0, a1);
+            c.x[X].s0 = sx;
+            c.x[X].s1 = std::min(sx + 1, g.cw - 1);
+            c.x[X].a0 = (uint16_t)(a0 << 4);
+            c.x[X].a1 = (uint16_t)(a1 << 4);
+        }
+        for (int Y = 0; Y < DH; Y++) {
+            const int dy = Y - g.oy;
+            if (dy < 0 || dy >= g.rh) continue;
+            int sy, b0, b1;
+            linear_coef(dy, scy, g.ch, false, sy, b0, b1);
+            c.y[Y].r0 = std::min(std::max(sy, 0), g.ch - 1);
+            c.y[Y].r1 = std::min(std::max(sy + 1, 0), g.ch - 1);
+            c.y[Y].b0 = b0 << 8;
+            c.y[Y].b1 = b1 << 8;
+        }
+        memcpy(c.key, key, sizeof(key));
+    }
+    memcpy(xt, c.x.data(), sizeof(XTab) * DW);
+    memcpy(yt, c.y.data(), sizeof(YTab) * DH);
+}
+
+struct RowCfg {
+    int TW, TH;
+};
+
+// Row-kernel tile: TW in {512, 256, 128, 64} (whole 64-pixel segments; 4 waves split them) chosen for
+// the least padding lanes, and enough rows for ~4096 pixels per 256-thread workgroup.
+RowCfg choose_row_tiles(int DW, int DH) {
+    RowCfg r{512, 8};
+    int best = 1 << 30;
+    for (int tw : {512, 256, 128, 64}) {
+        const int waste = ((DW + tw - 1) / tw) * tw - DW;
+        if (waste < best) { best = waste; r.TW = tw; }
+    }
+    r.TW = env_int("EVAM_PP_TW", r.TW);
+    if (r.TW != 64 && r.TW != 128 && r.TW != 256 && r.TW != 512) r.TW = 512;
+    r.TH = std::max(1, std::min(DH, env_int("EVAM_PP_TH", 4096 / r.TW)));
+    return r;
+}
+
+template <int FMT, int OUT, int NSEGX>
+hipError_t launch_staged_t(const SParams& p, int grid, int lds, hipStream_t s) {
+    if constexpr (kStageRows % (4 / NSEGX) == 0) {
+        hipLaunchKernelGGL((evam_pp_staged<FMT, OUT, kStageRows, NSEGX>), dim3(grid), dim3(kThreads), lds, s, p);
+        return hipGetLastError();
+    } else {
+        return hipErrorInvalidValue;  // never selected: staged_nsegx() only returns compatible widths
+    }
+}
+
+template <int FMT, int OUT>
+hipError_t launch_staged_n(int nsegx, const SParams& p, int grid, int lds, hipStream_t s) {
+    switch (nsegx) {
+    case 4: return launch_staged_t<FMT, OUT, 4>(p, grid, lds, s);
+    case 2: return launch_staged_t<FMT, OUT, 2>(p, grid, lds, s);
+    default: return launch_staged_t<FMT, OUT, 1>(p, grid, lds, s);
+    }
+}
+
+hipError_t launch_staged(int f, int out, int nsegx, const SParams& p, int grid, int lds, hipStream_t s) {
+    switch (f * 2 + out) {
+    case kNV12 * 2 + 0: return launch_staged_n<kNV12, 0>(nsegx, p, grid, lds, s);
+    case kNV12 * 2 + 1: return launch_staged_n<kNV12, 1>(nsegx, p, grid, lds, s);
+    case kI420 * 2 + 0: return launch_staged_n<kI420, 0>(nsegx, p, grid, lds, s);
+    case kI420 * 2 + 1: return launch_staged_n<kI420, 1>(nsegx, p, grid, lds, s);
+    case kBGRX * 2 + 0: return launch_staged_n<kBGRX, 0>(nsegx, p, grid, lds, s);
+    case kBGRX * 2 + 1: return launch_staged_n<kBGRX, 1>(nsegx, p, grid, lds, s);
+    case kBGR * 2 + 0: return launch_staged_n<kBGR, 0>(nsegx, p, grid, lds, s);
+    default: return launch_staged_n<kBGR, 1>(nsegx, p, grid, lds, s);
+    }
+}
+
+// Staged kernel geometry: the widest column segment count whose worst-case source footprint fits a
+// kSlot-byte LDS row slot. Returns 0 when none does (the direct row kernel is used instead).
+int staged_nsegx(int f, double ratio) {
+    const int bpp = fmt_bpp(f);
+    for (int n : {4, 2, 1}) {
+        if (kStageRows % (4 / n) != 0) continue;
+        const int tw = 64 * n;
+        const int span = (int)std::ceil((tw - 1) * ratio) + 3;  // source columns touched by one tile row
+        if (span * bpp + 32 <= kSlot) return n;
+    }
+    return 0;
+}
+
+template <int FMT, int OUT>
+hipError_t launch_rows_t(const RParams& p, int grid, int lds, hipStream_t s) {
+    hipLaunchKernelGGL((evam_pp_rows<FMT, OUT>), dim3(grid), dim3(kThreads), lds, s, p);
+    return hipGetLastError();
+}
+
+hipError_t launch_rows(int f, int out, const RParams& p, int grid, int lds, hipStream_t s) {
+    switch (f * 2 + out) {
+    case kNV12 * 2 + 0: return launch_rows_t<kNV12, 0>(p, grid, lds, s);
+    case kNV12 * 2 + 1: return launch_rows_t<kNV12, 1>(p, grid, lds, s);
+    case kI420 * 2 + 0: return launch_rows_t<kI420, 0>(p, grid, lds, s);
+    case kI420 * 2 + 1: return launch_rows_t<kI420, 1>(p, grid, lds, s);
+    case kBGRX * 2 + 0: return launch_rows_t<kBGRX, 0>(p, grid, lds, s);
+    case kBGRX * 2 + 1: return launch_rows_t<kBGRX, 1>(p, grid, lds, s);
+    case kBGR * 2 + 0: return launch_rows_t<kBGR, 0>(p, grid, lds, s);
+    default: return launch_rows_t<kBGR, 1>(p, grid, lds, s);
+    }
+}
+
 template <int FMT, int OUT>
 hipError_t launch_t(const KParams& p, int grid, int lds, hipStream_t s) {
     hipLaunchKernelGGL((evam_pp_kernel<FMT, OUT>), dim3(grid), dim3(kThreads), lds, s, p);
@@ -550,6 +1173,7 @@ struct evam_pp {
     std::vector<uint8_t> h_block, h_last;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool timed = false;
+    TabCache tab_cache;
 };
 
 extern "C" {
@@ -713,8 +1337,28 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
         if (h->opt_stats) src_bytes += item_src_bytes(fmt[i], geo[i], DW, DH);
     }
 
-    // ---- descriptor block ----
-    const size_t nbytes = kLutBytes + sizeof(ItemDesc) * (size_t)n_items;
+    // ---- uniform geometry per format group -> row kernel with host-built tables ----
+    bool uniform[4] = {true, true, true, true};
+    int rep[4] = {-1, -1, -1, -1};
+    for (int i = 0; i < n_items; i++) {
+        const int f = fmt[i];
+        if (rep[f] < 0) { rep[f] = i; continue; }
+        const Geom& a = geo[rep[f]];
+        const Geom& b = geo[i];
+        if (a.cw != b.cw || a.ch != b.ch || a.rw != b.rw || a.rh != b.rh || a.ox != b.ox || a.oy != b.oy)
+            uniform[f] = false;
+    }
+    const bool rows_enabled = env_int("EVAM_PP_ROWS", 1) != 0;
+
+    // ---- descriptor block: [LUT][items][per-group xtab (DW) + ytab (DH)] ----
+    const size_t items_bytes = sizeof(ItemDesc) * (size_t)n_items;
+    size_t tab_off[4] = {0, 0, 0, 0};
+    size_t nbytes = kLutBytes + items_bytes;
+    for (int f = 0; f < 4; f++) {
+        if (!count[f] || !uniform[f] || !rows_enabled) continue;
+        tab_off[f] = nbytes;
+        nbytes += sizeof(XTab) * (size_t)DW + sizeof(YTab) * (size_t)DH;
+    }
     h->h_block.assign(nbytes, 0);
     if (cfg->out_dtype == EVAM_DTYPE_F32) build_lut(*cfg, reinterpret_cast<float*>(h->h_block.data()));
     ItemDesc* desc = reinterpret_cast<ItemDesc*>(h->h_block.data() + kLutBytes);
@@ -734,6 +1378,11 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
             d.pad_ = 0;
             d.scale_x = 1. / ((double)g.rw / g.cw);
             d.scale_y = 1. / ((double)g.rh / g.ch);
+        }
+        if (tab_off[f]) {
+            XTab* xt = reinterpret_cast<XTab*>(h->h_block.data() + tab_off[f]);
+            YTab* yt = reinterpret_cast<YTab*>(xt + DW);
+            build_tables(geo[rep[f]], DW, DH, h->tab_cache, xt, yt);
         }
     }
 
@@ -761,6 +1410,58 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
     int launches = 0;
     for (int f = 0; f < 4; f++) {
         if (!count[f]) continue;
+        const int nsegx = tab_off[f] && env_int("EVAM_PP_STAGED", 1) ? staged_nsegx(f, max_ratio[f]) : 0;
+        if (nsegx) {
+            SParams sp{};
+            sp.items = reinterpret_cast<const ItemDesc*>(h->d_block + kLutBytes) + first[f];
+            sp.lut = reinterpret_cast<const float*>(h->d_block);
+            sp.xtab = reinterpret_cast<const XTab*>(h->d_block + tab_off[f]);
+            sp.ytab = reinterpret_cast<const YTab*>(sp.xtab + DW);
+            sp.dst = dst->data;
+            sp.DW = DW; sp.DH = DH;
+            const int tw = 64 * nsegx;
+            sp.TH = std::max(1, std::min(DH, env_int("EVAM_PP_TH", std::max(kStageRows, 4096 / tw))));
+            sp.TH = (sp.TH + kStageRows - 1) / kStageRows * kStageRows;
+            sp.tiles_x = (DW + tw - 1) / tw;
+            sp.tiles_per_item = sp.tiles_x * ((DH + sp.TH - 1) / sp.TH);
+            const int np = f == kI420 ? 3 : (f == kNV12 ? 2 : 1);
+            sp.offBuf = cfg->out_dtype == EVAM_DTYPE_F32 ? kLutBytes : 0;
+            sp.buf_bytes = 2 * kStageRows * np * kSlot;
+            sp.color_rgb = cfg->color_order == EVAM_COLOR_RGB;
+            sp.fill = (uint32_t)cfg->fill[0] | ((uint32_t)cfg->fill[1] << 8) | ((uint32_t)cfg->fill[2] << 16);
+            sp.ablate = env_int("EVAM_PP_ABLATE", 0);
+            const int64_t grid = (int64_t)count[f] * sp.tiles_per_item;
+            if (grid > 0x7FFFFFFF) return fail(EVAM_PP_ERR_INVALID_ARG, "evam_pp_run: too many tiles");
+            const int lds = sp.offBuf + 2 * sp.buf_bytes;
+            hipError_t e = launch_staged(f, cfg->out_dtype, nsegx, sp, (int)grid, lds, h->stream);
+            if (e != hipSuccess) return fail(EVAM_PP_ERR_HIP, "kernel launch failed: %s", hipGetErrorString(e));
+            launches++;
+            continue;
+        }
+        if (tab_off[f]) {
+            const RowCfg rc = choose_row_tiles(DW, DH);
+            RParams r{};
+            r.items = reinterpret_cast<const ItemDesc*>(h->d_block + kLutBytes) + first[f];
+            r.lut = reinterpret_cast<const float*>(h->d_block);
+            r.xtab = reinterpret_cast<const XTab*>(h->d_block + tab_off[f]);
+            r.ytab = reinterpret_cast<const YTab*>(r.xtab + DW);
+            r.dst = dst->data;
+            r.DW = DW; r.DH = DH;
+            r.TW = rc.TW; r.TH = rc.TH;
+            r.tiles_x = (DW + rc.TW - 1) / rc.TW;
+            r.tiles_per_item = r.tiles_x * ((DH + rc.TH - 1) / rc.TH);
+            r.nsegx = rc.TW / 64;
+            r.color_rgb = cfg->color_order == EVAM_COLOR_RGB;
+            r.fill = (uint32_t)cfg->fill[0] | ((uint32_t)cfg->fill[1] << 8) | ((uint32_t)cfg->fill[2] << 16);
+            r.ablate = env_int("EVAM_PP_ABLATE", 0);
+            const int64_t grid = (int64_t)count[f] * r.tiles_per_item;
+            if (grid > 0x7FFFFFFF) return fail(EVAM_PP_ERR_INVALID_ARG, "evam_pp_run: too many tiles");
+            const int lds = cfg->out_dtype == EVAM_DTYPE_F32 ? kLutBytes : 0;
+            hipError_t e = launch_rows(f, cfg->out_dtype, r, (int)grid, lds, h->stream);
+            if (e != hipSuccess) return fail(EVAM_PP_ERR_HIP, "kernel launch failed: %s", hipGetErrorString(e));
+            launches++;
+            continue;
+        }
         const TileCfg t = choose_tiles(DW, DH, cfg->out_dtype);
         KParams p{};
         p.items = reinterpret_cast<const ItemDesc*>(h->d_block + kLutBytes) + first[f];
