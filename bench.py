@@ -164,8 +164,9 @@ def main():
 
     wl = WORKLOADS[args.config]
     n = args.frames or wl["frames"]
-    if args.config == "c4" and world > 1:
-        n = max(1, wl["frames"] // world)  # 64 streams partitioned s mod G (strong split of a fixed stream set)
+    strong = args.config == "c4" and world > 1 and not args.frames
+    if strong:  # C4 is a fixed set of 64 streams, partitioned s mod G (strong split)
+        n = len(evam.streams.streams_for_rank(wl["frames"], world, rank))
     imgs = device_frames(evam, torch, wl, n, device, seed=1234 + rank)
     batch = evam.ImageBatch(imgs)
     info = make_info(evam, wl)
@@ -212,17 +213,10 @@ def main():
         dist.barrier()
     wall = time.perf_counter() - t0
     kern_ms = e0.elapsed_time(e1) / args.steps  # one launch per step
-    el = torch.tensor([wall], dtype=torch.float64, device=device)
-    if world > 1:
-        dist.all_reduce(el, op=dist.ReduceOp.MAX)
-        # optional stats all-gather (frames, bytes, ns) — after timing, never in the hot loop
-        mine = torch.tensor([n * args.steps, alg_bytes * args.steps, int(kern_ms * args.steps * 1e6)],
-                            dtype=torch.int64, device=device)
-        allst = [torch.zeros_like(mine) for _ in range(world)]
-        dist.all_gather(allst, mine)
-    wall_max = float(el.item())
-    total_frames = n * world * args.steps
-    value = total_frames / wall_max
+    tot = evam.streams.reduce_run(wall, n * args.steps, alg_bytes * args.steps,
+                                  device=device if world > 1 else None)
+    wall_max = tot.elapsed_max_s
+    value = tot.frames / wall_max
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
     traffic = load_pmc_traffic(args.config, n)
 
@@ -236,7 +230,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(wall_max / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
             "dtype": "u8" if wl["dtype"] == "u8" else "u8->f32",
             "data": "synthetic (seeded uniform u8 planes generated on device; no video decode)",

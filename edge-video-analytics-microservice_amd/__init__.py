@@ -17,5 +17,6 @@ from ._native import PreProcError, load_library  # noqa: F401
 from .preproc import (HipPreProcessor, Image, ImageBatch, PreProcInfo, Roi, Transform,  # noqa: F401
                       create_preprocessor, plane_layout)
 from . import _native as native  # noqa: F401
+from . import streams  # noqa: F401
 
 _sys.modules.setdefault("evam_amd", _sys.modules[__name__])
