@@ -60,6 +60,16 @@ CASES = {
     # top-left letterbox of a portrait NV12 ROI with per-channel fill
     "nv12_roi_letterbox_u8": ([("NV12", 64, 64, "gradient")], [(0, 6, 2, 18, 50), (0, 30, 40, 30, 10)],
                               dict(resize="aspect-ratio", fill=(1, 2, 3)), (32, 32), "u8"),
+    # SURVEY.md §8c size/ratio grid: 64x48 and 66x50 4:2:0 (odd chroma edge), BGRx 40x30;
+    # resize ratios < 1, 1, 2 (INTER_AREA special case), ~3.75 and 6
+    "nv12_64x48_ratio1_u8": ([("NV12", 64, 48, "uniform")], None, {}, (64, 48), "u8"),
+    "nv12_64x48_ratio2_u8": ([("NV12", 64, 48, "uniform")], None, {}, (32, 24), "u8"),
+    "i420_66x50_ratio3p75_u8": ([("I420", 66, 50, "uniform")], None, {}, (18, 13), "u8"),
+    "nv12_66x50_ratio6_f32": ([("NV12", 66, 50, "gradient")], None, dict(IMAGENET_BGR), (11, 8), "f32"),
+    "i420_64x48_upscale_f32": ([("I420", 64, 48, "gradient")], None, dict(range=(-1.0, 1.0)), (150, 112), "f32"),
+    "bgrx_40x30_rois_u8": ([("BGRX", 40, 30, "uniform")],
+                           [(0, 0, 0, 40, 30), (0, 39, 29, 5, 5), (0, 3, 5, 7, 9), (0, 20, -3, 30, 12)],
+                           {}, (16, 16), "u8"),
 }
 
 FOURCC = {"NV12": O.NV12, "I420": O.I420, "BGRX": O.BGRX, "BGR": O.BGR}
