@@ -1,0 +1,709 @@
+"""Pipeline-server counterpart: the direct caller of the pre-process path.
+
+EVAM drives pipelines through the DL Streamer Pipeline Server API (``evas/manager.py:100-155``):
+
+    PipelineServer.start({'log_level': ..., 'ignore_init_errors': True})
+    pipeline = PipelineServer.pipeline(name, version)
+    pipeline.start(source=src, destination=dest, parameters=model_params)
+    PipelineServer.wait();  PipelineServer.stop()
+
+This module exposes the same API over the reference's own ``pipelines/<name>/<version>/pipeline.json``
+templates. Loading a template covers:
+- ``{models[alias][version][network|proc]}`` and ``{env[VAR]}`` are resolved;
+- the launch string is parsed into elements;
+- the request's ``parameters`` are validated against the template schema and mapped onto element
+  properties. All schema forms of SURVEY.md §8b are handled:
+  - ``"element": "<name>"``;
+  - ``{"name", "property"}``;
+  - a list of those (fan-out);
+  - ``{"name", "format": "element-properties"}`` (dict passthrough);
+  - ``"format": "json"``;
+  - defaults, including ``{env[VAR]}``.
+
+The inference elements are ``gvadetect``, ``gvaclassify`` and ``gvaactionrecognitionbin``. Each one
+with ``pre-process-backend=hip`` gets a ``HipPreProcessor``; ``hip`` is also the default when the
+property is absent. Each element then runs:
+1. batched frame or ROI pre-processing on the GPU;
+2. the registered model (a torch callable: OpenVINO is not part of this stack);
+3. post-processing (``postproc.py``: transform-mapped boxes, ``tensor_to_label``, gvametaconvert JSON).
+
+Decode stays upstream. An ``application`` source delivers decoded frames:
+device ``Image``s, or host planes uploaded on arrival.
+"""
+from __future__ import annotations
+
+import json
+import os
+import queue
+import re
+import shlex
+import threading
+import time
+import xml.etree.ElementTree as ET
+from dataclasses import dataclass, field
+
+from . import _native as N
+from . import postproc as P
+from ._native import PreProcError
+
+INFERENCE_ELEMENTS = ("gvadetect", "gvaclassify", "gvaactionrecognitionbin", "gvainference")
+HIP_BACKENDS = ("hip",)
+# backends DL Streamer 2022.1 accepts that only the reference implements
+REFERENCE_ONLY_BACKENDS = ("ie", "opencv", "vaapi", "vaapi-surface-sharing")
+
+
+# ------------------------------------------------------------------------------------------------
+# Template handling
+# ------------------------------------------------------------------------------------------------
+@dataclass
+class Element:
+    """One element of a GStreamer launch string: ``factory prop=value ...`` or a caps filter."""
+
+    factory: str
+    properties: dict = field(default_factory=dict)
+    caps: str | None = None
+
+    @property
+    def name(self) -> str | None:
+        return self.properties.get("name")
+
+
+class _Fmt(dict):
+    """str.format mapping that leaves unknown top-level fields (e.g. {auto_source}) in place."""
+
+    def __missing__(self, key):
+        return "{" + key + "}"
+
+
+class _EnvLookup:
+    def __getitem__(self, key):
+        return os.environ.get(key, "")
+
+
+def resolve_template(template, models: dict, extra: dict | None = None) -> str:
+    """Join a template (str or list of str) and substitute ``{models[..]..}``, ``{env[..]}`` and extras."""
+    text = "".join(template) if isinstance(template, (list, tuple)) else str(template)
+
+    def sub(m):
+        expr = m.group(1)
+        root = expr.split("[", 1)[0]
+        if root == "models":
+            keys = re.findall(r"\[([^\]]+)\]", expr)
+            node = models
+            for k in keys:
+                if not isinstance(node, dict) or k not in node:
+                    raise KeyError(f"model reference {{{expr}}} not found")
+                node = node[k]
+            return str(node)
+        if root == "env":
+            return os.environ.get(re.findall(r"\[([^\]]+)\]", expr)[0], "")
+        if extra is not None and expr in extra:
+            return str(extra[expr])
+        return m.group(0)
+
+    return re.sub(r"\{([A-Za-z_][^{}]*)\}", sub, text)
+
+
+def parse_launch(text: str) -> list[Element]:
+    """Split a gst-launch string on ``!`` into elements; ``key=value`` tokens become properties."""
+    elems = []
+    for part in text.split("!"):
+        part = part.strip()
+        if not part:
+            continue
+        toks = shlex.split(part)
+        head = toks[0]
+        if "/" in head and "=" not in head.split(",", 1)[0]:     # caps filter, e.g. video/x-raw,format=BGRx
+            elems.append(Element("capsfilter", {}, caps=part))
+            continue
+        props = {}
+        for t in toks[1:]:
+            if "=" in t:
+                k, v = t.split("=", 1)
+                props[k] = v
+        elems.append(Element(head, props))
+    return elems
+
+
+def _type_ok(value, typ) -> bool:
+    if typ is None:
+        return True
+    if isinstance(typ, list):
+        return any(_type_ok(value, t) for t in typ)
+    return {"string": lambda v: isinstance(v, str),
+            "integer": lambda v: isinstance(v, int) and not isinstance(v, bool),
+            "number": lambda v: isinstance(v, (int, float)) and not isinstance(v, bool),
+            "boolean": lambda v: isinstance(v, bool),
+            "object": lambda v: isinstance(v, dict),
+            "array": lambda v: isinstance(v, list)}.get(typ, lambda v: True)(value)
+
+
+def _expand_default(value):
+    """``{env[VAR]}`` defaults: the variable's value, or None (property left unset) if it is empty."""
+    if isinstance(value, str):
+        m = re.fullmatch(r"\{env\[([^\]]+)\]\}", value)
+        if m:
+            return os.environ.get(m.group(1)) or None
+    return value
+
+
+def apply_parameters(elements: list[Element], schema: dict | None, parameters: dict | None) -> dict:
+    """Validate ``parameters`` against the template schema and set element properties.
+
+    Returns the effective parameter dict (request values plus defaults). Raises ValueError for an
+    unknown parameter or a type mismatch, as the reference's schema validation does.
+    """
+    props = (schema or {}).get("properties", {})
+    parameters = dict(parameters or {})
+    unknown = sorted(set(parameters) - set(props))
+    if unknown:
+        raise ValueError(f"unknown pipeline parameter(s): {unknown}")
+    by_name = {e.name: e for e in elements if e.name}
+    effective = {}
+    for key, spec in props.items():
+        if key in parameters:
+            value = parameters[key]
+            if not _type_ok(value, spec.get("type")):
+                raise ValueError(f"parameter {key!r}: expected {spec.get('type')}, got {type(value).__name__}")
+            if "enum" in spec and value not in spec["enum"]:
+                raise ValueError(f"parameter {key!r}: {value!r} not in {spec['enum']}")
+        elif "default" in spec:
+            value = _expand_default(spec["default"])
+            if value is None:
+                continue
+        else:
+            continue
+        effective[key] = value
+        targets = spec.get("element")
+        if targets is None:
+            continue
+        for tgt in targets if isinstance(targets, list) else [targets]:
+            if isinstance(tgt, str):
+                tgt = {"name": tgt}
+            el = by_name.get(tgt["name"])
+            if el is None:
+                raise ValueError(f"parameter {key!r} targets unknown element {tgt['name']!r}")
+            fmt = tgt.get("format")
+            if fmt == "element-properties":
+                if not isinstance(value, dict):
+                    raise ValueError(f"parameter {key!r}: element-properties needs an object")
+                for k, v in value.items():
+                    el.properties[k] = v
+            elif fmt == "json":
+                el.properties[tgt.get("property", key)] = json.dumps(value)
+            else:
+                el.properties[tgt.get("property", key)] = value
+    return effective
+
+
+# ------------------------------------------------------------------------------------------------
+# Models
+# ------------------------------------------------------------------------------------------------
+@dataclass
+class InferenceModel:
+    """A model bound to a network path: a torch callable over the pre-processed NCHW batch.
+
+    ``fn(tensor) -> output``: for detection, an SSD ``DetectionOutput`` blob ``[N, K, 7]`` (boxes
+    normalized to the input tensor). For classification, a dict ``{layer_name: [N, C]}`` or one
+    ``[N, C]`` tensor. ``input_size`` is ``(W, H)``. Labels and pre-processing come from the
+    model-proc (``models_list/*.json``).
+    """
+
+    fn: object
+    input_size: tuple
+    model_proc: dict | None = None
+    out_dtype: str = "f32"
+    name: str | None = None
+
+    def preproc_info(self, overrides: dict | None = None):
+        from .preproc import PreProcInfo
+
+        entry = None
+        if self.model_proc:
+            for e in self.model_proc.get("input_preproc", []):
+                if e.get("format", "image") == "image":
+                    entry = e
+                    break
+        info = PreProcInfo.from_model_proc(entry)
+        for k, v in (overrides or {}).items():
+            setattr(info, k, v)
+        return info
+
+    def postprocs(self):
+        return list((self.model_proc or {}).get("output_postproc", []))
+
+
+def ir_input_size(xml_path: str):
+    """(W, H) of an OpenVINO IR's first image input (``<layer type="Parameter">`` NCHW shape)."""
+    root = ET.parse(xml_path).getroot()
+    for layer in root.iter("layer"):
+        if layer.get("type") == "Parameter":
+            data = layer.find("data")
+            shape = data.get("shape") if data is not None else None
+            if shape:
+                dims = [int(d) for d in shape.split(",")]
+            else:
+                dims = [int(d.text) for d in layer.find("output").find("port").findall("dim")]
+            if len(dims) == 4:
+                return dims[3], dims[2]
+    raise ValueError(f"{xml_path}: no 4-D input layer")
+
+
+def scan_models(model_dir: str, precisions=("FP32", "FP16", "INT8")) -> dict:
+    """``{alias: {version: {"network": xml, "proc": json, "<precision>": xml}}}`` from a model tree.
+
+    Layout as the reference's model downloader writes it (``tools/model_downloader``):
+    ``<model_dir>/<alias>/<version>/<precision>/<model>.xml`` plus an optional ``<model>.json`` proc.
+    """
+    models: dict = {}
+    if not model_dir or not os.path.isdir(model_dir):
+        return models
+    for alias in sorted(os.listdir(model_dir)):
+        adir = os.path.join(model_dir, alias)
+        if not os.path.isdir(adir):
+            continue
+        for version in sorted(os.listdir(adir)):
+            vdir = os.path.join(adir, version)
+            if not os.path.isdir(vdir):
+                continue
+            entry = {}
+            for f in sorted(os.listdir(vdir)):
+                p = os.path.join(vdir, f)
+                if f.endswith(".json"):
+                    entry["proc"] = p
+                elif os.path.isdir(p):
+                    xml = [x for x in sorted(os.listdir(p)) if x.endswith(".xml")]
+                    if xml:
+                        entry[f] = os.path.join(p, xml[0])
+            for prec in precisions:
+                if prec in entry:
+                    entry["network"] = entry[prec]
+                    break
+            if entry:
+                models.setdefault(alias, {})[version] = entry
+    return models
+
+
+# ------------------------------------------------------------------------------------------------
+# Stages
+# ------------------------------------------------------------------------------------------------
+def _backend_of(el: Element) -> str:
+    b = str(el.properties.get("pre-process-backend", "hip"))
+    if b in HIP_BACKENDS:
+        return b
+    if b in REFERENCE_ONLY_BACKENDS:
+        raise PreProcError(N.ERR_UNSUPPORTED, f"{el.name or el.factory}: pre-process-backend={b!r} is the "
+                                              "reference's CPU/VA path; this build provides 'hip'")
+    raise PreProcError(N.ERR_UNSUPPORTED, f"{el.name or el.factory}: unknown pre-process-backend {b!r}")
+
+
+class _InferenceStage:
+    """Common part of gvadetect / gvaclassify: interval gating, model lookup, HIP pre-processor."""
+
+    def __init__(self, el: Element, server, device: int):
+        self.el = el
+        self.backend = _backend_of(el)
+        self.device = device
+        net = el.properties.get("model") or el.properties.get("enc-model")
+        self.model = server.model_for(net)
+        if self.model is None:
+            raise RuntimeError(f"{el.name or el.factory}: no model registered for {net!r} "
+                               "(PipelineServer.register_model)")
+        mp = el.properties.get("model-proc")
+        if mp and self.model.model_proc is None and os.path.exists(mp):
+            self.model.model_proc = json.load(open(mp))
+        self.interval = int(el.properties.get("inference-interval", 1))
+        self.threshold = float(el.properties.get("threshold", 0.5))
+        self.batch_size = int(el.properties.get("batch-size", 1))
+        self._pp = None
+        self.info = self.model.preproc_info()
+
+    def pp(self):
+        if self._pp is None:
+            from .preproc import HipPreProcessor
+
+            self._pp = HipPreProcessor(device=self.device)
+        return self._pp
+
+    def close(self):
+        if self._pp is not None:
+            self._pp.close()
+            self._pp = None
+
+    def _tensor(self, n):
+        import torch
+
+        W, H = self.model.input_size
+        dt = torch.float32 if self.model.out_dtype == "f32" else torch.uint8
+        return torch.empty((n, 3, H, W), dtype=dt, device=f"cuda:{self.device}")
+
+
+class DetectStage(_InferenceStage):
+    def process(self, items):
+        """items: list of (frame_index, Image, FrameResult). Appends regions to each FrameResult."""
+        run = [it for it in items if it[0] % self.interval == 0]
+        if not run:
+            return
+        out = self._tensor(len(run))
+        xfs = self.pp().convert([img for _, img, _ in run], out, self.info, want_transform=True)
+        raw = self.model.fn(out)
+        raw = raw.detach().float().cpu().numpy() if hasattr(raw, "detach") else raw
+        W, H = self.model.input_size
+        labels = None
+        for pp_ in self.model.postprocs():
+            labels = pp_.get("labels", labels)
+        for k, (_, img, fr) in enumerate(run):
+            dets = P.parse_ssd(raw[k], self.threshold)
+            fr.regions.extend(P.detections_to_regions(dets, xfs[k], img.width, img.height, W, H, labels,
+                                                      model=self.model.name))
+
+
+class ClassifyStage(_InferenceStage):
+    def __init__(self, el, server, device):
+        super().__init__(el, server, device)
+        oc = el.properties.get("object-class")
+        self.object_class = set(str(oc).split(",")) if oc else None
+        self.reclassify = int(el.properties.get("reclassify-interval", 1))
+
+    def process(self, items):
+        from .preproc import Roi
+
+        frames, rois, owners = [], [], []
+        for fi, img, fr in items:
+            if fi % self.interval:
+                continue
+            idx = len(frames)
+            frames.append(img)
+            for r in fr.regions:
+                if self.object_class is None or r.label in self.object_class:
+                    rois.append(Roi(idx, r.x, r.y, r.w, r.h))
+                    owners.append(r)
+        if not rois:
+            return
+        out = self._tensor(len(rois))
+        self.pp().convert(frames, out, self.info, rois=rois)
+        res = self.model.fn(out)
+        posts = self.model.postprocs() or [{}]
+        if not isinstance(res, dict):
+            res = {posts[0].get("layer_name", "classification"): res}
+        for pp_ in posts:
+            layer = pp_.get("layer_name") or next(iter(res))
+            logits = res[layer]
+            logits = logits.detach().float().cpu().numpy() if hasattr(logits, "detach") else logits
+            name = pp_.get("attribute_name", layer)
+            tens = P.classify(logits, pp_.get("labels"), pp_.get("method", "max"), name, model=self.model.name)
+            for r, t in zip(owners, tens):
+                r.tensors.append(t)
+
+
+class ActionRecognitionStage(_InferenceStage):
+    """gvaactionrecognitionbin encoder input: aspect+central-crop into a 16-slot per-stream clip ring."""
+
+    CLIP = 16
+
+    def __init__(self, el, server, device):
+        super().__init__(el, server, device)
+        self.ring = None
+        self.t = 0
+        dec = el.properties.get("dec-model")
+        self.decoder = server.model_for(dec) if dec else None
+        mp = el.properties.get("model-proc")
+        self.dec_proc = json.load(open(mp)) if mp and os.path.exists(mp) else None
+        if self.dec_proc:  # the decoder's model-proc carries the encoder's input_preproc too
+            self.info = InferenceModel(None, self.model.input_size, self.dec_proc).preproc_info()
+
+    def process(self, items):
+        import torch
+
+        W, H = self.model.input_size
+        for fi, img, fr in items:
+            if self.ring is None:
+                self.ring = torch.zeros((self.CLIP, 3, H, W), dtype=torch.float32, device=f"cuda:{self.device}")
+            self.pp().convert([img], self.ring, self.info, slot_offset=self.t % self.CLIP, slot_stride=1)
+            self.t += 1
+            if self.t >= self.CLIP and self.decoder is not None and fi % self.interval == 0:
+                order = [(self.t + k) % self.CLIP for k in range(self.CLIP)]   # oldest first
+                logits = self.decoder.fn(self.model.fn(self.ring[order]))
+                logits = logits.detach().float().cpu().numpy() if hasattr(logits, "detach") else logits
+                post = (self.dec_proc or {}).get("output_postproc", [{}])[0]
+                t = P.classify(logits.reshape(1, -1), post.get("labels"), post.get("method", "softmax"),
+                               post.get("attribute_name", "action"), model=self.decoder.name)[0]
+                fr.tensors.append(t)
+
+
+STAGES = {"gvadetect": DetectStage, "gvaclassify": ClassifyStage, "gvainference": DetectStage,
+          "gvaactionrecognitionbin": ActionRecognitionStage}
+
+
+# ------------------------------------------------------------------------------------------------
+# Pipelines
+# ------------------------------------------------------------------------------------------------
+@dataclass
+class PipelineDefinition:
+    name: str
+    version: str
+    path: str
+    type: str
+    template: object
+    description: str = ""
+    parameters: dict = field(default_factory=dict)
+
+    @classmethod
+    def load(cls, path: str, name: str, version: str) -> "PipelineDefinition":
+        d = json.load(open(path))
+        return cls(name, version, path, d.get("type", "GStreamer"), d.get("template", ""),
+                   d.get("description", ""), d.get("parameters", {}))
+
+
+class Pipeline:
+    """One pipeline instance (``PipelineServer.pipeline(name, version)``)."""
+
+    QUEUED, RUNNING, COMPLETED, ERROR, ABORTED = "QUEUED", "RUNNING", "COMPLETED", "ERROR", "ABORTED"
+
+    def __init__(self, server: "_Server", definition: PipelineDefinition, instance_id: int):
+        self.server = server
+        self.definition = definition
+        self.id = instance_id
+        self.state = self.QUEUED
+        self.error = None
+        self.elements: list[Element] = []
+        self.parameters: dict = {}
+        self.stages: list = []
+        self.frames = 0
+        self.start_time = None
+        self.end_time = None
+        self._thread = None
+        self._stop = threading.Event()
+
+    # -- construction ------------------------------------------------------------------------
+    def build(self, source=None, parameters=None):
+        src = source or {}
+        auto = {"uri": "urisourcebin uri={}".format(src.get("uri", "")),
+                "application": "appsrc name=source", "gst": src.get("element", "")}.get(src.get("type"),
+                                                                                       "appsrc name=source")
+        text = resolve_template(self.definition.template, self.server.models, {"auto_source": auto})
+        self.elements = parse_launch(text)
+        self.parameters = apply_parameters(self.elements, self.definition.parameters, parameters)
+        for el in self.elements:
+            if "model" in el.properties and "model-proc" not in el.properties:
+                proc = self.server.proc_for(el.properties["model"])
+                if proc:
+                    el.properties["model-proc"] = proc
+        return self
+
+    def element(self, name: str) -> Element | None:
+        return next((e for e in self.elements if e.name == name), None)
+
+    def backends(self) -> dict:
+        """{element name: pre-process backend} for the inference elements."""
+        return {(e.name or e.factory): _backend_of(e) for e in self.elements if e.factory in INFERENCE_ELEMENTS}
+
+    # -- execution ---------------------------------------------------------------------------
+    def start(self, source=None, destination=None, parameters=None):
+        """Build the element graph, instantiate the HIP stages, and run the frame loop in a thread."""
+        self.build(source, parameters)
+        self.stages = [STAGES[e.factory](e, self.server, self.server.device)
+                       for e in self.elements if e.factory in STAGES]
+        self.source = source or {}
+        self.destination = destination or {}
+        self.state = self.RUNNING
+        self.start_time = time.time()
+        self._thread = threading.Thread(target=self._run, name=f"pipeline-{self.id}", daemon=True)
+        self._thread.start()
+        return self.id
+
+    def _frames(self):
+        src = self.source
+        if src.get("type") == "application":
+            q = src.get("input")
+            while not self._stop.is_set():
+                try:
+                    item = q.get(timeout=0.1)
+                except queue.Empty:
+                    continue
+                if item is None:            # end of stream
+                    return
+                yield item
+        elif src.get("type") == "frames":
+            yield from src.get("frames", [])
+        else:
+            raise PreProcError(N.ERR_UNSUPPORTED, f"source type {src.get('type')!r}: decode is upstream of this "
+                                                  "build; use an 'application' source of decoded frames")
+
+    def _as_image(self, item):
+        from .preproc import Image
+
+        if isinstance(item, Image):
+            return item
+        if isinstance(item, dict):         # host frame {fourcc, width, height, planes}
+            return Image.from_host(item["fourcc"], item["width"], item["height"], item["planes"],
+                                   device=f"cuda:{self.server.device}")
+        raise TypeError(f"unsupported frame object {type(item).__name__}")
+
+    def _emit(self, fr: P.FrameResult, img):
+        dst = self.destination.get("metadata", self.destination)
+        out = dst.get("output")
+        mode = dst.get("mode", "frames")
+        if out is None:
+            return
+        if mode == "frames":
+            out.put((img, fr))
+        else:
+            out.put(P.gvametaconvert_json(fr))
+
+    def _run(self):
+        try:
+            batch = max([getattr(s, "batch_size", 1) for s in self.stages] + [1])
+            pend = []
+            for item in self._frames():
+                img = self._as_image(item)
+                ts = int(item.get("timestamp", 0)) if isinstance(item, dict) else self.frames
+                fr = P.FrameResult(img.width, img.height, timestamp=ts, source=self.source.get("uri"))
+                pend.append((self.frames, img, fr))
+                self.frames += 1
+                if len(pend) >= batch:
+                    self._flush(pend)
+                    pend = []
+                if self._stop.is_set():
+                    break
+            if pend:
+                self._flush(pend)
+            self.state = self.ABORTED if self._stop.is_set() else self.COMPLETED
+        except Exception as e:  # noqa: BLE001 — reported through status(), as the reference does
+            self.error = f"{type(e).__name__}: {e}"
+            self.state = self.ERROR
+        finally:
+            for s in self.stages:
+                s.close()
+            self.end_time = time.time()
+            dst = self.destination.get("metadata", self.destination)
+            if dst.get("output") is not None:
+                dst["output"].put(None)
+
+    def _flush(self, pend):
+        for s in self.stages:
+            s.process(pend)
+        for _, img, fr in pend:
+            self._emit(fr, img)
+
+    def stop(self):
+        self._stop.set()
+        return self.status()
+
+    def wait(self, timeout=None):
+        if self._thread is not None:
+            self._thread.join(timeout)
+        return self.status()
+
+    def status(self) -> dict:
+        el = ((self.end_time or time.time()) - self.start_time) if self.start_time else 0.0
+        return {"id": self.id, "state": self.state, "avg_fps": self.frames / el if el > 0 else 0.0,
+                "elapsed_time": el, "start_time": self.start_time, "message": self.error}
+
+
+class _Server:
+    """State behind the ``PipelineServer`` facade (one per process, like the reference's)."""
+
+    def __init__(self):
+        self.options: dict = {}
+        self.definitions: dict = {}
+        self.models: dict = {}
+        self.registry: dict = {}
+        self.instances: list[Pipeline] = []
+        self.started = False
+        self.device = 0
+
+    def start(self, options=None):
+        o = dict(options or {})
+        self.options = o
+        self.device = int(o.get("device", os.environ.get("EVAM_HIP_DEVICE", 0)))
+        pdir = o.get("pipeline_dir") or os.environ.get("PIPELINE_DIR", "pipelines")
+        mdir = o.get("model_dir") or os.environ.get("MODEL_DIR", "models")
+        self.models = scan_models(mdir)
+        self.definitions = {}
+        errors = []
+        if os.path.isdir(pdir):
+            for name in sorted(os.listdir(pdir)):
+                ndir = os.path.join(pdir, name)
+                if not os.path.isdir(ndir):
+                    continue
+                for version in sorted(os.listdir(ndir)):
+                    path = os.path.join(ndir, version, "pipeline.json")
+                    if os.path.exists(path):
+                        try:
+                            self.definitions.setdefault(name, {})[version] = PipelineDefinition.load(path, name, version)
+                        except (OSError, ValueError) as e:
+                            errors.append(f"{path}: {e}")
+        elif not o.get("ignore_init_errors", False):
+            raise FileNotFoundError(f"pipeline directory {pdir!r} not found")
+        if errors and not o.get("ignore_init_errors", False):
+            raise ValueError("; ".join(errors))
+        self.started = True
+
+    def model_for(self, network):
+        if network is None:
+            return None
+        if network in self.registry:
+            return self.registry[network]
+        m = re.search(r"([^/]+)/([^/]+)/[^/]+/[^/]+\.xml$", str(network))
+        return self.registry.get(f"{m.group(1)}/{m.group(2)}") if m else None
+
+    def proc_for(self, network):
+        for alias, versions in self.models.items():
+            for version, e in versions.items():
+                if network in e.values() and "proc" in e:
+                    return e["proc"]
+        return None
+
+
+_SERVER = _Server()
+
+
+class PipelineServer:
+    """Facade with the reference's class-level API (``evas/manager.py:100-155``)."""
+
+    @staticmethod
+    def start(options=None):
+        _SERVER.start(options)
+
+    @staticmethod
+    def pipelines():
+        return [{"name": d.name, "version": d.version, "type": d.type, "description": d.description,
+                 "parameters": d.parameters}
+                for vs in _SERVER.definitions.values() for d in vs.values()]
+
+    @staticmethod
+    def pipeline(name, version):
+        d = _SERVER.definitions.get(name, {}).get(str(version))
+        if d is None:
+            return None
+        p = Pipeline(_SERVER, d, len(_SERVER.instances) + 1)
+        _SERVER.instances.append(p)
+        return p
+
+    @staticmethod
+    def pipeline_instances():
+        return list(_SERVER.instances)
+
+    @staticmethod
+    def register_model(network_or_key: str, model: InferenceModel):
+        """Bind a model to a network path or an ``alias/version`` key (replaces OpenVINO loading)."""
+        _SERVER.registry[network_or_key] = model
+
+    @staticmethod
+    def models():
+        return _SERVER.models
+
+    @staticmethod
+    def wait(timeout=None):
+        for p in list(_SERVER.instances):
+            p.wait(timeout)
+
+    @staticmethod
+    def stop():
+        for p in list(_SERVER.instances):
+            p.stop()
+        for p in list(_SERVER.instances):
+            p.wait(5.0)
+        _SERVER.instances.clear()
+        _SERVER.started = False

@@ -1,0 +1,308 @@
+"""Pipeline-server counterpart and post-proc mapping (f2).
+
+The CPU legs cover:
+- template resolution, launch parsing and parameter schema forms (test templates under
+  tests/pipelines);
+- backend selection;
+- the README metadata golden rows;
+- optionally, the reference's own templates (only when /root/reference is present, i.e. in the build
+  container; never on the GPU box).
+
+The GPU leg runs the end-to-end loop: HIP pre-processing feeds synthetic torch models, and
+postproc maps the results to JSON.
+"""
+import json
+import os
+import queue
+
+import numpy as np
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PIPES = os.path.join(HERE, "pipelines")
+REF_PIPES = "/root/reference/pipelines"
+
+IR_XML = """<?xml version="1.0"?>
+<net name="{name}" version="11"><layers>
+<layer id="0" name="data" type="Parameter" version="opset1"><data shape="1,3,{h},{w}" element_type="f32"/>
+<output><port id="0" precision="FP32"><dim>1</dim><dim>3</dim><dim>{h}</dim><dim>{w}</dim></port></output></layer>
+</layers></net>"""
+
+
+def make_model_tree(root, spec):
+    """spec: {alias: {version: (w, h, proc_dict_or_None)}} -> model_dir with FP32/FP16 IR stubs."""
+    for alias, vs in spec.items():
+        for version, (w, h, proc) in vs.items():
+            for prec in ("FP16", "FP32"):
+                d = os.path.join(root, alias, version, prec)
+                os.makedirs(d, exist_ok=True)
+                with open(os.path.join(d, f"{alias}-{version}.xml"), "w") as f:
+                    f.write(IR_XML.format(name=alias, w=w, h=h))
+            if proc is not None:
+                with open(os.path.join(root, alias, version, f"{alias}-{version}.json"), "w") as f:
+                    json.dump(proc, f)
+    return root
+
+
+@pytest.fixture
+def ps(evam):
+    return evam.pipeline_server
+
+
+@pytest.fixture
+def model_dir(tmp_path):
+    return make_model_tree(str(tmp_path / "models"), {
+        "det_alias": {"det_ver": (64, 64, {"json_schema_version": "2.0.0", "input_preproc": [],
+                                           "output_postproc": [{"labels": ["bg", "car", "person"]}]})},
+        "cls_alias": {"cls_ver": (24, 24, {"input_preproc": [{"format": "image", "params": {"color_space": "RGB",
+                                                                                           "range": [0, 1]}}],
+                                           "output_postproc": [{"layer_name": "color", "attribute_name": "color",
+                                                                "labels": ["dark", "light"], "method": "max"}]})},
+        "ar": {"enc": (32, 32, None),
+               "dec": (32, 32, {"input_preproc": [{"format": "image", "params": {"resize": "aspect-ratio",
+                                                                                 "crop": "central"}}],
+                                "output_postproc": [{"attribute_name": "action", "method": "softmax",
+                                                     "labels": ["a", "b", "c"]}]})},
+    })
+
+
+def test_launch_parsing(ps):
+    els = ps.parse_launch('appsrc name=source ! decodebin ! videoconvert ! video/x-raw,format=BGRx '
+                          '! gvadetect model=/m/a.xml name=detection threshold=0.4 ! appsink name="sink x"')
+    assert [e.factory for e in els] == ["appsrc", "decodebin", "videoconvert", "capsfilter", "gvadetect", "appsink"]
+    assert els[3].caps == "video/x-raw,format=BGRx"
+    assert els[4].properties == {"model": "/m/a.xml", "name": "detection", "threshold": "0.4"}
+    assert els[5].name == "sink x"
+
+
+def test_model_tree_and_ir_shape(ps, model_dir):
+    models = ps.scan_models(model_dir)
+    e = models["det_alias"]["det_ver"]
+    assert e["network"] == e["FP32"] and e["network"].endswith("FP32/det_alias-det_ver.xml")
+    assert e["proc"].endswith(".json")
+    assert ps.ir_input_size(e["network"]) == (64, 64)
+    assert "proc" not in models["ar"]["enc"]
+
+
+def test_parameter_schema_forms(ps, model_dir, monkeypatch):
+    monkeypatch.setenv("EVAM_TEST_DET_DEVICE", "GPU")
+    ps.PipelineServer.start({"pipeline_dir": PIPES, "model_dir": model_dir})
+    p = ps.PipelineServer.pipeline("detect_classify", "hip")
+    p.build({"type": "application"}, {"detection-properties": {"pre-process-backend": "hip", "nireq": 4},
+                                      "inference-interval": 3, "detection-threshold": 0.25})
+    det, cls = p.element("det"), p.element("cls")
+    assert det.properties["pre-process-backend"] == "hip" and det.properties["nireq"] == 4      # passthrough
+    assert det.properties["inference-interval"] == 3 and cls.properties["inference-interval"] == 3  # fan-out
+    assert det.properties["threshold"] == 0.25                                                   # renamed
+    assert det.properties["device"] == "GPU"                                                     # {env[..]} default
+    assert cls.properties["object-class"] == "car"                                               # plain default
+    assert det.properties["model"].endswith("det_alias/det_ver/FP32/det_alias-det_ver.xml")
+    assert det.properties["model-proc"].endswith("det_alias-det_ver.json")                      # auto model-proc
+    assert p.elements[0].factory == "appsrc"                                                     # {auto_source}
+    assert p.backends() == {"det": "hip", "cls": "hip"}
+
+    monkeypatch.delenv("EVAM_TEST_DET_DEVICE")
+    q = ps.PipelineServer.pipeline("detect_classify", "hip").build({"type": "application"}, {})
+    assert "device" not in q.element("det").properties       # unset env default leaves the property alone
+
+    z = ps.PipelineServer.pipeline("zone", "count").build({"type": "application"},
+                                                          {"zones": [{"name": "A", "polygon": [[0, 0], [1, 1]]}]})
+    assert json.loads(z.element("zone").properties["kwarg"]) == [{"name": "A", "polygon": [[0, 0], [1, 1]]}]
+
+    with pytest.raises(ValueError):
+        ps.PipelineServer.pipeline("detect_classify", "hip").build({}, {"no-such-param": 1})
+    with pytest.raises(ValueError):
+        ps.PipelineServer.pipeline("detect_classify", "hip").build({}, {"inference-interval": "3"})
+    with pytest.raises(ValueError):
+        ps.PipelineServer.pipeline("zone", "count").build({}, {"mode": "other"})
+    assert ps.PipelineServer.pipeline("nope", "1") is None
+    names = {(d["name"], d["version"]) for d in ps.PipelineServer.pipelines()}
+    assert names == {("detect_classify", "hip"), ("action", "general"), ("zone", "count")}
+    ps.PipelineServer.stop()
+
+
+def test_backend_selection(ps, evam, model_dir):
+    ps.PipelineServer.start({"pipeline_dir": PIPES, "model_dir": model_dir})
+    for backend in ("opencv", "ie", "vaapi"):
+        p = ps.PipelineServer.pipeline("detect_classify", "hip").build(
+            {"type": "application"}, {"detection-properties": {"pre-process-backend": backend}})
+        with pytest.raises(evam.PreProcError) as ei:
+            p.backends()
+        assert ei.value.status == evam.native.ERR_UNSUPPORTED
+    p = ps.PipelineServer.pipeline("detect_classify", "hip").build({"type": "application"}, {})
+    assert p.backends() == {"det": "hip", "cls": "hip"}     # hip is the default in this build
+    ps.PipelineServer.stop()
+
+
+@pytest.mark.skipif(not os.path.isdir(REF_PIPES), reason="reference templates only in the build container")
+def test_reference_templates_resolve(ps):
+    """Every reference pipeline.json resolves, parses and accepts the hip backend selection."""
+    import tempfile
+
+    with tempfile.TemporaryDirectory() as td:
+        spec = {}
+        for name in os.listdir(REF_PIPES):
+            for version in os.listdir(os.path.join(REF_PIPES, name)):
+                text = open(os.path.join(REF_PIPES, name, version, "pipeline.json")).read()
+                import re
+
+                for a, v in re.findall(r"\{models\[([^\]]+)\]\[([^\]]+)\]", text):
+                    spec.setdefault(a, {})[v] = (64, 64, {"input_preproc": []})
+        make_model_tree(td, spec)
+        ps.PipelineServer.start({"pipeline_dir": REF_PIPES, "model_dir": td})
+        defs = ps.PipelineServer.pipelines()
+        assert len(defs) >= 10
+        n_inference = 0
+        for d in defs:
+            p = ps.PipelineServer.pipeline(d["name"], d["version"])
+            params = {}
+            for key, s in d["parameters"].get("properties", {}).items():
+                el = s.get("element")
+                if isinstance(el, dict) and el.get("format") == "element-properties":
+                    params[key] = {"pre-process-backend": "hip"}
+            p.build({"type": "uri", "uri": "file:///x.mp4"}, params)
+            assert p.elements[0].factory == "urisourcebin"
+            b = p.backends()
+            n_inference += len(b)
+            assert all(v == "hip" for v in b.values())
+        assert n_inference >= 10
+        ps.PipelineServer.stop()
+
+
+# ---- post-proc mapping (f2) ---------------------------------------------------------------------
+def test_readme_metadata_rows(evam):
+    """charts/README.md:117-119 sample rows: pixel rects from normalized boxes, and the exact JSON."""
+    P = evam.postproc
+    for line in open(os.path.join(HERE, "golden", "readme_metadata.jsonl")):
+        ref = json.loads(line)
+        W, H = ref["resolution"]["width"], ref["resolution"]["height"]
+        fr = P.FrameResult(W, H, timestamp=ref["timestamp"], source=ref["source"])
+        for o in ref["objects"]:
+            d = o["detection"]
+            bb = d["bounding_box"]
+            box = (bb["x_min"], bb["y_min"], bb["x_max"], bb["y_max"])
+            assert P.roi_rect(box, W, H) == (o["x"], o["y"], o["w"], o["h"])
+            t = P.Tensor("detection", d["confidence"], d["label_id"], d["label"], is_detection=True)
+            fr.regions.append(P.Region(*P.roi_rect(box, W, H), box, d["label"], d["label_id"], d["confidence"],
+                                       tensors=[t]))
+        assert P.gvametaconvert_json(fr) == line.strip()
+        pm = P.publisher_meta(fr, caps="video/x-raw", img_handle="h")
+        assert pm["gva_meta"][0]["tensor"][0] == {"name": "detection", "confidence": d["confidence"],
+                                                  "label_id": d["label_id"]}
+        assert (pm["width"], pm["height"], pm["channels"]) == (W, H, 3)
+
+
+def test_transform_mapping_letterbox(evam):
+    P = evam.postproc
+    # 1920x1080 -> 640x640 top-left letterbox: resized 640x360, scale 1/3
+    xf = evam.Transform(640 / 1920, 360 / 1080, 0, 0, 1920, 1080, 0, 0, 640, 360)
+    box_t = (0.25, 0.25, 0.5, 0.5)               # tensor-normalized
+    bb = P.tensor_box_to_frame(box_t, xf, 1920, 1080, 640, 640)
+    assert np.allclose(bb, (0.25, 160 / 360, 0.5, 320 / 360))
+    # centred placement: pad_y = 140
+    xf = evam.Transform(1 / 3, 1 / 3, 0, 0, 1920, 1080, 0, 140, 640, 360)
+    bb = P.tensor_box_to_frame((0.0, 140 / 640, 1.0, 500 / 640), xf, 1920, 1080, 640, 640)
+    assert np.allclose(bb, (0.0, 0.0, 1.0, 1.0))
+    # identity full-frame resize passes through unchanged (and clipped)
+    xf = evam.Transform(512 / 1920, 512 / 1080, 0, 0, 1920, 1080, 0, 0, 512, 512)
+    assert P.tensor_box_to_frame((0.1, -0.2, 1.3, 0.7), xf, 1920, 1080, 512, 512) == (0.1, 0.0, 1.0, 0.7)
+
+
+def test_parse_ssd_and_classify(evam):
+    P = evam.postproc
+    raw = np.array([[0, 1, 0.9, .1, .1, .2, .2], [0, 2, 0.3, .1, .1, .2, .2], [-1, 0, 0, 0, 0, 0, 0],
+                    [0, 1, 0.99, 0, 0, 1, 1]], np.float32)
+    d = P.parse_ssd(raw, 0.5)
+    assert len(d) == 1 and d[0][1] == 1 and abs(d[0][2] - 0.9) < 1e-6
+    t = P.classify(np.array([[1.0, 3.0], [5.0, 2.0]]), ["a", "b"], "softmax", "color")
+    assert [x.label for x in t] == ["b", "a"] and abs(t[0].confidence - 1 / (1 + np.exp(-2))) < 1e-12
+
+
+# ---- end to end on the GPU ---------------------------------------------------------------------
+@pytest.mark.gpu
+def test_end_to_end_detect_classify(ps, evam, model_dir, gpu, O):
+    import torch
+
+    calls = {}
+
+    def detector(t):
+        calls["det"] = tuple(t.shape)
+        n = t.shape[0]
+        out = torch.full((n, 3, 7), -1.0)
+        out[:, 0] = torch.tensor([0, 1, 0.9, 0.25, 0.25, 0.5, 0.75])     # car
+        out[:, 1] = torch.tensor([0, 2, 0.8, 0.0, 0.0, 0.1, 0.1])        # person (not classified)
+        return out
+
+    def classifier(t):
+        calls["cls"] = tuple(t.shape)
+        m = t.mean(dim=(1, 2, 3))
+        return {"color": torch.stack([1 - m, m], 1)}
+
+    ps.PipelineServer.start({"pipeline_dir": PIPES, "model_dir": model_dir})
+    ps.PipelineServer.register_model("det_alias/det_ver", ps.InferenceModel(detector, (64, 64), name="det"))
+    ps.PipelineServer.register_model("cls_alias/cls_ver", ps.InferenceModel(classifier, (24, 24), name="cls"))
+    qin, qout = queue.Queue(), queue.Queue()
+    rng = np.random.default_rng(3)
+    frames = [O.random_frame(rng, O.NV12, 320, 180) for _ in range(3)]
+    for f in frames:
+        qin.put({"fourcc": f.fourcc, "width": f.width, "height": f.height, "planes": f.planes})
+    qin.put(None)
+    p = ps.PipelineServer.pipeline("detect_classify", "hip")
+    p.start(source={"type": "application", "input": qin},
+            destination={"metadata": {"type": "application", "output": qout, "mode": "json"}},
+            parameters={"detection-properties": {"pre-process-backend": "hip"}})
+    st = p.wait(60)
+    assert st["state"] == "COMPLETED", st
+    lines = []
+    while True:
+        x = qout.get(timeout=5)
+        if x is None:
+            break
+        lines.append(json.loads(x))
+    assert len(lines) == 3
+    assert calls["det"] == (1, 3, 64, 64) and calls["cls"] == (1, 3, 24, 24)
+    for d in lines:
+        car, person = d["objects"]
+        assert (car["x"], car["y"], car["w"], car["h"]) == (80, 45, 80, 90)
+        assert car["roi_type"] == "car" and "color" in car and "color" not in person
+        assert car["color"]["label"] in ("dark", "light")
+    ps.PipelineServer.stop()
+
+
+@pytest.mark.gpu
+def test_end_to_end_action_ring(ps, evam, model_dir, gpu, O):
+    import torch
+
+    seen = []
+
+    def encoder(clip):
+        seen.append(clip.clone())
+        return clip.mean(dim=(2, 3))            # [16, 3]
+
+    def decoder(emb):
+        return emb.mean(0, keepdim=True)        # [1, 3]
+
+    ps.PipelineServer.start({"pipeline_dir": PIPES, "model_dir": model_dir})
+    ps.PipelineServer.register_model("ar/enc", ps.InferenceModel(encoder, (32, 32)))
+    ps.PipelineServer.register_model("ar/dec", ps.InferenceModel(decoder, (32, 32)))
+    rng = np.random.default_rng(5)
+    frames = [O.random_frame(rng, O.BGRX, 96, 54) for _ in range(18)]
+    src = {"type": "frames", "frames": [{"fourcc": f.fourcc, "width": f.width, "height": f.height,
+                                          "planes": f.planes} for f in frames]}
+    qout = queue.Queue()
+    p = ps.PipelineServer.pipeline("action", "general")
+    p.start(source=src, destination={"metadata": {"output": qout, "mode": "json"}})
+    assert p.wait(60)["state"] == "COMPLETED"
+    out = []
+    while (x := qout.get(timeout=5)) is not None:
+        out.append(json.loads(x))
+    assert len(out) == 18
+    assert all("tensors" not in d for d in out[:15]) and all("tensors" in d for d in out[15:])
+    assert len(seen) == 3
+    # the first full clip is frames 0..15 in order, each aspect+central-cropped 96x54 -> 57x32 -> 32x32
+    ref = np.zeros((16, 3, 32, 32), np.float32)
+    c = O.COracle()
+    for i in range(16):
+        c.preprocess_item(frames[i], None, ref, i, mode=2, lut=O.np_norm_lut(0))
+    assert np.array_equal(seen[0].cpu().numpy(), ref)
+    ps.PipelineServer.stop()
