@@ -19,6 +19,7 @@ from .preproc import (HipPreProcessor, Image, ImageBatch, PreProcInfo, Roi, Tran
 from . import _native as native  # noqa: F401
 from . import streams  # noqa: F401
 from . import postproc  # noqa: F401
+from . import feed  # noqa: F401
 from . import pipeline_server  # noqa: F401
 
 _sys.modules.setdefault("evam_amd", _sys.modules[__name__])

@@ -1,0 +1,47 @@
+"""Host->device feed: pinned ring + copy stream, parity with the oracle per batch."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("fmt,depth", [("NV12", 2), ("I420", 3), ("BGRX", 2)])
+def test_feed_batches_match_oracle(evam, O, coracle, gpu, fmt, depth):
+    import torch
+
+    fc = {"NV12": O.NV12, "I420": O.I420, "BGRX": O.BGRX}[fmt]
+    W, H, B, DW, DH = 200, 120, 3, 96, 64
+    feed = evam.feed.HostFeed(fc, W, H, batch=B, depth=depth)
+    pp = evam.HipPreProcessor(device=0)
+    info = evam.PreProcInfo(range=(0.0, 1.0), mean=(0.5, 0.4, 0.3), std=(0.2, 0.25, 0.3))
+    lut = O.np_norm_lut(3, (0.0, 1.0), (0.5, 0.4, 0.3), (0.2, 0.25, 0.3))
+    rng = np.random.default_rng(11)
+    outs, refs = [], []
+    for step in range(2 * depth + 1):                       # wraps the ring at least twice
+        frames = [O.random_frame(rng, fc, W, H) for _ in range(B)]
+        k = feed.acquire()
+        if step % 2:
+            feed.fill(k, frames)
+        else:                                               # decoder-writes-into-pinned path
+            for i, f in enumerate(frames):
+                for dst, src in zip(feed.host_planes(k)[i], f.planes):
+                    dst[:, :src.shape[1]] = src
+        feed.submit(k)
+        out = torch.empty((B, 3, DH, DW), dtype=torch.float32, device=gpu)
+        pp.convert(feed.batch(k), out, info)
+        feed.release(k)
+        outs.append(out)
+        ref = np.zeros((B, 3, DH, DW), np.float32)
+        for i, f in enumerate(frames):
+            coracle.preprocess_item(f, None, ref, i, lut=lut)
+        refs.append(ref)
+    torch.cuda.synchronize()
+    pp.close()
+    for step, (o, r) in enumerate(zip(outs, refs)):
+        assert np.array_equal(o.cpu().numpy().view(np.uint32), r.view(np.uint32)), f"step {step}"
+
+
+def test_feed_rejects_oversize_batch(evam, O, gpu):
+    feed = evam.feed.HostFeed("NV12", 64, 48, batch=1, depth=2)
+    with pytest.raises(ValueError):
+        feed.fill(feed.acquire(), [O.random_frame(np.random.default_rng(0), O.NV12, 64, 48)] * 2)
