@@ -13,6 +13,16 @@ tail -3 "$OUT/pytest_gpu_$TAG.log"
 echo "[gpu_check] bench"; date
 timeout -k 10 300 python bench.py > "$OUT/bench_$TAG.json" 2> "$OUT/bench_$TAG.err" || { tail -20 "$OUT/bench_$TAG.err"; exit 1; }
 cat "$OUT/bench_$TAG.json"
+if [ "${EXTRA:-0}" = "1" ]; then
+  for c in c1 c3 c4 c5; do
+    echo "[gpu_check] bench $c"; date
+    timeout -k 10 300 python bench.py --config $c --steps 200 --warmup 50 --no-cpu-baseline > "$OUT/bench_${c}_$TAG.json" 2> "$OUT/bench_${c}_$TAG.err" || { tail -20 "$OUT/bench_${c}_$TAG.err"; exit 1; }
+    cat "$OUT/bench_${c}_$TAG.json"
+  done
+  echo "[gpu_check] bench host feed"; date
+  timeout -k 10 300 python bench.py --feed host --steps 100 --warmup 20 --no-cpu-baseline > "$OUT/bench_host_$TAG.json" 2> "$OUT/bench_host_$TAG.err" || { tail -20 "$OUT/bench_host_$TAG.err"; exit 1; }
+  cat "$OUT/bench_host_$TAG.json"
+fi
 echo "[gpu_check] rocprofv3 kernel trace"; date
 export TMPDIR=/tmp
 cd /tmp
