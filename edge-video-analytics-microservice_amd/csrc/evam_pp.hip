@@ -867,6 +867,287 @@ __global__ __launch_bounds__(kThreads) void evam_pp_staged(const SParams P) {
     }
 }
 
+// Source footprint of one item's visible output columns: the 16 B-aligned byte window [fs, fs + 16 n)
+// of a luma / packed row (fsY, nY) and of a chroma row (fsC, nC) that its taps read. Shared by the
+// ROI kernel (device) and its host-side planner, so both agree on the slot size.
+__host__ __device__ inline void item_footprint(int FMT, int bpp, int x0, int cw, int rw, int ox, double scx, int DW,
+                                               int& fsY, int& nY, int& fsC, int& nC) {
+    fsY = nY = fsC = nC = 0;
+    const int Xv0 = ox > 0 ? ox : 0;
+    const int Xv1 = (ox + rw < DW ? ox + rw : DW) - 1;
+    if (Xv0 > Xv1) return;
+    int sa, sb, c0, c1;
+    linear_coef(Xv0 - ox, scx, cw, true, sa, c0, c1);
+    linear_coef(Xv1 - ox, scx, cw, true, sb, c0, c1);
+    const int xa = x0 + sa, xb = x0 + (sb + 1 < cw - 1 ? sb + 1 : cw - 1);
+    fsY = (xa * bpp) & ~15;
+    nY = (((xb * bpp + bpp + 15) & ~15) - fsY) >> 4;
+    if (FMT == kNV12) {
+        fsC = (2 * (xa >> 1)) & ~15;
+        nC = (((2 * (xb >> 1) + 2 + 15) & ~15) - fsC) >> 4;
+    } else if (FMT == kI420) {
+        fsC = (xa >> 1) & ~15;
+        nC = ((((xb >> 1) + 1 + 15) & ~15) - fsC) >> 4;
+    }
+}
+
+constexpr int kRoiK = 4;  // max pixels per lane per row group in the ROI kernel
+
+struct QParams {
+    const ItemDesc* items;
+    const float* lut;    // [3][256]
+    void* dst;
+    int DW, DH;
+    int TH, tiles_per_item;   // a tile is all DW columns x TH rows of one item
+    int offXT, offYT, offBuf; // LDS carve: [LUT][XTab x DW][YTab x TH][buf0][buf1]
+    int slot;                 // bytes of one staged row segment (multiple of 16, <= kSlot)
+    int buf_bytes;            // one staging buffer: slots x slot
+    int K;                    // pixels per lane per group: ceil(R * DW / 256) <= kRoiK
+    int nfull;                // floor(R * DW / 256): k-steps in which every lane of every wave stores
+    int color_rgb;
+    uint32_t fill;
+};
+
+// Staged kernel for batches whose items differ in geometry (gvaclassify ROI batches, mixed crops).
+// One workgroup owns all DW columns x TH rows of one item. It builds that item's OpenCV coefficient
+// tables in LDS (device-side, the same double/float sequence as the host tables), then walks the tile
+// in groups of R output rows exactly like evam_pp_staged:
+//  * the group's source row segments (the item's whole visible footprint, <= slot bytes) arrive in LDS
+//    by LDS-DMA while the previous group is converted;
+//  * taps are LDS byte reads.
+// The R x DW pixels of a group are packed densely onto the 256 lanes (pixel p = tid + 256 k). Narrow
+// outputs such as 72x72 classifier inputs keep every lane busy and every store row-contiguous; a
+// 64-column tiling would leave most lanes of the second segment idle.
+template <int FMT, int OUT, int R>
+__global__ __launch_bounds__(kThreads) void evam_pp_roi(const QParams P) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    using T = FmtTraits<FMT>;
+    constexpr bool kYUV = FMT == kNV12 || FMT == kI420;
+    constexpr int NP = FMT == kI420 ? 3 : (FMT == kNV12 ? 2 : 1);
+    constexpr int NS = 2 * R * NP;
+    static_assert(NS % 4 == 0, "slots are issued four waves at a time");
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int t = blockIdx.x;
+    const int item = t / P.tiles_per_item;
+    const int ty = t - item * P.tiles_per_item;
+    const __attribute__((address_space(4))) ItemDesc* it =
+        (const __attribute__((address_space(4))) ItemDesc*)(P.items) + item;
+    const uint8_t* p0 = it->plane[0];
+    const uint8_t* p1 = it->plane[1];
+    const uint8_t* p2 = it->plane[2];
+    const int pitch0 = it->pitch[0], pitch1 = it->pitch[1], pitch2 = it->pitch[2];
+    const int x0 = it->x0, y0 = it->y0, cw = it->cw, ch = it->ch;
+    const int rw = it->rw, rh = it->rh, ox = it->ox, oy = it->oy;
+    const double scx = it->scale_x, scy = it->scale_y;
+    const size_t plane = (size_t)P.DW * P.DH;
+    const size_t esz = OUT == 1 ? 4 : 1;
+    uint8_t* const d0 = reinterpret_cast<uint8_t*>(P.dst) + (size_t)it->slot * 3 * plane * esz;
+    uint8_t* const d1 = d0 + plane * esz;
+    uint8_t* const d2 = d1 + plane * esz;
+    const __amdgpu_buffer_rsrc_t rsY = __builtin_amdgcn_make_buffer_rsrc((void*)p0, (short)0, 0x7FFFFFFF, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsC = __builtin_amdgcn_make_buffer_rsrc((void*)(p1 ? p1 : p0), (short)0, 0x7FFFFFFF, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsV = __builtin_amdgcn_make_buffer_rsrc((void*)(p2 ? p2 : p0), (short)0, 0x7FFFFFFF, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsD0 = __builtin_amdgcn_make_buffer_rsrc((void*)d0, (short)0, 0x7FFFFFFF, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsD1 = __builtin_amdgcn_make_buffer_rsrc((void*)d1, (short)0, 0x7FFFFFFF, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsD2 = __builtin_amdgcn_make_buffer_rsrc((void*)d2, (short)0, 0x7FFFFFFF, 0x00020000);
+
+    float* lut_s = reinterpret_cast<float*>(smem);
+    if constexpr (OUT == 1) {
+        for (int i = tid; i < 768; i += kThreads) lut_s[i] = P.lut[i];
+    }
+    XTab* xt = reinterpret_cast<XTab*>(smem + P.offXT);
+    YTab* yt = reinterpret_cast<YTab*>(smem + P.offYT);
+    const int Y0 = ty * P.TH, Y1 = min(Y0 + P.TH, P.DH), rows = Y1 - Y0;
+    for (int X = tid; X < P.DW; X += kThreads) {
+        XTab e;
+        e.s0 = 0; e.s1 = 0; e.a0 = 0; e.a1 = 0; e.pad = 0;
+        const int dx = X - ox;
+        if (dx >= 0 && dx < rw) {
+            int sx, a0, a1;
+            linear_coef(dx, scx, cw, true, sx, a0, a1);
+            e.s0 = sx;
+            e.s1 = min(sx + 1, cw - 1);
+            e.a0 = (uint16_t)(a0 << 4);
+            e.a1 = (uint16_t)(a1 << 4);
+        }
+        xt[X] = e;
+    }
+    for (int ly = tid; ly < rows; ly += kThreads) {
+        YTab e;
+        e.r0 = 0; e.r1 = 0; e.b0 = 0; e.b1 = 0;
+        const int dy = Y0 + ly - oy;
+        if (dy >= 0 && dy < rh) {
+            int sy, b0, b1;
+            linear_coef(dy, scy, ch, false, sy, b0, b1);
+            e.r0 = min(max(sy, 0), ch - 1);
+            e.r1 = min(max(sy + 1, 0), ch - 1);
+            e.b0 = b0 << 8;
+            e.b1 = b1 << 8;
+        }
+        yt[ly] = e;
+    }
+    int fsY, nY, fsC, nC;
+    item_footprint(FMT, T::bpp, x0, cw, rw, ox, scx, P.DW, fsY, nY, fsC, nC);
+    fsY = __builtin_amdgcn_readfirstlane(fsY);
+    nY = __builtin_amdgcn_readfirstlane(nY);
+    fsC = __builtin_amdgcn_readfirstlane(fsC);
+    nC = __builtin_amdgcn_readfirstlane(nC);
+    __syncthreads();
+
+    const int f0 = P.fill & 0xFF, f1 = (P.fill >> 8) & 0xFF, f2 = (P.fill >> 16) & 0xFF;
+    // Per-lane pixel state for k = 0..K-1, identical for every group: row in the group, element offset
+    // inside the group, packed LDS tap offsets (tap 0 low, tap 1 high half) and horizontal weights.
+    int rr[kRoiK];
+    uint32_t rc[kRoiK], lY[kRoiK], lC[kRoiK], wa[kRoiK];
+    bool val[kRoiK];
+#pragma unroll
+    for (int k = 0; k < kRoiK; k++) {
+        const int p = tid + k * kThreads;
+        val[k] = k < P.K && p < R * P.DW;
+        const int r = val[k] ? p / P.DW : 0;
+        const int c = val[k] ? p - r * P.DW : 0;
+        rr[k] = r;
+        rc[k] = (uint32_t)p;
+        const XTab e = xt[c];
+        wa[k] = (uint32_t)e.a0 | ((uint32_t)e.a1 << 16);
+        lY[k] = lC[k] = 0;
+        if (val[k] && wa[k] != 0) {
+            const int ca = x0 + e.s0, cb = x0 + e.s1;
+            lY[k] = (uint32_t)(ca * T::bpp - fsY) | ((uint32_t)(cb * T::bpp - fsY) << 16);
+            if constexpr (FMT == kNV12)
+                lC[k] = (uint32_t)(2 * (ca >> 1) - fsC) | ((uint32_t)(2 * (cb >> 1) - fsC) << 16);
+            else if constexpr (FMT == kI420)
+                lC[k] = (uint32_t)((ca >> 1) - fsC) | ((uint32_t)((cb >> 1) - fsC) << 16);
+        }
+    }
+    const int ngroups = (rows + R - 1) / R;
+    const int slot = P.slot;
+
+    auto issue = [&](int g, uint8_t* buf) {
+        if (nY == 0) return;  // no visible columns: every pixel is fill
+#pragma unroll
+        for (int s0 = 0; s0 < NS; s0 += 4) {
+            const int s = s0 + wave;
+            const int pl = s / (2 * R), loc = s - pl * 2 * R, r = loc >> 1, tap = loc & 1;
+            const int ly = g * R + r;
+            if (ly >= rows) continue;
+            const int b0 = __builtin_amdgcn_readfirstlane(yt[ly].b0);
+            const int b1 = __builtin_amdgcn_readfirstlane(yt[ly].b1);
+            if ((b0 | b1) == 0) continue;  // padding row: nothing to stage
+            const int ya = y0 + __builtin_amdgcn_readfirstlane(yt[ly].r0);
+            const int yb = y0 + __builtin_amdgcn_readfirstlane(yt[ly].r1);
+            const int yr = tap ? yb : ya;
+            if (pl > 0 && tap && (ya >> 1) == (yb >> 1)) continue;  // chroma row shared by both taps
+            const int nck = pl == 0 ? nY : nC;
+            if (lane < nck) {
+                __attribute__((address_space(3))) void* dstl =
+                    (__attribute__((address_space(3))) void*)(buf + s * slot);
+                if (pl == 0)
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsY, dstl, 16, lane * 16, yr * pitch0 + fsY, 0, 0);
+                else if (pl == 1)
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsC, dstl, 16, lane * 16, (yr >> 1) * pitch1 + fsC, 0, 0);
+                else
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsV, dstl, 16, lane * 16, (yr >> 1) * pitch2 + fsC, 0, 0);
+            }
+        }
+    };
+
+    auto compute = [&](int g, const uint8_t* buf) {
+        const uint32_t gbase = (uint32_t)((Y0 + g * R) * P.DW);
+#pragma unroll
+        for (int k = 0; k < kRoiK; k++) {
+            const int ly = g * R + rr[k];
+            if (!val[k] || ly >= rows) continue;
+            const YTab e = yt[ly];
+            int v[3];
+            if ((e.b0 | e.b1) == 0 || wa[k] == 0) {  // letterbox padding row / column
+                v[0] = f0; v[1] = f1; v[2] = f2;
+            } else {
+                const uint32_t a0 = wa[k] & 0xFFFF, a1 = wa[k] >> 16;
+                const uint32_t tY0 = lY[k] & 0xFFFF, tY1 = lY[k] >> 16;
+                const uint8_t* sy0 = buf + (2 * rr[k]) * slot;
+                const uint8_t* sy1 = sy0 + slot;
+                int c[4][3];
+                if constexpr (kYUV) {
+                    const uint32_t tC0 = lC[k] & 0xFFFF, tC1 = lC[k] >> 16;
+                    const int ya = y0 + e.r0, yb = y0 + e.r1;
+                    const uint8_t* sc0 = buf + (2 * R + 2 * rr[k]) * slot;
+                    const uint8_t* sc1 = (ya >> 1) == (yb >> 1) ? sc0 : sc0 + slot;
+                    Chroma<FMT> cA, cB, cC, cD;
+                    if constexpr (FMT == kNV12) {
+                        cA.u = *reinterpret_cast<const uint16_t*>(sc0 + tC0);
+                        cB.u = *reinterpret_cast<const uint16_t*>(sc0 + tC1);
+                        cC.u = *reinterpret_cast<const uint16_t*>(sc1 + tC0);
+                        cD.u = *reinterpret_cast<const uint16_t*>(sc1 + tC1);
+                    } else {
+                        const uint8_t* sv0 = sc0 + 2 * R * slot;
+                        const uint8_t* sv1 = sc1 + 2 * R * slot;
+                        cA.u = sc0[tC0]; cA.v = sv0[tC0];
+                        cB.u = sc0[tC1]; cB.v = sv0[tC1];
+                        cC.u = sc1[tC0]; cC.v = sv1[tC0];
+                        cD.u = sc1[tC1]; cD.v = sv1[tC1];
+                    }
+                    y_plus_uv((int)sy0[tY0], chroma_terms<FMT>(cA), c[0][0], c[0][1], c[0][2]);
+                    y_plus_uv((int)sy0[tY1], chroma_terms<FMT>(cB), c[1][0], c[1][1], c[1][2]);
+                    y_plus_uv((int)sy1[tY0], chroma_terms<FMT>(cC), c[2][0], c[2][1], c[2][2]);
+                    y_plus_uv((int)sy1[tY1], chroma_terms<FMT>(cD), c[3][0], c[3][1], c[3][2]);
+                } else {
+                    const uint8_t* tap[4] = {sy0 + tY0, sy0 + tY1, sy1 + tY0, sy1 + tY1};
+#pragma unroll
+                    for (int q = 0; q < 4; q++) {
+                        if constexpr (FMT == kBGRX) {
+                            const uint32_t px = *reinterpret_cast<const uint32_t*>(tap[q]);
+                            c[q][0] = px & 0xFF; c[q][1] = (px >> 8) & 0xFF; c[q][2] = (px >> 16) & 0xFF;
+                        } else {
+                            c[q][0] = tap[q][0]; c[q][1] = tap[q][1]; c[q][2] = tap[q][2];
+                        }
+                    }
+                }
+                const uint32_t wb0 = (uint32_t)e.b0, wb1 = (uint32_t)e.b1;
+#pragma unroll
+                for (int ch3 = 0; ch3 < 3; ch3++) {
+                    const uint32_t D0 = __umul24(c[0][ch3], a0) + __umul24(c[1][ch3], a1);
+                    const uint32_t D1 = __umul24(c[2][ch3], a0) + __umul24(c[3][ch3], a1);
+                    v[ch3] = vresize(D0, D1, wb0, wb1);
+                }
+                if (P.color_rgb) { const int tmp = v[0]; v[0] = v[2]; v[2] = tmp; }
+            }
+            const uint32_t vo = (gbase + rc[k]) * (uint32_t)esz;
+            if constexpr (OUT == 1) {
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lut_s[v[0]]), rsD0, vo, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lut_s[256 + v[1]]), rsD1, vo, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lut_s[512 + v[2]]), rsD2, vo, 0, 0);
+            } else {
+                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v[0], rsD0, vo, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v[1], rsD1, vo, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v[2], rsD2, vo, 0, 0);
+            }
+        }
+    };
+
+    uint8_t* const buf0 = smem + P.offBuf;
+    uint8_t* const buf1 = buf0 + P.buf_bytes;
+    issue(0, buf0);
+    for (int g = 0; g < ngroups; g++) {
+        // Wait for group g's DMA. After a full group every wave issued at least 3 * nfull stores behind
+        // that DMA, so those may stay in flight; otherwise drain everything.
+        const bool prev_full = g > 0 && g * R <= rows;
+        const int keep = prev_full ? P.nfull : 0;
+        if (keep >= 4) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+        else if (keep == 3) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+        else if (keep == 2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        else if (keep == 1) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();  // every wave's DMA for g landed; every wave done reading g-1
+        if (g + 1 < ngroups) issue(g + 1, (g & 1) ? buf0 : buf1);
+        compute(g, (g & 1) ? buf1 : buf0);
+    }
+}
+
 // ------------------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------------------
@@ -1157,6 +1438,62 @@ hipError_t launch(int f, int out, const KParams& p, int grid, int lds, hipStream
     case kBGR * 2 + 0: return launch_t<kBGR, 0>(p, grid, lds, s);
     default: return launch_t<kBGR, 1>(p, grid, lds, s);
     }
+}
+
+template <int FMT, int OUT, int R>
+hipError_t launch_roi_t(const QParams& p, int grid, int lds, hipStream_t s) {
+    hipLaunchKernelGGL((evam_pp_roi<FMT, OUT, R>), dim3(grid), dim3(kThreads), lds, s, p);
+    return hipGetLastError();
+}
+
+template <int FMT, int OUT>
+hipError_t launch_roi_r(int R, const QParams& p, int grid, int lds, hipStream_t s) {
+    return R == 4 ? launch_roi_t<FMT, OUT, 4>(p, grid, lds, s) : launch_roi_t<FMT, OUT, 2>(p, grid, lds, s);
+}
+
+hipError_t launch_roi(int f, int out, int R, const QParams& p, int grid, int lds, hipStream_t s) {
+    switch (f * 2 + out) {
+    case kNV12 * 2 + 0: return launch_roi_r<kNV12, 0>(R, p, grid, lds, s);
+    case kNV12 * 2 + 1: return launch_roi_r<kNV12, 1>(R, p, grid, lds, s);
+    case kI420 * 2 + 0: return launch_roi_r<kI420, 0>(R, p, grid, lds, s);
+    case kI420 * 2 + 1: return launch_roi_r<kI420, 1>(R, p, grid, lds, s);
+    case kBGRX * 2 + 0: return launch_roi_r<kBGRX, 0>(R, p, grid, lds, s);
+    case kBGRX * 2 + 1: return launch_roi_r<kBGRX, 1>(R, p, grid, lds, s);
+    case kBGR * 2 + 0: return launch_roi_r<kBGR, 0>(R, p, grid, lds, s);
+    default: return launch_roi_r<kBGR, 1>(R, p, grid, lds, s);
+    }
+}
+
+// ROI-kernel plan for one format group with per-item geometry: rows per group R (the R x DW pixels
+// of a group cover the 256 lanes at most kRoiK times) and the LDS slot that fits every item's
+// footprint. Returns false when the group needs the generic kernel (very wide outputs, or a
+// footprint beyond kSlot, i.e. an extreme downscale of a wide crop).
+bool plan_roi(int f, const std::vector<Geom>& geo, const std::vector<int>& fmt, int DW, int DH, int out_dtype,
+              QParams& q, int& R, int& lds) {
+    if (DW > 512) return false;
+    R = DW <= 256 ? 4 : 2;
+    int need = 16;
+    for (size_t i = 0; i < geo.size(); i++) {
+        if (fmt[i] != f) continue;
+        const Geom& g = geo[i];
+        int fsY, nY, fsC, nC;
+        item_footprint(f, fmt_bpp(f), g.x0, g.cw, g.rw, g.ox, 1. / ((double)g.rw / g.cw), DW, fsY, nY, fsC, nC);
+        need = std::max(need, 16 * std::max(nY, nC));
+    }
+    if (need > kSlot) return false;
+    const int np = f == kI420 ? 3 : (f == kNV12 ? 2 : 1);
+    q.DW = DW; q.DH = DH;
+    q.TH = std::min(DH, std::max(R, (16384 / DW) / R * R));
+    q.tiles_per_item = (DH + q.TH - 1) / q.TH;
+    q.offXT = out_dtype == EVAM_DTYPE_F32 ? kLutBytes : 0;
+    q.offYT = q.offXT + (int)sizeof(XTab) * DW;
+    q.offBuf = q.offYT + (int)sizeof(YTab) * q.TH;
+    q.slot = need;
+    q.buf_bytes = 2 * R * np * need;
+    q.K = (R * DW + kThreads - 1) / kThreads;
+    q.nfull = (R * DW) / kThreads;
+    lds = q.offBuf + 2 * q.buf_bytes;
+    return lds <= 64 * 1024 && q.K <= kRoiK;
 }
 
 }  // namespace
@@ -1461,6 +1798,23 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
             if (e != hipSuccess) return fail(EVAM_PP_ERR_HIP, "kernel launch failed: %s", hipGetErrorString(e));
             launches++;
             continue;
+        }
+        {
+            QParams q{};
+            int R = 0, lds = 0;
+            if (env_int("EVAM_PP_ROI", 1) && plan_roi(f, geo, fmt, DW, DH, cfg->out_dtype, q, R, lds)) {
+                q.items = reinterpret_cast<const ItemDesc*>(h->d_block + kLutBytes) + first[f];
+                q.lut = reinterpret_cast<const float*>(h->d_block);
+                q.dst = dst->data;
+                q.color_rgb = cfg->color_order == EVAM_COLOR_RGB;
+                q.fill = (uint32_t)cfg->fill[0] | ((uint32_t)cfg->fill[1] << 8) | ((uint32_t)cfg->fill[2] << 16);
+                const int64_t grid = (int64_t)count[f] * q.tiles_per_item;
+                if (grid > 0x7FFFFFFF) return fail(EVAM_PP_ERR_INVALID_ARG, "evam_pp_run: too many tiles");
+                hipError_t e = launch_roi(f, cfg->out_dtype, R, q, (int)grid, lds, h->stream);
+                if (e != hipSuccess) return fail(EVAM_PP_ERR_HIP, "kernel launch failed: %s", hipGetErrorString(e));
+                launches++;
+                continue;
+            }
         }
         const TileCfg t = choose_tiles(DW, DH, cfg->out_dtype);
         KParams p{};

@@ -132,6 +132,41 @@ def test_roi_batch(evam, O, coracle, gpu, fmt):
     assert_same(got, ref, f"roi batch {fmt}")
 
 
+@pytest.mark.parametrize("fmt", FORMATS)
+@pytest.mark.parametrize("dst,dtype,resize,placement", [
+    ((72, 72), "u8", "no-aspect-ratio", "top_left"),     # ROI kernel, R=4, K=2
+    ((300, 120), "f32", "aspect-ratio", "center"),       # ROI kernel, R=2 (DW > 256), letterbox columns+rows
+    ((600, 40), "u8", "no-aspect-ratio", "top_left"),    # DW > 512: generic kernel
+    ((17, 5), "f32", "aspect-ratio", "top_left"),        # K=1, nfull=0
+    ((64, 64), "f32", "aspect-ratio", "center"),         # R*DW = 256 exactly
+])
+@pytest.mark.parametrize("roi_kernel", ["1", "0"])
+def test_roi_kernels(evam, O, coracle, gpu, fmt, dst, dtype, resize, placement, roi_kernel, monkeypatch):
+    """Per-item-geometry batches through the staged ROI kernel and (EVAM_PP_ROI=0) the generic one."""
+    import torch
+
+    monkeypatch.setenv("EVAM_PP_ROI", roi_kernel)
+    rng = np.random.default_rng(zlib.crc32(f"{fmt}{dst}{resize}".encode()))
+    W, H = 480, 270
+    frames = [O.random_frame(rng, fc(O, fmt), W, H, pattern="gradient" if i else "uniform") for i in range(3)]
+    rois = []
+    for si in range(3):
+        for _ in range(12):
+            w, h = int(rng.integers(2, 420)), int(rng.integers(2, 260))
+            x, y = int(rng.integers(-30, W - 1)), int(rng.integers(-30, H - 1))
+            rois.append((si, x, y, max(w, 2 - x), max(h, 2 - y)))
+    rois += [(0, 0, 0, W, H), (2, W - 2, H - 2, 9, 9), (1, 100, 50, 1, 1)]
+    info = evam.PreProcInfo(resize=resize, placement=placement, fill=(9, 99, 199), color_space="RGB",
+                            **({"range": (0.0, 1.0), "mean": (0.1, 0.2, 0.3), "std": (0.3, 0.2, 0.1)}
+                               if dtype == "f32" else {}))
+    DW, DH = dst
+    shape = (len(rois), 3, DH, DW)
+    tdt = torch.float32 if dtype == "f32" else torch.uint8
+    got, _ = run_hip(evam, torch, upload(evam, frames, gpu), shape, tdt, info, rois=[evam.Roi(*r) for r in rois])
+    ref, _ = run_oracle(O, coracle, frames, shape, dtype, info, rois=rois)
+    assert_same(got, ref, f"roi {fmt} {dst} {resize} kernel={roi_kernel}")
+
+
 @pytest.mark.parametrize("placement", ["top_left", "center"])
 @pytest.mark.parametrize("fill", [(0, 0, 0), (114, 114, 114), (1, 2, 3)])
 def test_letterbox(evam, O, coracle, gpu, placement, fill):
