@@ -14,7 +14,7 @@ HIP kernels for gfx950 behind the C ABI in ``include/evam_pp.h``.
 import sys as _sys
 
 from ._native import PreProcError, load_library  # noqa: F401
-from .preproc import (HipPreProcessor, Image, ImageBatch, PreProcInfo, Roi, Transform,  # noqa: F401
+from .preproc import (HipPreProcessor, Image, ImageBatch, PreProcInfo, Roi, RoiBatch, Transform,  # noqa: F401
                       create_preprocessor, plane_layout)
 from . import _native as native  # noqa: F401
 from . import streams  # noqa: F401

@@ -1496,6 +1496,26 @@ bool plan_roi(int f, const std::vector<Geom>& geo, const std::vector<int>& fmt, 
     return lds <= 64 * 1024 && q.K <= kRoiK;
 }
 
+
+// Descriptor upload ring. The per-call descriptor block ([LUT][ItemDesc x n][tables]) changes with
+// every new ROI set; it is written into a pinned host slot and copied on a private copy stream into a
+// device slot of the same index, so the host never blocks on the copy and the copy of call k+1 can
+// overlap the kernel of call k. Slot reuse is fenced by two events: `copied` (the H2D out of the host
+// slot finished) and `used` (the last kernel that read the device slot finished).
+struct DescRing {
+    static constexpr int N = 3;
+    uint8_t* host[N] = {};
+    uint8_t* dev[N] = {};
+    size_t cap[N] = {};
+    hipEvent_t copied[N] = {};
+    hipEvent_t used[N] = {};
+    bool copied_rec[N] = {};
+    bool used_rec[N] = {};
+    hipStream_t copy = nullptr;
+    int cur = -1;
+    std::vector<uint8_t> last;  // bytes currently held by dev[cur]
+};
+
 }  // namespace
 
 struct evam_pp {
@@ -1504,14 +1524,77 @@ struct evam_pp {
     hipStream_t stream = nullptr;
     int opt_stats = 0, opt_timing = 0;
     evam_pp_stats stats{};
-    // descriptor block: [LUT 3 KB][ItemDesc x n] in device memory; re-uploaded only when it changes.
-    uint8_t* d_block = nullptr;
-    size_t d_block_cap = 0;
-    std::vector<uint8_t> h_block, h_last;
+    std::vector<uint8_t> h_block;  // this call's descriptor block, built on the host
+    DescRing ring;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool timed = false;
     TabCache tab_cache;
+    evam_preproc lut_key{};        // cfg the cached LUT was built from (norm fields + dtype)
+    bool lut_valid = false;
+    float lut[768];
 };
+
+namespace {
+
+void ring_release(DescRing& r) {
+    for (int k = 0; k < DescRing::N; k++) {
+        if (r.host[k]) (void)hipHostFree(r.host[k]);
+        if (r.dev[k]) (void)hipFree(r.dev[k]);
+        if (r.copied[k]) (void)hipEventDestroy(r.copied[k]);
+        if (r.used[k]) (void)hipEventDestroy(r.used[k]);
+        r.host[k] = r.dev[k] = nullptr;
+        r.copied[k] = r.used[k] = nullptr;
+        r.cap[k] = 0;
+    }
+    if (r.copy) (void)hipStreamDestroy(r.copy);
+    r.copy = nullptr;
+    r.cur = -1;
+}
+
+// Make h->h_block visible to kernels on h->stream; returns the device copy. Re-uploads only when the
+// bytes differ from the block already resident in the current slot.
+int ring_upload(evam_pp* h, const uint8_t** out) {
+    DescRing& r = h->ring;
+    const size_t n = h->h_block.size();
+    if (r.cur >= 0 && r.last.size() == n && memcmp(r.last.data(), h->h_block.data(), n) == 0) {
+        *out = r.dev[r.cur];
+        return EVAM_PP_OK;
+    }
+    if (!r.copy) {
+        HIP_TRY(hipStreamCreateWithFlags(&r.copy, hipStreamNonBlocking));
+        for (int k = 0; k < DescRing::N; k++) {
+            HIP_TRY(hipEventCreateWithFlags(&r.copied[k], hipEventDisableTiming));
+            HIP_TRY(hipEventCreateWithFlags(&r.used[k], hipEventDisableTiming));
+        }
+    }
+    const int k = (r.cur + 1) % DescRing::N;
+    if (r.copied_rec[k]) HIP_TRY(hipEventSynchronize(r.copied[k]));  // host slot free
+    if (r.cap[k] < n) {
+        if (r.used_rec[k]) HIP_TRY(hipEventSynchronize(r.used[k]));  // device slot no longer read
+        if (r.host[k]) HIP_TRY(hipHostFree(r.host[k]));
+        if (r.dev[k]) HIP_TRY(hipFree(r.dev[k]));
+        r.host[k] = r.dev[k] = nullptr;
+        r.cap[k] = 0;
+        const size_t cap = std::max<size_t>(n * 2, 64 * 1024);
+        if (hipHostMalloc((void**)&r.host[k], cap, hipHostMallocDefault) != hipSuccess)
+            return fail(EVAM_PP_ERR_OOM, "evam_pp_run: hipHostMalloc(%zu) failed", cap);
+        if (hipMalloc((void**)&r.dev[k], cap) != hipSuccess)
+            return fail(EVAM_PP_ERR_OOM, "evam_pp_run: hipMalloc(%zu) failed", cap);
+        r.cap[k] = cap;
+    }
+    memcpy(r.host[k], h->h_block.data(), n);
+    if (r.used_rec[k]) HIP_TRY(hipStreamWaitEvent(r.copy, r.used[k], 0));
+    HIP_TRY(hipMemcpyAsync(r.dev[k], r.host[k], n, hipMemcpyHostToDevice, r.copy));
+    HIP_TRY(hipEventRecord(r.copied[k], r.copy));
+    r.copied_rec[k] = true;
+    HIP_TRY(hipStreamWaitEvent(h->stream, r.copied[k], 0));
+    r.cur = k;
+    r.last.assign(h->h_block.begin(), h->h_block.end());
+    *out = r.dev[k];
+    return EVAM_PP_OK;
+}
+
+}  // namespace
 
 extern "C" {
 
@@ -1545,10 +1628,11 @@ int evam_pp_create(int hip_device, void* hip_stream, evam_pp** out) {
 void evam_pp_destroy(evam_pp* h) {
     if (!h) return;
     (void)hipSetDevice(h->device);
-    if (h->d_block) {
+    if (h->ring.copy) {
         (void)hipStreamSynchronize(h->stream);
-        (void)hipFree(h->d_block);
+        (void)hipStreamSynchronize(h->ring.copy);
     }
+    ring_release(h->ring);
     if (h->ev0) (void)hipEventDestroy(h->ev0);
     if (h->ev1) (void)hipEventDestroy(h->ev1);
     delete h;
@@ -1696,8 +1780,24 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
         tab_off[f] = nbytes;
         nbytes += sizeof(XTab) * (size_t)DW + sizeof(YTab) * (size_t)DH;
     }
-    h->h_block.assign(nbytes, 0);
-    if (cfg->out_dtype == EVAM_DTYPE_F32) build_lut(*cfg, reinterpret_cast<float*>(h->h_block.data()));
+    h->h_block.resize(nbytes);
+    if (cfg->out_dtype == EVAM_DTYPE_F32) {
+        // The LUT depends only on the normalisation fields: rebuilt when they change.
+        evam_preproc key{};
+        key.out_dtype = cfg->out_dtype;
+        key.norm_flags = cfg->norm_flags;
+        memcpy(key.range, cfg->range, sizeof(key.range));
+        memcpy(key.mean, cfg->mean, sizeof(key.mean));
+        memcpy(key.std, cfg->std, sizeof(key.std));
+        if (!h->lut_valid || memcmp(&key, &h->lut_key, sizeof(key)) != 0) {
+            build_lut(*cfg, h->lut);
+            h->lut_key = key;
+            h->lut_valid = true;
+        }
+        memcpy(h->h_block.data(), h->lut, kLutBytes);
+    } else {
+        memset(h->h_block.data(), 0, kLutBytes);
+    }
     ItemDesc* desc = reinterpret_cast<ItemDesc*>(h->h_block.data() + kLutBytes);
     int order = 0;
     int first[4] = {0, 0, 0, 0};
@@ -1724,23 +1824,8 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
     }
 
     HIP_TRY(hipSetDevice(h->device));
-    if (h->h_last.size() != nbytes || memcmp(h->h_last.data(), h->h_block.data(), nbytes) != 0) {
-        if (nbytes > h->d_block_cap) {
-            if (h->d_block) {
-                HIP_TRY(hipStreamSynchronize(h->stream));
-                HIP_TRY(hipFree(h->d_block));
-                h->d_block = nullptr;
-                h->d_block_cap = 0;
-            }
-            const size_t cap = std::max<size_t>(nbytes * 2, 64 * 1024);
-            if (hipMalloc(&h->d_block, cap) != hipSuccess)
-                return fail(EVAM_PP_ERR_OOM, "evam_pp_run: hipMalloc(%zu) failed", cap);
-            h->d_block_cap = cap;
-        }
-        // Stream-ordered after every earlier launch that read the block, so it is safe to overwrite.
-        HIP_TRY(hipMemcpyAsync(h->d_block, h->h_block.data(), nbytes, hipMemcpyHostToDevice, h->stream));
-        h->h_last = h->h_block;
-    }
+    const uint8_t* d_block = nullptr;
+    if (int rc = ring_upload(h, &d_block)) return rc;
 
     // ---- launches ----
     if (h->opt_timing) HIP_TRY(hipEventRecord(h->ev0, h->stream));
@@ -1750,9 +1835,9 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
         const int nsegx = tab_off[f] && env_int("EVAM_PP_STAGED", 1) ? staged_nsegx(f, max_ratio[f]) : 0;
         if (nsegx) {
             SParams sp{};
-            sp.items = reinterpret_cast<const ItemDesc*>(h->d_block + kLutBytes) + first[f];
-            sp.lut = reinterpret_cast<const float*>(h->d_block);
-            sp.xtab = reinterpret_cast<const XTab*>(h->d_block + tab_off[f]);
+            sp.items = reinterpret_cast<const ItemDesc*>(d_block + kLutBytes) + first[f];
+            sp.lut = reinterpret_cast<const float*>(d_block);
+            sp.xtab = reinterpret_cast<const XTab*>(d_block + tab_off[f]);
             sp.ytab = reinterpret_cast<const YTab*>(sp.xtab + DW);
             sp.dst = dst->data;
             sp.DW = DW; sp.DH = DH;
@@ -1778,9 +1863,9 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
         if (tab_off[f]) {
             const RowCfg rc = choose_row_tiles(DW, DH);
             RParams r{};
-            r.items = reinterpret_cast<const ItemDesc*>(h->d_block + kLutBytes) + first[f];
-            r.lut = reinterpret_cast<const float*>(h->d_block);
-            r.xtab = reinterpret_cast<const XTab*>(h->d_block + tab_off[f]);
+            r.items = reinterpret_cast<const ItemDesc*>(d_block + kLutBytes) + first[f];
+            r.lut = reinterpret_cast<const float*>(d_block);
+            r.xtab = reinterpret_cast<const XTab*>(d_block + tab_off[f]);
             r.ytab = reinterpret_cast<const YTab*>(r.xtab + DW);
             r.dst = dst->data;
             r.DW = DW; r.DH = DH;
@@ -1803,8 +1888,8 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
             QParams q{};
             int R = 0, lds = 0;
             if (env_int("EVAM_PP_ROI", 1) && plan_roi(f, geo, fmt, DW, DH, cfg->out_dtype, q, R, lds)) {
-                q.items = reinterpret_cast<const ItemDesc*>(h->d_block + kLutBytes) + first[f];
-                q.lut = reinterpret_cast<const float*>(h->d_block);
+                q.items = reinterpret_cast<const ItemDesc*>(d_block + kLutBytes) + first[f];
+                q.lut = reinterpret_cast<const float*>(d_block);
                 q.dst = dst->data;
                 q.color_rgb = cfg->color_order == EVAM_COLOR_RGB;
                 q.fill = (uint32_t)cfg->fill[0] | ((uint32_t)cfg->fill[1] << 8) | ((uint32_t)cfg->fill[2] << 16);
@@ -1818,8 +1903,8 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
         }
         const TileCfg t = choose_tiles(DW, DH, cfg->out_dtype);
         KParams p{};
-        p.items = reinterpret_cast<const ItemDesc*>(h->d_block + kLutBytes) + first[f];
-        p.lut = reinterpret_cast<const float*>(h->d_block);
+        p.items = reinterpret_cast<const ItemDesc*>(d_block + kLutBytes) + first[f];
+        p.lut = reinterpret_cast<const float*>(d_block);
         p.dst = dst->data;
         p.DW = DW; p.DH = DH;
         p.TW = t.TW; p.TH = t.TH;
@@ -1850,6 +1935,8 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
         if (e != hipSuccess) return fail(EVAM_PP_ERR_HIP, "kernel launch failed: %s", hipGetErrorString(e));
         launches++;
     }
+    HIP_TRY(hipEventRecord(h->ring.used[h->ring.cur], h->stream));
+    h->ring.used_rec[h->ring.cur] = true;
     if (h->opt_timing) HIP_TRY(hipEventRecord(h->ev1, h->stream));
     h->timed = h->opt_timing != 0;
 
