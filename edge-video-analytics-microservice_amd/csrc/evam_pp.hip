@@ -867,9 +867,60 @@ __global__ __launch_bounds__(kThreads) void evam_pp_staged(const SParams P) {
     }
 }
 
+struct Geom {
+    int x0, y0, cw, ch, rw, rh, ox, oy;
+};
+
+// ROI clipping / 4:2:0 even alignment / aspect-ratio geometry (rules documented in include/evam_pp.h).
+// Shared by the host planner and the ROI kernel, which derives every item's geometry from the raw
+// evam_roi on the device. Integer and IEEE-double operations only, so both sides agree bit for bit.
+// Returns 0 or EVAM_PP_ERR_EMPTY_ROI.
+__host__ __device__ inline int roi_clip(int f, int W, int H, bool has_roi, int rx, int ry, int rwid, int rhei, Geom& g) {
+    int x0 = 0, y0 = 0, x1 = W, y1 = H;
+    if (has_roi && rwid > 0 && rhei > 0) {
+        auto cl = [](int v, int hi) { return v < 0 ? 0 : (v > hi ? hi : v); };
+        x0 = cl(rx, W); y0 = cl(ry, H);
+        x1 = cl(rx + rwid, W); y1 = cl(ry + rhei, H);
+        if (f == kNV12 || f == kI420) {
+            x0 &= ~1; y0 &= ~1;
+            x1 = (x1 + 1) & ~1; x1 = x1 < W ? x1 : W;
+            y1 = (y1 + 1) & ~1; y1 = y1 < H ? y1 : H;
+        }
+    }
+    if (x1 - x0 <= 0 || y1 - y0 <= 0) return EVAM_PP_ERR_EMPTY_ROI;
+    g.x0 = x0; g.y0 = y0; g.cw = x1 - x0; g.ch = y1 - y0;
+    return 0;
+}
+
+__host__ __device__ inline int roi_geometry(int f, int W, int H, bool has_roi, int rx, int ry, int rwid, int rhei,
+                                            int mode, int placement, int DW, int DH, Geom& g) {
+    if (roi_clip(f, W, H, has_roi, rx, ry, rwid, rhei, g)) return EVAM_PP_ERR_EMPTY_ROI;
+    g.ox = 0; g.oy = 0;
+    if (mode == EVAM_RESIZE_NO_ASPECT) {
+        g.rw = DW; g.rh = DH;
+        return 0;
+    }
+    const double sx = (double)DW / g.cw, sy = (double)DH / g.ch;
+    const bool x_dom = mode == EVAM_RESIZE_ASPECT ? (sx <= sy) : (sx >= sy);
+    if (x_dom) { g.rw = DW; g.rh = (int)(g.ch * sx); }
+    else { g.rh = DH; g.rw = (int)(g.cw * sy); }
+    g.rw = g.rw > 1 ? g.rw : 1;
+    g.rh = g.rh > 1 ? g.rh : 1;
+    if (mode == EVAM_RESIZE_ASPECT) {
+        g.rw = g.rw < DW ? g.rw : DW;
+        g.rh = g.rh < DH ? g.rh : DH;
+        if (placement == EVAM_PLACE_CENTER) { g.ox = (DW - g.rw) / 2; g.oy = (DH - g.rh) / 2; }
+    } else {
+        g.rw = g.rw > DW ? g.rw : DW;
+        g.rh = g.rh > DH ? g.rh : DH;
+        g.ox = -((g.rw - DW) / 2);
+        g.oy = -((g.rh - DH) / 2);
+    }
+    return 0;
+}
+
 // Source footprint of one item's visible output columns: the 16 B-aligned byte window [fs, fs + 16 n)
-// of a luma / packed row (fsY, nY) and of a chroma row (fsC, nC) that its taps read. Shared by the
-// ROI kernel (device) and its host-side planner, so both agree on the slot size.
+// of a luma / packed row (fsY, nY) and of a chroma row (fsC, nC) that its taps read.
 __host__ __device__ inline void item_footprint(int FMT, int bpp, int x0, int cw, int rw, int ox, double scx, int DW,
                                                int& fsY, int& nY, int& fsC, int& nC) {
     fsY = nY = fsC = nC = 0;
@@ -891,60 +942,107 @@ __host__ __device__ inline void item_footprint(int FMT, int bpp, int x0, int cw,
     }
 }
 
-constexpr int kRoiK = 4;  // max pixels per lane per row group in the ROI kernel
+// Upper bound of the staged bytes of one output row of an item whose crop is cw pixels wide (both
+// luma / packed taps plus both chroma taps of every chroma plane), for the host's buffer sizing.
+inline int row_bytes_bound(int f, int cw) {
+    const int bpp = f == kBGRX ? 4 : (f == kBGR ? 3 : 1);
+    const int segY = ((cw * bpp + 15) / 16 + 1) * 16;
+    const int segC = f == kNV12 ? ((cw + 1 + 15) / 16 + 1) * 16 : (f == kI420 ? ((cw / 2 + 1 + 15) / 16 + 1) * 16 : 0);
+    const int npc = f == kI420 ? 2 : (f == kNV12 ? 1 : 0);
+    return 2 * segY + 2 * npc * segC;
+}
+
+// One decoded source, for kernels that resolve items on the device.
+struct alignas(16) SrcDesc {  // 48 B
+    const uint8_t* plane[3];
+    int32_t pitch[3];
+    int32_t width, height;
+    int32_t pad_;
+};
+static_assert(sizeof(SrcDesc) == 48, "SrcDesc layout");
+static_assert(sizeof(evam_roi) == 20, "evam_roi layout");
+
+constexpr int kRoiK = 8;  // max pixels per lane per row group in the ROI kernel
 
 struct QParams {
-    const ItemDesc* items;
-    const float* lut;    // [3][256]
+    const SrcDesc* srcs;
+    const evam_roi* rois;     // the caller's ROI array, as passed to evam_pp_run
+    const int32_t* index;     // item indices handled by this launch (NULL: 0..n-1)
+    const float* lut;         // [3][256]
     void* dst;
     int DW, DH;
     int TH, tiles_per_item;   // a tile is all DW columns x TH rows of one item
+    int mode, placement;      // evam_resize_mode, evam_placement
+    int slot_offset, slot_stride;
     int offXT, offYT, offBuf; // LDS carve: [LUT][XTab x DW][YTab x TH][buf0][buf1]
-    int slot;                 // bytes of one staged row segment (multiple of 16, <= kSlot)
-    int buf_bytes;            // one staging buffer: slots x slot
-    int K;                    // pixels per lane per group: ceil(R * DW / 256) <= kRoiK
-    int nfull;                // floor(R * DW / 256): k-steps in which every lane of every wave stores
+    int buf_bytes;            // one staging buffer
     int color_rgb;
     uint32_t fill;
 };
 
+template <int N>
+__device__ __forceinline__ void wait_vmcnt_stores(int nk) {
+    // s_waitcnt takes an immediate: vmcnt(N * nk) for the wave-uniform store-step count nk.
+    switch (nk) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(%0)" :: "n"(N) : "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * N) : "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(%0)" :: "n"(3 * N) : "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(%0)" :: "n"(4 * N) : "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(%0)" :: "n"(5 * N) : "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(%0)" :: "n"(6 * N) : "memory"); break;
+    case 7: asm volatile("s_waitcnt vmcnt(%0)" :: "n"(7 * N) : "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(%0)" :: "n"(8 * N) : "memory"); break;
+    }
+}
+
 // Staged kernel for batches whose items differ in geometry (gvaclassify ROI batches, mixed crops).
-// One workgroup owns all DW columns x TH rows of one item. It builds that item's OpenCV coefficient
-// tables in LDS (device-side, the same double/float sequence as the host tables), then walks the tile
-// in groups of R output rows exactly like evam_pp_staged:
-//  * the group's source row segments (the item's whole visible footprint, <= slot bytes) arrive in LDS
-//    by LDS-DMA while the previous group is converted;
-//  * taps are LDS byte reads.
-// The R x DW pixels of a group are packed densely onto the 256 lanes (pixel p = tid + 256 k). Narrow
-// outputs such as 72x72 classifier inputs keep every lane busy and every store row-contiguous; a
-// 64-column tiling would leave most lanes of the second segment idle.
-template <int FMT, int OUT, int R>
+// The host passes the caller's raw ROI array; each workgroup resolves its item's crop, resized size
+// and placement on the device (roi_geometry, the host's own rules) and owns all DW columns x TH rows
+// of that item:
+//  * OpenCV coefficient tables for its columns / rows are built in LDS (exact double/float sequence);
+//  * rows are walked in groups whose size R adapts to the item: as many output rows as the staging
+//    buffer holds for this crop's width (narrow crops: many rows per group, few barriers), capped so
+//    the R x DW pixels cover the 256 lanes at most kRoiK times;
+//  * a group's source row segments (luma taps and chroma taps, each exactly the item's footprint)
+//    are packed back to back in LDS and arrive by LDS-DMA while the previous group is converted;
+//  * the group's R x DW output pixels are packed densely onto the lanes (pixel p = tid + 256 k), so a
+//    72-wide classifier row keeps every lane busy and every store is row-contiguous.
+template <int FMT, int OUT>
 __global__ __launch_bounds__(kThreads) void evam_pp_roi(const QParams P) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     using T = FmtTraits<FMT>;
     constexpr bool kYUV = FMT == kNV12 || FMT == kI420;
     constexpr int NP = FMT == kI420 ? 3 : (FMT == kNV12 ? 2 : 1);
-    constexpr int NS = 2 * R * NP;
-    static_assert(NS % 4 == 0, "slots are issued four waves at a time");
+    constexpr int NKIND = 2 * NP;  // segments per output row: (plane, tap)
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int t = blockIdx.x;
-    const int item = t / P.tiles_per_item;
-    const int ty = t - item * P.tiles_per_item;
-    const __attribute__((address_space(4))) ItemDesc* it =
-        (const __attribute__((address_space(4))) ItemDesc*)(P.items) + item;
-    const uint8_t* p0 = it->plane[0];
-    const uint8_t* p1 = it->plane[1];
-    const uint8_t* p2 = it->plane[2];
-    const int pitch0 = it->pitch[0], pitch1 = it->pitch[1], pitch2 = it->pitch[2];
-    const int x0 = it->x0, y0 = it->y0, cw = it->cw, ch = it->ch;
-    const int rw = it->rw, rh = it->rh, ox = it->ox, oy = it->oy;
-    const double scx = it->scale_x, scy = it->scale_y;
+    const int li = t / P.tiles_per_item;
+    const int ty = t - li * P.tiles_per_item;
+    const int item = P.index ? ((const __attribute__((address_space(4))) int32_t*)P.index)[li] : li;
+    const __attribute__((address_space(4))) evam_roi* roi =
+        (const __attribute__((address_space(4))) evam_roi*)(P.rois) + item;
+    const __attribute__((address_space(4))) SrcDesc* src =
+        (const __attribute__((address_space(4))) SrcDesc*)(P.srcs) + roi->src_index;
+    Geom g;
+    roi_geometry(FMT, src->width, src->height, true, roi->x, roi->y, roi->w, roi->h, P.mode, P.placement, P.DW,
+                 P.DH, g);  // never empty: the host validated every item
+    const int x0 = __builtin_amdgcn_readfirstlane(g.x0), y0 = __builtin_amdgcn_readfirstlane(g.y0);
+    const int cw = __builtin_amdgcn_readfirstlane(g.cw), ch = __builtin_amdgcn_readfirstlane(g.ch);
+    const int rw = __builtin_amdgcn_readfirstlane(g.rw), rh = __builtin_amdgcn_readfirstlane(g.rh);
+    const int ox = __builtin_amdgcn_readfirstlane(g.ox), oy = __builtin_amdgcn_readfirstlane(g.oy);
+    const double scx = 1. / ((double)rw / cw), scy = 1. / ((double)rh / ch);
+    const uint8_t* p0 = src->plane[0];
+    const uint8_t* p1 = src->plane[1];
+    const uint8_t* p2 = src->plane[2];
+    const int pitch0 = src->pitch[0], pitch1 = src->pitch[1], pitch2 = src->pitch[2];
     const size_t plane = (size_t)P.DW * P.DH;
     const size_t esz = OUT == 1 ? 4 : 1;
-    uint8_t* const d0 = reinterpret_cast<uint8_t*>(P.dst) + (size_t)it->slot * 3 * plane * esz;
+    const int slot = P.slot_offset + item * P.slot_stride;
+    uint8_t* const d0 = reinterpret_cast<uint8_t*>(P.dst) + (size_t)slot * 3 * plane * esz;
     uint8_t* const d1 = d0 + plane * esz;
     uint8_t* const d2 = d1 + plane * esz;
     const __amdgpu_buffer_rsrc_t rsY = __builtin_amdgcn_make_buffer_rsrc((void*)p0, (short)0, 0x7FFFFFFF, 0x00020000);
@@ -960,8 +1058,9 @@ __global__ __launch_bounds__(kThreads) void evam_pp_roi(const QParams P) {
     }
     XTab* xt = reinterpret_cast<XTab*>(smem + P.offXT);
     YTab* yt = reinterpret_cast<YTab*>(smem + P.offYT);
+    const int DW = P.DW;
     const int Y0 = ty * P.TH, Y1 = min(Y0 + P.TH, P.DH), rows = Y1 - Y0;
-    for (int X = tid; X < P.DW; X += kThreads) {
+    for (int X = tid; X < DW; X += kThreads) {
         XTab e;
         e.s0 = 0; e.s1 = 0; e.a0 = 0; e.a1 = 0; e.pad = 0;
         const int dx = X - ox;
@@ -990,31 +1089,41 @@ __global__ __launch_bounds__(kThreads) void evam_pp_roi(const QParams P) {
         yt[ly] = e;
     }
     int fsY, nY, fsC, nC;
-    item_footprint(FMT, T::bpp, x0, cw, rw, ox, scx, P.DW, fsY, nY, fsC, nC);
+    item_footprint(FMT, T::bpp, x0, cw, rw, ox, scx, DW, fsY, nY, fsC, nC);
     fsY = __builtin_amdgcn_readfirstlane(fsY);
     nY = __builtin_amdgcn_readfirstlane(nY);
     fsC = __builtin_amdgcn_readfirstlane(fsC);
     nC = __builtin_amdgcn_readfirstlane(nC);
+    // Packed row layout in a staging buffer: [Y tap0 | Y tap1 | C tap0 | C tap1 (| V tap0 | V tap1)].
+    const int segY = nY * 16, segC = nC * 16;
+    const int rowb = 2 * segY + 2 * (NP - 1) * segC;
+    int R = rowb > 0 ? P.buf_bytes / rowb : rows;
+    R = min(R, (kRoiK * kThreads) / DW);
+    R = max(1, min(R, rows));
+    const int npx = R * DW;                       // pixels per full group
+    const int K = (npx + kThreads - 1) / kThreads;
+    // store steps this wave issues in a full group: k with some lane of the wave holding a pixel
+    int nk_w = 0;
+    for (int k = 0; k < K; k++) nk_w += (k * kThreads + wave * 64 < npx) ? 1 : 0;
     __syncthreads();
 
     const int f0 = P.fill & 0xFF, f1 = (P.fill >> 8) & 0xFF, f2 = (P.fill >> 16) & 0xFF;
-    // Per-lane pixel state for k = 0..K-1, identical for every group: row in the group, element offset
-    // inside the group, packed LDS tap offsets (tap 0 low, tap 1 high half) and horizontal weights.
+    // Per-lane pixel state for k < K, identical for every group: row of the pixel inside the group
+    // (as its LDS row offset), packed LDS tap offsets (tap 0 low, tap 1 high half), horizontal weights.
+    uint32_t lb[kRoiK], lY[kRoiK], lC[kRoiK], wa[kRoiK];
     int rr[kRoiK];
-    uint32_t rc[kRoiK], lY[kRoiK], lC[kRoiK], wa[kRoiK];
-    bool val[kRoiK];
 #pragma unroll
     for (int k = 0; k < kRoiK; k++) {
         const int p = tid + k * kThreads;
-        val[k] = k < P.K && p < R * P.DW;
-        const int r = val[k] ? p / P.DW : 0;
-        const int c = val[k] ? p - r * P.DW : 0;
-        rr[k] = r;
-        rc[k] = (uint32_t)p;
+        const bool v = k < K && p < npx;
+        const int r = v ? p / DW : 0;
+        const int c = v ? p - r * DW : 0;
+        rr[k] = v ? r : -1;
+        lb[k] = (uint32_t)(r * rowb);
         const XTab e = xt[c];
         wa[k] = (uint32_t)e.a0 | ((uint32_t)e.a1 << 16);
         lY[k] = lC[k] = 0;
-        if (val[k] && wa[k] != 0) {
+        if (v && wa[k] != 0) {
             const int ca = x0 + e.s0, cb = x0 + e.s1;
             lY[k] = (uint32_t)(ca * T::bpp - fsY) | ((uint32_t)(cb * T::bpp - fsY) << 16);
             if constexpr (FMT == kNV12)
@@ -1024,16 +1133,13 @@ __global__ __launch_bounds__(kThreads) void evam_pp_roi(const QParams P) {
         }
     }
     const int ngroups = (rows + R - 1) / R;
-    const int slot = P.slot;
 
-    auto issue = [&](int g, uint8_t* buf) {
+    auto issue = [&](int grp, uint8_t* buf) {
         if (nY == 0) return;  // no visible columns: every pixel is fill
-#pragma unroll
-        for (int s0 = 0; s0 < NS; s0 += 4) {
-            const int s = s0 + wave;
-            const int pl = s / (2 * R), loc = s - pl * 2 * R, r = loc >> 1, tap = loc & 1;
-            const int ly = g * R + r;
-            if (ly >= rows) continue;
+        const int nseg = NKIND * min(R, rows - grp * R);
+        for (int s = wave; s < nseg; s += 4) {
+            const int r = s / NKIND, kind = s - r * NKIND, pl = kind >> 1, tap = kind & 1;
+            const int ly = grp * R + r;
             const int b0 = __builtin_amdgcn_readfirstlane(yt[ly].b0);
             const int b1 = __builtin_amdgcn_readfirstlane(yt[ly].b1);
             if ((b0 | b1) == 0) continue;  // padding row: nothing to stage
@@ -1042,25 +1148,28 @@ __global__ __launch_bounds__(kThreads) void evam_pp_roi(const QParams P) {
             const int yr = tap ? yb : ya;
             if (pl > 0 && tap && (ya >> 1) == (yb >> 1)) continue;  // chroma row shared by both taps
             const int nck = pl == 0 ? nY : nC;
-            if (lane < nck) {
-                __attribute__((address_space(3))) void* dstl =
-                    (__attribute__((address_space(3))) void*)(buf + s * slot);
-                if (pl == 0)
-                    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsY, dstl, 16, lane * 16, yr * pitch0 + fsY, 0, 0);
-                else if (pl == 1)
-                    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsC, dstl, 16, lane * 16, (yr >> 1) * pitch1 + fsC, 0, 0);
-                else
-                    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsV, dstl, 16, lane * 16, (yr >> 1) * pitch2 + fsC, 0, 0);
+            uint8_t* dst = buf + r * rowb + (pl == 0 ? tap * segY : 2 * segY + (pl - 1) * 2 * segC + tap * segC);
+            for (int c = 0; c < nck; c += 64) {
+                if (lane + c < nck) {
+                    __attribute__((address_space(3))) void* dstl = (__attribute__((address_space(3))) void*)(dst + c * 16);
+                    if (pl == 0)
+                        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsY, dstl, 16, (lane + c) * 16, yr * pitch0 + fsY, 0, 0);
+                    else if (pl == 1)
+                        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsC, dstl, 16, (lane + c) * 16, (yr >> 1) * pitch1 + fsC, 0, 0);
+                    else
+                        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsV, dstl, 16, (lane + c) * 16, (yr >> 1) * pitch2 + fsC, 0, 0);
+                }
             }
         }
     };
 
-    auto compute = [&](int g, const uint8_t* buf) {
-        const uint32_t gbase = (uint32_t)((Y0 + g * R) * P.DW);
+    auto compute = [&](int grp, const uint8_t* buf) {
+        const uint32_t gbase = (uint32_t)((Y0 + grp * R) * DW);
 #pragma unroll
         for (int k = 0; k < kRoiK; k++) {
-            const int ly = g * R + rr[k];
-            if (!val[k] || ly >= rows) continue;
+            if (k >= K) break;
+            const int ly = grp * R + rr[k];
+            if (rr[k] < 0 || ly >= rows) continue;
             const YTab e = yt[ly];
             int v[3];
             if ((e.b0 | e.b1) == 0 || wa[k] == 0) {  // letterbox padding row / column
@@ -1068,14 +1177,14 @@ __global__ __launch_bounds__(kThreads) void evam_pp_roi(const QParams P) {
             } else {
                 const uint32_t a0 = wa[k] & 0xFFFF, a1 = wa[k] >> 16;
                 const uint32_t tY0 = lY[k] & 0xFFFF, tY1 = lY[k] >> 16;
-                const uint8_t* sy0 = buf + (2 * rr[k]) * slot;
-                const uint8_t* sy1 = sy0 + slot;
+                const uint8_t* sy0 = buf + lb[k];
+                const uint8_t* sy1 = sy0 + segY;
                 int c[4][3];
                 if constexpr (kYUV) {
                     const uint32_t tC0 = lC[k] & 0xFFFF, tC1 = lC[k] >> 16;
                     const int ya = y0 + e.r0, yb = y0 + e.r1;
-                    const uint8_t* sc0 = buf + (2 * R + 2 * rr[k]) * slot;
-                    const uint8_t* sc1 = (ya >> 1) == (yb >> 1) ? sc0 : sc0 + slot;
+                    const uint8_t* sc0 = sy0 + 2 * segY;
+                    const uint8_t* sc1 = (ya >> 1) == (yb >> 1) ? sc0 : sc0 + segC;
                     Chroma<FMT> cA, cB, cC, cD;
                     if constexpr (FMT == kNV12) {
                         cA.u = *reinterpret_cast<const uint16_t*>(sc0 + tC0);
@@ -1083,8 +1192,8 @@ __global__ __launch_bounds__(kThreads) void evam_pp_roi(const QParams P) {
                         cC.u = *reinterpret_cast<const uint16_t*>(sc1 + tC0);
                         cD.u = *reinterpret_cast<const uint16_t*>(sc1 + tC1);
                     } else {
-                        const uint8_t* sv0 = sc0 + 2 * R * slot;
-                        const uint8_t* sv1 = sc1 + 2 * R * slot;
+                        const uint8_t* sv0 = sc0 + 2 * segC;
+                        const uint8_t* sv1 = sc1 + 2 * segC;
                         cA.u = sc0[tC0]; cA.v = sv0[tC0];
                         cB.u = sc0[tC1]; cB.v = sv0[tC1];
                         cC.u = sc1[tC0]; cC.v = sv1[tC0];
@@ -1115,7 +1224,7 @@ __global__ __launch_bounds__(kThreads) void evam_pp_roi(const QParams P) {
                 }
                 if (P.color_rgb) { const int tmp = v[0]; v[0] = v[2]; v[2] = tmp; }
             }
-            const uint32_t vo = (gbase + rc[k]) * (uint32_t)esz;
+            const uint32_t vo = (gbase + (uint32_t)(tid + k * kThreads)) * (uint32_t)esz;
             if constexpr (OUT == 1) {
                 __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lut_s[v[0]]), rsD0, vo, 0, 0);
                 __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lut_s[256 + v[1]]), rsD1, vo, 0, 0);
@@ -1131,20 +1240,16 @@ __global__ __launch_bounds__(kThreads) void evam_pp_roi(const QParams P) {
     uint8_t* const buf0 = smem + P.offBuf;
     uint8_t* const buf1 = buf0 + P.buf_bytes;
     issue(0, buf0);
-    for (int g = 0; g < ngroups; g++) {
-        // Wait for group g's DMA. After a full group every wave issued at least 3 * nfull stores behind
-        // that DMA, so those may stay in flight; otherwise drain everything.
-        const bool prev_full = g > 0 && g * R <= rows;
-        const int keep = prev_full ? P.nfull : 0;
-        if (keep >= 4) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-        else if (keep == 3) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
-        else if (keep == 2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-        else if (keep == 1) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    for (int grp = 0; grp < ngroups; grp++) {
+        // Wait for this wave's share of group grp's DMA. Group grp-1 was full (only the last group can
+        // be partial), so this wave issued at least 3 stores for each of its nk_w store steps after
+        // that DMA: those may stay in flight.
+        if (grp > 0) wait_vmcnt_stores<3>(nk_w);
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();  // every wave's DMA for g landed; every wave done reading g-1
-        if (g + 1 < ngroups) issue(g + 1, (g & 1) ? buf0 : buf1);
-        compute(g, (g & 1) ? buf1 : buf0);
+        __builtin_amdgcn_s_barrier();  // every wave's DMA for grp landed; every wave done reading grp-1
+        if (grp + 1 < ngroups) issue(grp + 1, (grp & 1) ? buf0 : buf1);
+        compute(grp, (grp & 1) ? buf1 : buf0);
     }
 }
 
@@ -1184,46 +1289,9 @@ int fmt_id(int fourcc) {
 int fmt_bpp(int f) { return f == kBGRX ? 4 : (f == kBGR ? 3 : 1); }
 int fmt_nplanes(int f) { return f == kNV12 ? 2 : (f == kI420 ? 3 : 1); }
 
-struct Geom {
-    int x0, y0, cw, ch, rw, rh, ox, oy;
-};
-
-// ROI clipping / 4:2:0 even alignment / aspect-ratio geometry. Rules documented in include/evam_pp.h.
 int item_geometry(int f, int W, int H, const evam_roi* roi, const evam_preproc& cfg, int DW, int DH, Geom& g) {
-    int x0 = 0, y0 = 0, x1 = W, y1 = H;
-    if (roi && roi->w > 0 && roi->h > 0) {
-        auto cl = [](int v, int hi) { return v < 0 ? 0 : (v > hi ? hi : v); };
-        x0 = cl(roi->x, W); y0 = cl(roi->y, H);
-        x1 = cl(roi->x + roi->w, W); y1 = cl(roi->y + roi->h, H);
-        if (f == kNV12 || f == kI420) {
-            x0 &= ~1; y0 &= ~1;
-            x1 = std::min(W, (x1 + 1) & ~1);
-            y1 = std::min(H, (y1 + 1) & ~1);
-        }
-    }
-    if (x1 - x0 <= 0 || y1 - y0 <= 0) return EVAM_PP_ERR_EMPTY_ROI;
-    g.x0 = x0; g.y0 = y0; g.cw = x1 - x0; g.ch = y1 - y0; g.ox = 0; g.oy = 0;
-    if (cfg.resize_mode == EVAM_RESIZE_NO_ASPECT) {
-        g.rw = DW; g.rh = DH;
-        return 0;
-    }
-    const double sx = (double)DW / g.cw, sy = (double)DH / g.ch;
-    const bool x_dom = cfg.resize_mode == EVAM_RESIZE_ASPECT ? (sx <= sy) : (sx >= sy);
-    if (x_dom) { g.rw = DW; g.rh = (int)(g.ch * sx); }
-    else { g.rh = DH; g.rw = (int)(g.cw * sy); }
-    g.rw = std::max(g.rw, 1);
-    g.rh = std::max(g.rh, 1);
-    if (cfg.resize_mode == EVAM_RESIZE_ASPECT) {
-        g.rw = std::min(g.rw, DW);
-        g.rh = std::min(g.rh, DH);
-        if (cfg.placement == EVAM_PLACE_CENTER) { g.ox = (DW - g.rw) / 2; g.oy = (DH - g.rh) / 2; }
-    } else {
-        g.rw = std::max(g.rw, DW);
-        g.rh = std::max(g.rh, DH);
-        g.ox = -((g.rw - DW) / 2);
-        g.oy = -((g.rh - DH) / 2);
-    }
-    return 0;
+    return roi_geometry(f, W, H, roi != nullptr, roi ? roi->x : 0, roi ? roi->y : 0, roi ? roi->w : 0,
+                        roi ? roi->h : 0, cfg.resize_mode, cfg.placement, DW, DH, g);
 }
 
 void build_lut(const evam_preproc& cfg, float* lut) {
@@ -1440,62 +1508,46 @@ hipError_t launch(int f, int out, const KParams& p, int grid, int lds, hipStream
     }
 }
 
-template <int FMT, int OUT, int R>
+template <int FMT, int OUT>
 hipError_t launch_roi_t(const QParams& p, int grid, int lds, hipStream_t s) {
-    hipLaunchKernelGGL((evam_pp_roi<FMT, OUT, R>), dim3(grid), dim3(kThreads), lds, s, p);
+    if (lds > 64 * 1024) {
+        hipError_t e = hipFuncSetAttribute((const void*)evam_pp_roi<FMT, OUT>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL((evam_pp_roi<FMT, OUT>), dim3(grid), dim3(kThreads), lds, s, p);
     return hipGetLastError();
 }
 
-template <int FMT, int OUT>
-hipError_t launch_roi_r(int R, const QParams& p, int grid, int lds, hipStream_t s) {
-    return R == 4 ? launch_roi_t<FMT, OUT, 4>(p, grid, lds, s) : launch_roi_t<FMT, OUT, 2>(p, grid, lds, s);
-}
-
-hipError_t launch_roi(int f, int out, int R, const QParams& p, int grid, int lds, hipStream_t s) {
+hipError_t launch_roi(int f, int out, const QParams& p, int grid, int lds, hipStream_t s) {
     switch (f * 2 + out) {
-    case kNV12 * 2 + 0: return launch_roi_r<kNV12, 0>(R, p, grid, lds, s);
-    case kNV12 * 2 + 1: return launch_roi_r<kNV12, 1>(R, p, grid, lds, s);
-    case kI420 * 2 + 0: return launch_roi_r<kI420, 0>(R, p, grid, lds, s);
-    case kI420 * 2 + 1: return launch_roi_r<kI420, 1>(R, p, grid, lds, s);
-    case kBGRX * 2 + 0: return launch_roi_r<kBGRX, 0>(R, p, grid, lds, s);
-    case kBGRX * 2 + 1: return launch_roi_r<kBGRX, 1>(R, p, grid, lds, s);
-    case kBGR * 2 + 0: return launch_roi_r<kBGR, 0>(R, p, grid, lds, s);
-    default: return launch_roi_r<kBGR, 1>(R, p, grid, lds, s);
+    case kNV12 * 2 + 0: return launch_roi_t<kNV12, 0>(p, grid, lds, s);
+    case kNV12 * 2 + 1: return launch_roi_t<kNV12, 1>(p, grid, lds, s);
+    case kI420 * 2 + 0: return launch_roi_t<kI420, 0>(p, grid, lds, s);
+    case kI420 * 2 + 1: return launch_roi_t<kI420, 1>(p, grid, lds, s);
+    case kBGRX * 2 + 0: return launch_roi_t<kBGRX, 0>(p, grid, lds, s);
+    case kBGRX * 2 + 1: return launch_roi_t<kBGRX, 1>(p, grid, lds, s);
+    case kBGR * 2 + 0: return launch_roi_t<kBGR, 0>(p, grid, lds, s);
+    default: return launch_roi_t<kBGR, 1>(p, grid, lds, s);
     }
 }
 
-// ROI-kernel plan for one format group with per-item geometry: rows per group R (the R x DW pixels
-// of a group cover the 256 lanes at most kRoiK times) and the LDS slot that fits every item's
-// footprint. Returns false when the group needs the generic kernel (very wide outputs, or a
-// footprint beyond kSlot, i.e. an extreme downscale of a wide crop).
-bool plan_roi(int f, const std::vector<Geom>& geo, const std::vector<int>& fmt, int DW, int DH, int out_dtype,
-              QParams& q, int& R, int& lds) {
-    if (DW > 512) return false;
-    R = DW <= 256 ? 4 : 2;
-    int need = 16;
-    for (size_t i = 0; i < geo.size(); i++) {
-        if (fmt[i] != f) continue;
-        const Geom& g = geo[i];
-        int fsY, nY, fsC, nC;
-        item_footprint(f, fmt_bpp(f), g.x0, g.cw, g.rw, g.ox, 1. / ((double)g.rw / g.cw), DW, fsY, nY, fsC, nC);
-        need = std::max(need, 16 * std::max(nY, nC));
-    }
-    if (need > kSlot) return false;
-    const int np = f == kI420 ? 3 : (f == kNV12 ? 2 : 1);
+// ROI-kernel plan for one format group with per-item geometry: the tile height, the LDS carve and the
+// staging buffer size, sized for the widest crop of the group (max_row_bytes = row_bytes_bound of it).
+// Returns false when the group needs the generic kernel (outputs wider than kRoiK x 256 pixels, or a
+// crop so wide that one output row's segments overflow the LDS budget).
+bool plan_roi(int DW, int DH, int out_dtype, int max_row_bytes, QParams& q, int& lds) {
+    if (DW > kRoiK * kThreads) return false;
+    const int def_buf = env_int("EVAM_PP_ROI_BUF", 12 * 1024);
     q.DW = DW; q.DH = DH;
-    q.TH = std::min(DH, std::max(R, (16384 / DW) / R * R));
+    q.TH = (int64_t)DW * DH <= 32768 ? DH : std::max(8, std::min(DH, 16384 / DW));
     q.tiles_per_item = (DH + q.TH - 1) / q.TH;
     q.offXT = out_dtype == EVAM_DTYPE_F32 ? kLutBytes : 0;
     q.offYT = q.offXT + (int)sizeof(XTab) * DW;
     q.offBuf = q.offYT + (int)sizeof(YTab) * q.TH;
-    q.slot = need;
-    q.buf_bytes = 2 * R * np * need;
-    q.K = (R * DW + kThreads - 1) / kThreads;
-    q.nfull = (R * DW) / kThreads;
+    q.buf_bytes = (std::max(def_buf, max_row_bytes) + 15) & ~15;
     lds = q.offBuf + 2 * q.buf_bytes;
-    return lds <= 64 * 1024 && q.K <= kRoiK;
+    return lds <= 160 * 1024;
 }
-
 
 // Descriptor upload ring. The per-call descriptor block ([LUT][ItemDesc x n][tables]) changes with
 // every new ROI set; it is written into a pinned host slot and copied on a private copy stream into a
@@ -1532,6 +1584,8 @@ struct evam_pp {
     evam_preproc lut_key{};        // cfg the cached LUT was built from (norm fields + dtype)
     bool lut_valid = false;
     float lut[768];
+    std::vector<int> sc_fmt;       // per-call scratch, kept to avoid reallocation
+    std::vector<Geom> sc_geo;
 };
 
 namespace {
@@ -1726,61 +1780,114 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
         }
     }
 
-    // ---- plan: geometry per item, grouped by source format ----
-    std::vector<Geom> geo(n_items);
-    std::vector<int> fmt(n_items);
-    double max_ratio[4] = {0, 0, 0, 0};
+    // ---- pass 1 (integer only): item -> source, format, clipped crop; validation ----
+    std::vector<int>& fmt = h->sc_fmt;
+    std::vector<Geom>& geo = h->sc_geo;
+    fmt.resize(n_items);
+    geo.resize(n_items);
     int count[4] = {0, 0, 0, 0};
-    int64_t src_bytes = 0;
+    int rep[4] = {-1, -1, -1, -1};
+    int max_cw[4] = {0, 0, 0, 0};
+    bool uniform[4] = {true, true, true, true};
     for (int i = 0; i < n_items; i++) {
         const evam_roi* r = items ? &items[i] : nullptr;
         const int si = items ? r->src_index : i;
         if (si < 0 || si >= n_srcs)
             return fail(EVAM_PP_ERR_INVALID_ARG, "evam_pp_run: items[%d].src_index %d out of range", i, si);
-        const int slot = dst->slot_offset + i * dst->slot_stride;
+        const int64_t slot = (int64_t)dst->slot_offset + (int64_t)i * dst->slot_stride;
         if (slot < 0 || slot >= dst->n)
-            return fail(EVAM_PP_ERR_INVALID_ARG, "evam_pp_run: item %d -> slot %d outside tensor batch %d", i, slot, dst->n);
+            return fail(EVAM_PP_ERR_INVALID_ARG, "evam_pp_run: item %d -> slot %lld outside tensor batch %d", i,
+                        (long long)slot, dst->n);
         const evam_image& s = srcs[si];
-        fmt[i] = fmt_id(s.fourcc);
-        int rc = item_geometry(fmt[i], s.width, s.height, r, *cfg, DW, DH, geo[i]);
-        if (rc) return fail(rc, "evam_pp_run: items[%d] ROI (%d,%d,%d,%d) is empty after clipping to %dx%d", i,
-                            r ? r->x : 0, r ? r->y : 0, r ? r->w : 0, r ? r->h : 0, s.width, s.height);
-        max_ratio[fmt[i]] = std::max(max_ratio[fmt[i]], (double)geo[i].cw / geo[i].rw);
-        count[fmt[i]]++;
-        if (out_xform) {
-            evam_transform& t = out_xform[i];
-            t.scale_x = (float)((double)geo[i].rw / geo[i].cw);
-            t.scale_y = (float)((double)geo[i].rh / geo[i].ch);
-            t.crop_x = geo[i].x0; t.crop_y = geo[i].y0; t.crop_w = geo[i].cw; t.crop_h = geo[i].ch;
-            t.pad_x = geo[i].ox; t.pad_y = geo[i].oy;
-            t.resized_w = geo[i].rw; t.resized_h = geo[i].rh;
-        }
-        if (h->opt_stats) src_bytes += item_src_bytes(fmt[i], geo[i], DW, DH);
+        const int f = fmt_id(s.fourcc);
+        fmt[i] = f;
+        Geom& g = geo[i];
+        if (roi_clip(f, s.width, s.height, r != nullptr, r ? r->x : 0, r ? r->y : 0, r ? r->w : 0, r ? r->h : 0, g))
+            return fail(EVAM_PP_ERR_EMPTY_ROI, "evam_pp_run: items[%d] ROI (%d,%d,%d,%d) is empty after clipping to %dx%d",
+                        i, r ? r->x : 0, r ? r->y : 0, r ? r->w : 0, r ? r->h : 0, s.width, s.height);
+        count[f]++;
+        max_cw[f] = std::max(max_cw[f], g.cw);
+        if (rep[f] < 0) rep[f] = i;
+        else if (g.cw != geo[rep[f]].cw || g.ch != geo[rep[f]].ch) uniform[f] = false;  // geometry = f(cw, ch)
     }
 
-    // ---- uniform geometry per format group -> row kernel with host-built tables ----
-    bool uniform[4] = {true, true, true, true};
-    int rep[4] = {-1, -1, -1, -1};
+    // ---- per format group: kernel choice ----
+    //   uniform geometry        -> staged / row kernels, host-built tables, per-item ItemDesc
+    //   per-item geometry       -> ROI kernel: raw evam_roi + SrcDesc, geometry resolved on the device
+    //   ROI plan impossible     -> generic kernel, per-item ItemDesc
+    enum { kPathNone, kPathUniform, kPathRoi, kPathGeneric };
+    const bool rows_enabled = env_int("EVAM_PP_ROWS", 1) != 0;
+    const bool roi_enabled = env_int("EVAM_PP_ROI", 1) != 0;
+    int path[4];
+    QParams qp[4];
+    int qlds[4] = {0, 0, 0, 0};
+    bool any_desc = false, any_roi = false;
+    int nfmt = 0;
+    for (int f = 0; f < 4; f++) {
+        path[f] = kPathNone;
+        if (!count[f]) continue;
+        nfmt++;
+        if (uniform[f] && rows_enabled) path[f] = kPathUniform;
+        else if (roi_enabled && plan_roi(DW, DH, cfg->out_dtype, row_bytes_bound(f, max_cw[f]), qp[f], qlds[f])) path[f] = kPathRoi;
+        else path[f] = kPathGeneric;
+        any_desc |= path[f] != kPathRoi;
+        any_roi |= path[f] == kPathRoi;
+    }
+    // Full geometry on the host only where something consumes it.
+    const bool all_geo = out_xform != nullptr || h->opt_stats;
+    int64_t src_bytes = 0;
     for (int i = 0; i < n_items; i++) {
         const int f = fmt[i];
-        if (rep[f] < 0) { rep[f] = i; continue; }
-        const Geom& a = geo[rep[f]];
-        const Geom& b = geo[i];
-        if (a.cw != b.cw || a.ch != b.ch || a.rw != b.rw || a.rh != b.rh || a.ox != b.ox || a.oy != b.oy)
-            uniform[f] = false;
+        if (!all_geo && path[f] == kPathRoi) continue;
+        Geom& g = geo[i];
+        const evam_roi* r = items ? &items[i] : nullptr;
+        const evam_image& s = srcs[items ? r->src_index : i];
+        roi_geometry(f, s.width, s.height, r != nullptr, r ? r->x : 0, r ? r->y : 0, r ? r->w : 0, r ? r->h : 0,
+                     cfg->resize_mode, cfg->placement, DW, DH, g);
+        if (out_xform) {
+            evam_transform& t = out_xform[i];
+            t.scale_x = (float)((double)g.rw / g.cw);
+            t.scale_y = (float)((double)g.rh / g.ch);
+            t.crop_x = g.x0; t.crop_y = g.y0; t.crop_w = g.cw; t.crop_h = g.ch;
+            t.pad_x = g.ox; t.pad_y = g.oy;
+            t.resized_w = g.rw; t.resized_h = g.rh;
+        }
+        if (h->opt_stats) src_bytes += item_src_bytes(f, g, DW, DH);
     }
-    const bool rows_enabled = env_int("EVAM_PP_ROWS", 1) != 0;
 
-    // ---- descriptor block: [LUT][items][per-group xtab (DW) + ytab (DH)] ----
-    const size_t items_bytes = sizeof(ItemDesc) * (size_t)n_items;
+    // ---- descriptor block ----
+    // [LUT][ItemDesc x (items of uniform/generic groups)][per uniform group: XTab x DW, YTab x DH]
+    // [SrcDesc x n_srcs][evam_roi x n_items][per ROI group of a mixed-format batch: int32 item index x count]
+    size_t nbytes = kLutBytes;
+    size_t desc_off = nbytes;
+    int n_desc = 0;
+    if (any_desc)
+        for (int f = 0; f < 4; f++)
+            if (path[f] == kPathUniform || path[f] == kPathGeneric) n_desc += count[f];
+    nbytes += sizeof(ItemDesc) * (size_t)n_desc;
     size_t tab_off[4] = {0, 0, 0, 0};
-    size_t nbytes = kLutBytes + items_bytes;
     for (int f = 0; f < 4; f++) {
-        if (!count[f] || !uniform[f] || !rows_enabled) continue;
+        if (path[f] != kPathUniform) continue;
         tab_off[f] = nbytes;
         nbytes += sizeof(XTab) * (size_t)DW + sizeof(YTab) * (size_t)DH;
     }
+    size_t src_off = 0, roi_off = 0, idx_off[4] = {0, 0, 0, 0};
+    if (any_roi) {
+        nbytes = (nbytes + 15) & ~(size_t)15;
+        src_off = nbytes;
+        nbytes += sizeof(SrcDesc) * (size_t)n_srcs;
+        roi_off = nbytes;
+        nbytes += sizeof(evam_roi) * (size_t)n_items;
+        if (nfmt > 1)
+            for (int f = 0; f < 4; f++) {
+                if (path[f] != kPathRoi) continue;
+                nbytes = (nbytes + 15) & ~(size_t)15;
+                idx_off[f] = nbytes;
+                nbytes += sizeof(int32_t) * (size_t)count[f];
+            }
+    }
     h->h_block.resize(nbytes);
+    uint8_t* blk = h->h_block.data();
     if (cfg->out_dtype == EVAM_DTYPE_F32) {
         // The LUT depends only on the normalisation fields: rebuilt when they change.
         evam_preproc key{};
@@ -1794,32 +1901,53 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
             h->lut_key = key;
             h->lut_valid = true;
         }
-        memcpy(h->h_block.data(), h->lut, kLutBytes);
+        memcpy(blk, h->lut, kLutBytes);
     } else {
-        memset(h->h_block.data(), 0, kLutBytes);
+        memset(blk, 0, kLutBytes);
     }
-    ItemDesc* desc = reinterpret_cast<ItemDesc*>(h->h_block.data() + kLutBytes);
-    int order = 0;
     int first[4] = {0, 0, 0, 0};
-    for (int f = 0; f < 4; f++) {
-        first[f] = order;
-        for (int i = 0; i < n_items; i++) {
-            if (fmt[i] != f) continue;
-            const evam_image& s = srcs[items ? items[i].src_index : i];
-            ItemDesc& d = desc[order++];
-            for (int p = 0; p < 3; p++) { d.plane[p] = s.planes[p]; d.pitch[p] = s.pitch[p]; }
-            const Geom& g = geo[i];
-            d.x0 = g.x0; d.y0 = g.y0; d.cw = g.cw; d.ch = g.ch;
-            d.rw = g.rw; d.rh = g.rh; d.ox = g.ox; d.oy = g.oy;
-            d.slot = dst->slot_offset + i * dst->slot_stride;
-            d.pad_ = 0;
-            d.scale_x = 1. / ((double)g.rw / g.cw);
-            d.scale_y = 1. / ((double)g.rh / g.ch);
+    if (any_desc) {
+        ItemDesc* desc = reinterpret_cast<ItemDesc*>(blk + desc_off);
+        int order = 0;
+        for (int f = 0; f < 4; f++) {
+            if (path[f] != kPathUniform && path[f] != kPathGeneric) continue;
+            first[f] = order;
+            for (int i = 0; i < n_items; i++) {
+                if (fmt[i] != f) continue;
+                const evam_image& s = srcs[items ? items[i].src_index : i];
+                ItemDesc& d = desc[order++];
+                for (int p = 0; p < 3; p++) { d.plane[p] = s.planes[p]; d.pitch[p] = s.pitch[p]; }
+                const Geom& g = geo[i];
+                d.x0 = g.x0; d.y0 = g.y0; d.cw = g.cw; d.ch = g.ch;
+                d.rw = g.rw; d.rh = g.rh; d.ox = g.ox; d.oy = g.oy;
+                d.slot = dst->slot_offset + i * dst->slot_stride;
+                d.pad_ = 0;
+                d.scale_x = 1. / ((double)g.rw / g.cw);
+                d.scale_y = 1. / ((double)g.rh / g.ch);
+            }
+            if (path[f] == kPathUniform) {
+                XTab* xt = reinterpret_cast<XTab*>(blk + tab_off[f]);
+                YTab* yt = reinterpret_cast<YTab*>(xt + DW);
+                build_tables(geo[rep[f]], DW, DH, h->tab_cache, xt, yt);
+            }
         }
-        if (tab_off[f]) {
-            XTab* xt = reinterpret_cast<XTab*>(h->h_block.data() + tab_off[f]);
-            YTab* yt = reinterpret_cast<YTab*>(xt + DW);
-            build_tables(geo[rep[f]], DW, DH, h->tab_cache, xt, yt);
+    }
+    if (any_roi) {
+        SrcDesc* sd = reinterpret_cast<SrcDesc*>(blk + src_off);
+        for (int i = 0; i < n_srcs; i++) {
+            for (int p = 0; p < 3; p++) { sd[i].plane[p] = srcs[i].planes[p]; sd[i].pitch[p] = srcs[i].pitch[p]; }
+            sd[i].width = srcs[i].width; sd[i].height = srcs[i].height; sd[i].pad_ = 0;
+        }
+        evam_roi* rd = reinterpret_cast<evam_roi*>(blk + roi_off);
+        if (items) memcpy(rd, items, sizeof(evam_roi) * (size_t)n_items);
+        else
+            for (int i = 0; i < n_items; i++) rd[i] = evam_roi{i, 0, 0, 0, 0};  // w <= 0: the full frame
+        for (int f = 0; f < 4; f++) {
+            if (!idx_off[f]) continue;
+            int32_t* ix = reinterpret_cast<int32_t*>(blk + idx_off[f]);
+            int o = 0;
+            for (int i = 0; i < n_items; i++)
+                if (fmt[i] == f) ix[o++] = i;
         }
     }
 
@@ -1830,41 +1958,66 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
     // ---- launches ----
     if (h->opt_timing) HIP_TRY(hipEventRecord(h->ev0, h->stream));
     int launches = 0;
+    const uint32_t fill = (uint32_t)cfg->fill[0] | ((uint32_t)cfg->fill[1] << 8) | ((uint32_t)cfg->fill[2] << 16);
+    const int color_rgb = cfg->color_order == EVAM_COLOR_RGB;
     for (int f = 0; f < 4; f++) {
-        if (!count[f]) continue;
-        const int nsegx = tab_off[f] && env_int("EVAM_PP_STAGED", 1) ? staged_nsegx(f, max_ratio[f]) : 0;
-        if (nsegx) {
-            SParams sp{};
-            sp.items = reinterpret_cast<const ItemDesc*>(d_block + kLutBytes) + first[f];
-            sp.lut = reinterpret_cast<const float*>(d_block);
-            sp.xtab = reinterpret_cast<const XTab*>(d_block + tab_off[f]);
-            sp.ytab = reinterpret_cast<const YTab*>(sp.xtab + DW);
-            sp.dst = dst->data;
-            sp.DW = DW; sp.DH = DH;
-            const int tw = 64 * nsegx;
-            sp.TH = std::max(1, std::min(DH, env_int("EVAM_PP_TH", std::max(kStageRows, 4096 / tw))));
-            sp.TH = (sp.TH + kStageRows - 1) / kStageRows * kStageRows;
-            sp.tiles_x = (DW + tw - 1) / tw;
-            sp.tiles_per_item = sp.tiles_x * ((DH + sp.TH - 1) / sp.TH);
-            const int np = f == kI420 ? 3 : (f == kNV12 ? 2 : 1);
-            sp.offBuf = cfg->out_dtype == EVAM_DTYPE_F32 ? kLutBytes : 0;
-            sp.buf_bytes = 2 * kStageRows * np * kSlot;
-            sp.color_rgb = cfg->color_order == EVAM_COLOR_RGB;
-            sp.fill = (uint32_t)cfg->fill[0] | ((uint32_t)cfg->fill[1] << 8) | ((uint32_t)cfg->fill[2] << 16);
-            sp.ablate = env_int("EVAM_PP_ABLATE", 0);
-            const int64_t grid = (int64_t)count[f] * sp.tiles_per_item;
+        if (path[f] == kPathNone) continue;
+        const ItemDesc* items_d = reinterpret_cast<const ItemDesc*>(d_block + desc_off) + first[f];
+        const float* lut_d = reinterpret_cast<const float*>(d_block);
+        if (path[f] == kPathRoi) {
+            QParams q = qp[f];
+            q.srcs = reinterpret_cast<const SrcDesc*>(d_block + src_off);
+            q.rois = reinterpret_cast<const evam_roi*>(d_block + roi_off);
+            q.index = idx_off[f] ? reinterpret_cast<const int32_t*>(d_block + idx_off[f]) : nullptr;
+            q.lut = lut_d;
+            q.dst = dst->data;
+            q.mode = cfg->resize_mode;
+            q.placement = cfg->placement;
+            q.slot_offset = dst->slot_offset;
+            q.slot_stride = dst->slot_stride;
+            q.color_rgb = color_rgb;
+            q.fill = fill;
+            const int64_t grid = (int64_t)count[f] * q.tiles_per_item;
             if (grid > 0x7FFFFFFF) return fail(EVAM_PP_ERR_INVALID_ARG, "evam_pp_run: too many tiles");
-            const int lds = sp.offBuf + 2 * sp.buf_bytes;
-            hipError_t e = launch_staged(f, cfg->out_dtype, nsegx, sp, (int)grid, lds, h->stream);
+            hipError_t e = launch_roi(f, cfg->out_dtype, q, (int)grid, qlds[f], h->stream);
             if (e != hipSuccess) return fail(EVAM_PP_ERR_HIP, "kernel launch failed: %s", hipGetErrorString(e));
             launches++;
             continue;
         }
-        if (tab_off[f]) {
+        if (path[f] == kPathUniform) {
+            const Geom& g0 = geo[rep[f]];
+            const int nsegx = env_int("EVAM_PP_STAGED", 1) ? staged_nsegx(f, (double)g0.cw / g0.rw) : 0;
+            if (nsegx) {
+                SParams sp{};
+                sp.items = items_d;
+                sp.lut = lut_d;
+                sp.xtab = reinterpret_cast<const XTab*>(d_block + tab_off[f]);
+                sp.ytab = reinterpret_cast<const YTab*>(sp.xtab + DW);
+                sp.dst = dst->data;
+                sp.DW = DW; sp.DH = DH;
+                const int tw = 64 * nsegx;
+                sp.TH = std::max(1, std::min(DH, env_int("EVAM_PP_TH", std::max(kStageRows, 4096 / tw))));
+                sp.TH = (sp.TH + kStageRows - 1) / kStageRows * kStageRows;
+                sp.tiles_x = (DW + tw - 1) / tw;
+                sp.tiles_per_item = sp.tiles_x * ((DH + sp.TH - 1) / sp.TH);
+                const int np = f == kI420 ? 3 : (f == kNV12 ? 2 : 1);
+                sp.offBuf = cfg->out_dtype == EVAM_DTYPE_F32 ? kLutBytes : 0;
+                sp.buf_bytes = 2 * kStageRows * np * kSlot;
+                sp.color_rgb = color_rgb;
+                sp.fill = fill;
+                sp.ablate = env_int("EVAM_PP_ABLATE", 0);
+                const int64_t grid = (int64_t)count[f] * sp.tiles_per_item;
+                if (grid > 0x7FFFFFFF) return fail(EVAM_PP_ERR_INVALID_ARG, "evam_pp_run: too many tiles");
+                const int lds = sp.offBuf + 2 * sp.buf_bytes;
+                hipError_t e = launch_staged(f, cfg->out_dtype, nsegx, sp, (int)grid, lds, h->stream);
+                if (e != hipSuccess) return fail(EVAM_PP_ERR_HIP, "kernel launch failed: %s", hipGetErrorString(e));
+                launches++;
+                continue;
+            }
             const RowCfg rc = choose_row_tiles(DW, DH);
             RParams r{};
-            r.items = reinterpret_cast<const ItemDesc*>(d_block + kLutBytes) + first[f];
-            r.lut = reinterpret_cast<const float*>(d_block);
+            r.items = items_d;
+            r.lut = lut_d;
             r.xtab = reinterpret_cast<const XTab*>(d_block + tab_off[f]);
             r.ytab = reinterpret_cast<const YTab*>(r.xtab + DW);
             r.dst = dst->data;
@@ -1873,8 +2026,8 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
             r.tiles_x = (DW + rc.TW - 1) / rc.TW;
             r.tiles_per_item = r.tiles_x * ((DH + rc.TH - 1) / rc.TH);
             r.nsegx = rc.TW / 64;
-            r.color_rgb = cfg->color_order == EVAM_COLOR_RGB;
-            r.fill = (uint32_t)cfg->fill[0] | ((uint32_t)cfg->fill[1] << 8) | ((uint32_t)cfg->fill[2] << 16);
+            r.color_rgb = color_rgb;
+            r.fill = fill;
             r.ablate = env_int("EVAM_PP_ABLATE", 0);
             const int64_t grid = (int64_t)count[f] * r.tiles_per_item;
             if (grid > 0x7FFFFFFF) return fail(EVAM_PP_ERR_INVALID_ARG, "evam_pp_run: too many tiles");
@@ -1884,27 +2037,10 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
             launches++;
             continue;
         }
-        {
-            QParams q{};
-            int R = 0, lds = 0;
-            if (env_int("EVAM_PP_ROI", 1) && plan_roi(f, geo, fmt, DW, DH, cfg->out_dtype, q, R, lds)) {
-                q.items = reinterpret_cast<const ItemDesc*>(d_block + kLutBytes) + first[f];
-                q.lut = reinterpret_cast<const float*>(d_block);
-                q.dst = dst->data;
-                q.color_rgb = cfg->color_order == EVAM_COLOR_RGB;
-                q.fill = (uint32_t)cfg->fill[0] | ((uint32_t)cfg->fill[1] << 8) | ((uint32_t)cfg->fill[2] << 16);
-                const int64_t grid = (int64_t)count[f] * q.tiles_per_item;
-                if (grid > 0x7FFFFFFF) return fail(EVAM_PP_ERR_INVALID_ARG, "evam_pp_run: too many tiles");
-                hipError_t e = launch_roi(f, cfg->out_dtype, R, q, (int)grid, lds, h->stream);
-                if (e != hipSuccess) return fail(EVAM_PP_ERR_HIP, "kernel launch failed: %s", hipGetErrorString(e));
-                launches++;
-                continue;
-            }
-        }
         const TileCfg t = choose_tiles(DW, DH, cfg->out_dtype);
         KParams p{};
-        p.items = reinterpret_cast<const ItemDesc*>(d_block + kLutBytes) + first[f];
-        p.lut = reinterpret_cast<const float*>(d_block);
+        p.items = items_d;
+        p.lut = lut_d;
         p.dst = dst->data;
         p.DW = DW; p.DH = DH;
         p.TW = t.TW; p.TH = t.TH;
@@ -1916,10 +2052,9 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
         p.n_tiles = (int)n_tiles;
         p.tw_magic = t.TW > 1 ? (uint32_t)(0xFFFFFFFFu / (uint32_t)t.TW) + 1u : 0u;
         p.offCol = t.offCol; p.offRow = t.offRow;
-        p.color_rgb = cfg->color_order == EVAM_COLOR_RGB;
-        p.fill = (uint32_t)cfg->fill[0] | ((uint32_t)cfg->fill[1] << 8) | ((uint32_t)cfg->fill[2] << 16);
+        p.color_rgb = color_rgb;
+        p.fill = fill;
         p.ablate = env_int("EVAM_PP_ABLATE", 0);
-        const int64_t grid = n_tiles;
         const int lds = t.lds;
         if (lds > 64 * 1024) {
             hipError_t e = hipSuccess;
@@ -1931,7 +2066,7 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
             }
             if (e != hipSuccess) return fail(EVAM_PP_ERR_HIP, "hipFuncSetAttribute: %s", hipGetErrorString(e));
         }
-        hipError_t e = launch(f, cfg->out_dtype, p, (int)grid, lds, h->stream);
+        hipError_t e = launch(f, cfg->out_dtype, p, (int)n_tiles, lds, h->stream);
         if (e != hipSuccess) return fail(EVAM_PP_ERR_HIP, "kernel launch failed: %s", hipGetErrorString(e));
         launches++;
     }
