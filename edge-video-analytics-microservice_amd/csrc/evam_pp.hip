@@ -1094,23 +1094,31 @@ __global__ __launch_bounds__(kThreads) void evam_pp_roi(const QParams P) {
     nY = __builtin_amdgcn_readfirstlane(nY);
     fsC = __builtin_amdgcn_readfirstlane(fsC);
     nC = __builtin_amdgcn_readfirstlane(nC);
-    // Packed row layout in a staging buffer: [Y tap0 | Y tap1 | C tap0 | C tap1 (| V tap0 | V tap1)].
+    // Staging buffer layout for a group of R output rows, one plane region after the other:
+    //   Y: segment (2 r + tap) at (2 r + tap) * segY;   C (U / UV): at offC + (2 r + tap) * segC;
+    //   V (I420): at offC + 2 R segC + (2 r + tap) * segC.
+    // Each plane region is contiguous, so its 16-byte chunks are staged by wave-wide LDS-DMA with one
+    // per-lane source offset each: 64 chunks (of any rows and taps) per instruction.
     const int segY = nY * 16, segC = nC * 16;
     const int rowb = 2 * segY + 2 * (NP - 1) * segC;
     int R = rowb > 0 ? P.buf_bytes / rowb : rows;
     R = min(R, (kRoiK * kThreads) / DW);
     R = max(1, min(R, rows));
+    const int offC = 2 * R * segY;
     const int npx = R * DW;                       // pixels per full group
     const int K = (npx + kThreads - 1) / kThreads;
     // store steps this wave issues in a full group: k with some lane of the wave holding a pixel
     int nk_w = 0;
     for (int k = 0; k < K; k++) nk_w += (k * kThreads + wave * 64 < npx) ? 1 : 0;
+    // q / n for q < 2^16 by one mul_hi: m = ceil(2^32 / n) is exact there (n = 1: the identity).
+    const uint32_t mY = nY > 1 ? (uint32_t)((0x100000000ull + nY - 1) / nY) : 0u;
+    const uint32_t mC = nC > 1 ? (uint32_t)((0x100000000ull + nC - 1) / nC) : 0u;
     __syncthreads();
 
     const int f0 = P.fill & 0xFF, f1 = (P.fill >> 8) & 0xFF, f2 = (P.fill >> 16) & 0xFF;
-    // Per-lane pixel state for k < K, identical for every group: row of the pixel inside the group
-    // (as its LDS row offset), packed LDS tap offsets (tap 0 low, tap 1 high half), horizontal weights.
-    uint32_t lb[kRoiK], lY[kRoiK], lC[kRoiK], wa[kRoiK];
+    // Per-lane pixel state for k < K, identical for every group: row of the pixel inside the group,
+    // packed LDS tap offsets (tap 0 low, tap 1 high half), horizontal weights.
+    uint32_t lY[kRoiK], lC[kRoiK], wa[kRoiK];
     int rr[kRoiK];
 #pragma unroll
     for (int k = 0; k < kRoiK; k++) {
@@ -1119,7 +1127,6 @@ __global__ __launch_bounds__(kThreads) void evam_pp_roi(const QParams P) {
         const int r = v ? p / DW : 0;
         const int c = v ? p - r * DW : 0;
         rr[k] = v ? r : -1;
-        lb[k] = (uint32_t)(r * rowb);
         const XTab e = xt[c];
         wa[k] = (uint32_t)e.a0 | ((uint32_t)e.a1 << 16);
         lY[k] = lC[k] = 0;
@@ -1134,33 +1141,36 @@ __global__ __launch_bounds__(kThreads) void evam_pp_roi(const QParams P) {
     }
     const int ngroups = (rows + R - 1) / R;
 
-    auto issue = [&](int grp, uint8_t* buf) {
-        if (nY == 0) return;  // no visible columns: every pixel is fill
-        const int nseg = NKIND * min(R, rows - grp * R);
-        for (int s = wave; s < nseg; s += 4) {
-            const int r = s / NKIND, kind = s - r * NKIND, pl = kind >> 1, tap = kind & 1;
-            const int ly = grp * R + r;
-            const int b0 = __builtin_amdgcn_readfirstlane(yt[ly].b0);
-            const int b1 = __builtin_amdgcn_readfirstlane(yt[ly].b1);
-            if ((b0 | b1) == 0) continue;  // padding row: nothing to stage
-            const int ya = y0 + __builtin_amdgcn_readfirstlane(yt[ly].r0);
-            const int yb = y0 + __builtin_amdgcn_readfirstlane(yt[ly].r1);
-            const int yr = tap ? yb : ya;
-            if (pl > 0 && tap && (ya >> 1) == (yb >> 1)) continue;  // chroma row shared by both taps
-            const int nck = pl == 0 ? nY : nC;
-            uint8_t* dst = buf + r * rowb + (pl == 0 ? tap * segY : 2 * segY + (pl - 1) * 2 * segC + tap * segC);
-            for (int c = 0; c < nck; c += 64) {
-                if (lane + c < nck) {
-                    __attribute__((address_space(3))) void* dstl = (__attribute__((address_space(3))) void*)(dst + c * 16);
-                    if (pl == 0)
-                        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsY, dstl, 16, (lane + c) * 16, yr * pitch0 + fsY, 0, 0);
-                    else if (pl == 1)
-                        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsC, dstl, 16, (lane + c) * 16, (yr >> 1) * pitch1 + fsC, 0, 0);
-                    else
-                        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsV, dstl, 16, (lane + c) * 16, (yr >> 1) * pitch2 + fsC, 0, 0);
-                }
+    // One plane region of group grp: chunk q -> (segment, chunk) -> (row, tap) -> source offset.
+    auto issue_plane = [&](int grp, uint8_t* base, int nr, int n, uint32_t m, int pl) {
+        const int nq = 2 * nr * n;
+        for (int q0 = wave * 64; q0 < nq; q0 += 4 * 64) {
+            const int q = q0 + lane;
+            const int seg = n > 1 ? (int)__umulhi((uint32_t)q, m) : q;
+            const int c = q - seg * n;
+            const int r = seg >> 1, tap = seg & 1;
+            const YTab e = yt[min(grp * R + r, rows - 1)];
+            const int ya = y0 + e.r0, yb = y0 + e.r1;
+            bool on = q < nq && (e.b0 | e.b1) != 0;           // padding rows stage nothing
+            if (pl > 0) on = on && !(tap && (ya >> 1) == (yb >> 1));  // chroma row shared by both taps
+            __attribute__((address_space(3))) void* dstl = (__attribute__((address_space(3))) void*)(base + q0 * 16);
+            if (on) {
+                const int yr = tap ? yb : ya;
+                if (pl == 0)
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsY, dstl, 16, yr * pitch0 + fsY + c * 16, 0, 0, 0);
+                else if (pl == 1)
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsC, dstl, 16, (yr >> 1) * pitch1 + fsC + c * 16, 0, 0, 0);
+                else
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsV, dstl, 16, (yr >> 1) * pitch2 + fsC + c * 16, 0, 0, 0);
             }
         }
+    };
+    auto issue = [&](int grp, uint8_t* buf) {
+        if (nY == 0) return;  // no visible columns: every pixel is fill
+        const int nr = min(R, rows - grp * R);
+        issue_plane(grp, buf, nr, nY, mY, 0);
+        if constexpr (NP >= 2) issue_plane(grp, buf + offC, nr, nC, mC, 1);
+        if constexpr (NP >= 3) issue_plane(grp, buf + offC + 2 * R * segC, nr, nC, mC, 2);
     };
 
     auto compute = [&](int grp, const uint8_t* buf) {
@@ -1177,13 +1187,13 @@ __global__ __launch_bounds__(kThreads) void evam_pp_roi(const QParams P) {
             } else {
                 const uint32_t a0 = wa[k] & 0xFFFF, a1 = wa[k] >> 16;
                 const uint32_t tY0 = lY[k] & 0xFFFF, tY1 = lY[k] >> 16;
-                const uint8_t* sy0 = buf + lb[k];
+                const uint8_t* sy0 = buf + 2 * rr[k] * segY;
                 const uint8_t* sy1 = sy0 + segY;
                 int c[4][3];
                 if constexpr (kYUV) {
                     const uint32_t tC0 = lC[k] & 0xFFFF, tC1 = lC[k] >> 16;
                     const int ya = y0 + e.r0, yb = y0 + e.r1;
-                    const uint8_t* sc0 = sy0 + 2 * segY;
+                    const uint8_t* sc0 = buf + offC + 2 * rr[k] * segC;
                     const uint8_t* sc1 = (ya >> 1) == (yb >> 1) ? sc0 : sc0 + segC;
                     Chroma<FMT> cA, cB, cC, cD;
                     if constexpr (FMT == kNV12) {
@@ -1192,8 +1202,8 @@ __global__ __launch_bounds__(kThreads) void evam_pp_roi(const QParams P) {
                         cC.u = *reinterpret_cast<const uint16_t*>(sc1 + tC0);
                         cD.u = *reinterpret_cast<const uint16_t*>(sc1 + tC1);
                     } else {
-                        const uint8_t* sv0 = sc0 + 2 * segC;
-                        const uint8_t* sv1 = sc1 + 2 * segC;
+                        const uint8_t* sv0 = sc0 + 2 * R * segC;
+                        const uint8_t* sv1 = sc1 + 2 * R * segC;
                         cA.u = sc0[tC0]; cA.v = sv0[tC0];
                         cB.u = sc0[tC1]; cB.v = sv0[tC1];
                         cC.u = sc1[tC0]; cC.v = sv1[tC0];
@@ -1546,7 +1556,7 @@ bool plan_roi(int DW, int DH, int out_dtype, int max_row_bytes, QParams& q, int&
     q.offBuf = q.offYT + (int)sizeof(YTab) * q.TH;
     q.buf_bytes = (std::max(def_buf, max_row_bytes) + 15) & ~15;
     lds = q.offBuf + 2 * q.buf_bytes;
-    return lds <= 160 * 1024;
+    return q.buf_bytes <= 32 * 1024 && lds <= 160 * 1024;
 }
 
 // Descriptor upload ring. The per-call descriptor block ([LUT][ItemDesc x n][tables]) changes with
@@ -1568,6 +1578,20 @@ struct DescRing {
     std::vector<uint8_t> last;  // bytes currently held by dev[cur]
 };
 
+// Per-call ROI descriptors ([SrcDesc x n_srcs][evam_roi x n][item indices]) change with every
+// detection result. They are written into a slot of pinned, coherent (fine-grained) host memory that
+// the ROI kernel reads directly over PCIe: each workgroup fetches only its own ~70 bytes, so a call
+// costs one memcpy and no copy command. `used[k]` fences the reuse of slot k.
+struct PinRing {
+    static constexpr int N = 4;
+    uint8_t* host[N] = {};
+    const uint8_t* dev[N] = {};  // device address of host[k]
+    size_t cap[N] = {};
+    hipEvent_t used[N] = {};
+    bool used_rec[N] = {};
+    int cur = -1;
+};
+
 }  // namespace
 
 struct evam_pp {
@@ -1578,6 +1602,7 @@ struct evam_pp {
     evam_pp_stats stats{};
     std::vector<uint8_t> h_block;  // this call's descriptor block, built on the host
     DescRing ring;
+    PinRing pin;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool timed = false;
     TabCache tab_cache;
@@ -1603,6 +1628,43 @@ void ring_release(DescRing& r) {
     if (r.copy) (void)hipStreamDestroy(r.copy);
     r.copy = nullptr;
     r.cur = -1;
+}
+
+void pin_release(PinRing& r) {
+    for (int k = 0; k < PinRing::N; k++) {
+        if (r.host[k]) (void)hipHostFree(r.host[k]);
+        if (r.used[k]) (void)hipEventDestroy(r.used[k]);
+        r.host[k] = nullptr;
+        r.dev[k] = nullptr;
+        r.used[k] = nullptr;
+        r.cap[k] = 0;
+    }
+    r.cur = -1;
+}
+
+// Next pinned slot with at least n bytes (waits only if a kernel of PinRing::N calls ago still reads it).
+int pin_acquire(evam_pp* h, size_t n, uint8_t** host, const uint8_t** dev) {
+    PinRing& r = h->pin;
+    const int k = (r.cur + 1) % PinRing::N;
+    if (!r.used[k]) HIP_TRY(hipEventCreateWithFlags(&r.used[k], hipEventDisableTiming));
+    if (r.used_rec[k]) HIP_TRY(hipEventSynchronize(r.used[k]));
+    if (r.cap[k] < n) {
+        if (r.host[k]) HIP_TRY(hipHostFree(r.host[k]));
+        r.host[k] = nullptr;
+        r.dev[k] = nullptr;
+        r.cap[k] = 0;
+        const size_t cap = std::max<size_t>(n * 2, 64 * 1024);
+        if (hipHostMalloc((void**)&r.host[k], cap, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+            return fail(EVAM_PP_ERR_OOM, "evam_pp_run: hipHostMalloc(%zu) failed", cap);
+        void* d = nullptr;
+        HIP_TRY(hipHostGetDevicePointer(&d, r.host[k], 0));
+        r.dev[k] = reinterpret_cast<const uint8_t*>(d);
+        r.cap[k] = cap;
+    }
+    r.cur = k;
+    *host = r.host[k];
+    *dev = r.dev[k];
+    return EVAM_PP_OK;
 }
 
 // Make h->h_block visible to kernels on h->stream; returns the device copy. Re-uploads only when the
@@ -1682,11 +1744,12 @@ int evam_pp_create(int hip_device, void* hip_stream, evam_pp** out) {
 void evam_pp_destroy(evam_pp* h) {
     if (!h) return;
     (void)hipSetDevice(h->device);
-    if (h->ring.copy) {
+    if (h->ring.copy || h->pin.cur >= 0) {
         (void)hipStreamSynchronize(h->stream);
-        (void)hipStreamSynchronize(h->ring.copy);
+        if (h->ring.copy) (void)hipStreamSynchronize(h->ring.copy);
     }
     ring_release(h->ring);
+    pin_release(h->pin);
     if (h->ev0) (void)hipEventDestroy(h->ev0);
     if (h->ev1) (void)hipEventDestroy(h->ev1);
     delete h;
@@ -1871,19 +1934,20 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
         tab_off[f] = nbytes;
         nbytes += sizeof(XTab) * (size_t)DW + sizeof(YTab) * (size_t)DH;
     }
-    size_t src_off = 0, roi_off = 0, idx_off[4] = {0, 0, 0, 0};
+    // ROI groups: [SrcDesc x n_srcs][evam_roi x n_items][per ROI group of a mixed-format batch: indices],
+    // in a pinned zero-copy slot (PinRing).
+    size_t src_off = 0, roi_off = 0, idx_off[4] = {0, 0, 0, 0}, dyn_bytes = 0;
     if (any_roi) {
-        nbytes = (nbytes + 15) & ~(size_t)15;
-        src_off = nbytes;
-        nbytes += sizeof(SrcDesc) * (size_t)n_srcs;
-        roi_off = nbytes;
-        nbytes += sizeof(evam_roi) * (size_t)n_items;
+        src_off = 0;
+        dyn_bytes = sizeof(SrcDesc) * (size_t)n_srcs;
+        roi_off = dyn_bytes;
+        dyn_bytes += sizeof(evam_roi) * (size_t)n_items;
         if (nfmt > 1)
             for (int f = 0; f < 4; f++) {
                 if (path[f] != kPathRoi) continue;
-                nbytes = (nbytes + 15) & ~(size_t)15;
-                idx_off[f] = nbytes;
-                nbytes += sizeof(int32_t) * (size_t)count[f];
+                dyn_bytes = (dyn_bytes + 15) & ~(size_t)15;
+                idx_off[f] = dyn_bytes;
+                dyn_bytes += sizeof(int32_t) * (size_t)count[f];
             }
     }
     h->h_block.resize(nbytes);
@@ -1932,26 +1996,28 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
             }
         }
     }
+    HIP_TRY(hipSetDevice(h->device));
+    uint8_t* dyn = nullptr;
+    const uint8_t* d_dyn = nullptr;
     if (any_roi) {
-        SrcDesc* sd = reinterpret_cast<SrcDesc*>(blk + src_off);
+        if (int rc = pin_acquire(h, dyn_bytes, &dyn, &d_dyn)) return rc;
+        SrcDesc* sd = reinterpret_cast<SrcDesc*>(dyn + src_off);
         for (int i = 0; i < n_srcs; i++) {
             for (int p = 0; p < 3; p++) { sd[i].plane[p] = srcs[i].planes[p]; sd[i].pitch[p] = srcs[i].pitch[p]; }
             sd[i].width = srcs[i].width; sd[i].height = srcs[i].height; sd[i].pad_ = 0;
         }
-        evam_roi* rd = reinterpret_cast<evam_roi*>(blk + roi_off);
+        evam_roi* rd = reinterpret_cast<evam_roi*>(dyn + roi_off);
         if (items) memcpy(rd, items, sizeof(evam_roi) * (size_t)n_items);
         else
             for (int i = 0; i < n_items; i++) rd[i] = evam_roi{i, 0, 0, 0, 0};  // w <= 0: the full frame
         for (int f = 0; f < 4; f++) {
             if (!idx_off[f]) continue;
-            int32_t* ix = reinterpret_cast<int32_t*>(blk + idx_off[f]);
+            int32_t* ix = reinterpret_cast<int32_t*>(dyn + idx_off[f]);
             int o = 0;
             for (int i = 0; i < n_items; i++)
                 if (fmt[i] == f) ix[o++] = i;
         }
     }
-
-    HIP_TRY(hipSetDevice(h->device));
     const uint8_t* d_block = nullptr;
     if (int rc = ring_upload(h, &d_block)) return rc;
 
@@ -1966,9 +2032,9 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
         const float* lut_d = reinterpret_cast<const float*>(d_block);
         if (path[f] == kPathRoi) {
             QParams q = qp[f];
-            q.srcs = reinterpret_cast<const SrcDesc*>(d_block + src_off);
-            q.rois = reinterpret_cast<const evam_roi*>(d_block + roi_off);
-            q.index = idx_off[f] ? reinterpret_cast<const int32_t*>(d_block + idx_off[f]) : nullptr;
+            q.srcs = reinterpret_cast<const SrcDesc*>(d_dyn + src_off);
+            q.rois = reinterpret_cast<const evam_roi*>(d_dyn + roi_off);
+            q.index = idx_off[f] ? reinterpret_cast<const int32_t*>(d_dyn + idx_off[f]) : nullptr;
             q.lut = lut_d;
             q.dst = dst->data;
             q.mode = cfg->resize_mode;
@@ -2072,6 +2138,10 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
     }
     HIP_TRY(hipEventRecord(h->ring.used[h->ring.cur], h->stream));
     h->ring.used_rec[h->ring.cur] = true;
+    if (any_roi) {
+        HIP_TRY(hipEventRecord(h->pin.used[h->pin.cur], h->stream));
+        h->pin.used_rec[h->pin.cur] = true;
+    }
     if (h->opt_timing) HIP_TRY(hipEventRecord(h->ev1, h->stream));
     h->timed = h->opt_timing != 0;
 
