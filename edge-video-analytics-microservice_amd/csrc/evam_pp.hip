@@ -978,6 +978,7 @@ struct QParams {
     int buf_bytes;            // one staging buffer
     int color_rgb;
     uint32_t fill;
+    int ablate;               // diagnostics only (EVAM_PP_ABLATE bits): 2 no pixel math, 4 no stores, 16 no DMA
 };
 
 template <int N>
@@ -1166,7 +1167,7 @@ __global__ __launch_bounds__(kThreads) void evam_pp_roi(const QParams P) {
         }
     };
     auto issue = [&](int grp, uint8_t* buf) {
-        if (nY == 0) return;  // no visible columns: every pixel is fill
+        if (nY == 0 || (P.ablate & 16)) return;  // no visible columns: every pixel is fill
         const int nr = min(R, rows - grp * R);
         issue_plane(grp, buf, nr, nY, mY, 0);
         if constexpr (NP >= 2) issue_plane(grp, buf + offC, nr, nC, mC, 1);
@@ -1182,7 +1183,7 @@ __global__ __launch_bounds__(kThreads) void evam_pp_roi(const QParams P) {
             if (rr[k] < 0 || ly >= rows) continue;
             const YTab e = yt[ly];
             int v[3];
-            if ((e.b0 | e.b1) == 0 || wa[k] == 0) {  // letterbox padding row / column
+            if ((e.b0 | e.b1) == 0 || wa[k] == 0 || (P.ablate & 2)) {  // letterbox padding row / column
                 v[0] = f0; v[1] = f1; v[2] = f2;
             } else {
                 const uint32_t a0 = wa[k] & 0xFFFF, a1 = wa[k] >> 16;
@@ -1235,6 +1236,10 @@ __global__ __launch_bounds__(kThreads) void evam_pp_roi(const QParams P) {
                 if (P.color_rgb) { const int tmp = v[0]; v[0] = v[2]; v[2] = tmp; }
             }
             const uint32_t vo = (gbase + (uint32_t)(tid + k * kThreads)) * (uint32_t)esz;
+            if (P.ablate & 4) {
+                asm volatile("" :: "v"(v[0]), "v"(v[1]), "v"(v[2]));
+                continue;
+            }
             if constexpr (OUT == 1) {
                 __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lut_s[v[0]]), rsD0, vo, 0, 0);
                 __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lut_s[256 + v[1]]), rsD1, vo, 0, 0);
@@ -2043,6 +2048,7 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
             q.slot_stride = dst->slot_stride;
             q.color_rgb = color_rgb;
             q.fill = fill;
+            q.ablate = env_int("EVAM_PP_ABLATE", 0);
             const int64_t grid = (int64_t)count[f] * q.tiles_per_item;
             if (grid > 0x7FFFFFFF) return fail(EVAM_PP_ERR_INVALID_ARG, "evam_pp_run: too many tiles");
             hipError_t e = launch_roi(f, cfg->out_dtype, q, (int)grid, qlds[f], h->stream);
@@ -2062,9 +2068,15 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
                 sp.dst = dst->data;
                 sp.DW = DW; sp.DH = DH;
                 const int tw = 64 * nsegx;
-                sp.TH = std::max(1, std::min(DH, env_int("EVAM_PP_TH", std::max(kStageRows, 4096 / tw))));
-                sp.TH = (sp.TH + kStageRows - 1) / kStageRows * kStageRows;
                 sp.tiles_x = (DW + tw - 1) / tw;
+                // ~4096 pixels per workgroup, but short enough tiles that small batches still put
+                // 8 workgroups on every CU (a whole clip-ring step is only 32 x 224 x 224 pixels).
+                int th = std::max(kStageRows, 4096 / tw);
+                const int64_t cols = (int64_t)count[f] * sp.tiles_x;
+                const int64_t want = 8 * (int64_t)h->n_cu;
+                if (cols * ((DH + th - 1) / th) < want) th = (int)std::max<int64_t>(kStageRows, cols * DH / want);
+                sp.TH = std::max(1, std::min(DH, env_int("EVAM_PP_TH", th)));
+                sp.TH = (sp.TH + kStageRows - 1) / kStageRows * kStageRows;
                 sp.tiles_per_item = sp.tiles_x * ((DH + sp.TH - 1) / sp.TH);
                 const int np = f == kI420 ? 3 : (f == kNV12 ? 2 : 1);
                 sp.offBuf = cfg->out_dtype == EVAM_DTYPE_F32 ? kLutBytes : 0;
