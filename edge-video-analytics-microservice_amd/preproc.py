@@ -295,10 +295,13 @@ class HipPreProcessor:
     def _tensor_desc(self, out, slot_offset: int, slot_stride: int):
         """Validated evam_tensor for ``out`` (cached for the last tensor: the steady state of a stage
         that packs into the same inference blob every call)."""
-        key = (out.data_ptr(), out.shape, out.dtype, out.device, out.is_contiguous(), slot_offset, slot_stride)
+        key = (out.data_ptr(), out.shape, out.dtype, out.device, out.is_contiguous())
         c = self._tdesc
         if c is not None and c[0] == key:
-            return c[1], c[2]
+            t = c[1]
+            if t.slot_offset != slot_offset or t.slot_stride != slot_stride:
+                t.slot_offset, t.slot_stride = int(slot_offset), int(slot_stride)
+            return t, c[2]
         torch = self._torch
         if out.dim() != 4 or out.shape[1] != 3 or not out.is_contiguous():
             raise PreProcError(N.ERR_INVALID_ARG, f"out must be a contiguous [N,3,H,W] tensor, got {tuple(out.shape)}")
