@@ -746,7 +746,7 @@ __global__ __launch_bounds__(kThreads) void evam_pp_staged(const SParams P) {
 
     // ---- LDS-DMA of group g into buffer `buf` (slot s = plane * 2R + 2 * row + tap) ----
     auto issue = [&](int g, uint8_t* buf) {
-        if (!cols) return;
+        if (!cols || (P.ablate & 16)) return;
 #pragma unroll
         for (int s0 = 0; s0 < NS; s0 += 4) {
             const int s = s0 + wave;
@@ -839,6 +839,10 @@ __global__ __launch_bounds__(kThreads) void evam_pp_staged(const SParams P) {
                 if (P.color_rgb) { const int tmp = v[0]; v[0] = v[2]; v[2] = tmp; }
             }
             if (!xin) continue;
+            if (P.ablate & 4) {
+                asm volatile("" :: "v"(v[0]), "v"(v[1]), "v"(v[2]));
+                continue;
+            }
             if constexpr (OUT == 1) {
                 __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lut_s[v[0]]), rsD0, xo, sO, 0);
                 __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lut_s[256 + v[1]]), rsD1, xo, sO, 0);
@@ -864,6 +868,346 @@ __global__ __launch_bounds__(kThreads) void evam_pp_staged(const SParams P) {
         __builtin_amdgcn_s_barrier();  // every wave's DMA for g landed; every wave done reading g-1
         if (g + 1 < ngroups) issue(g + 1, (g & 1) ? buf0 : buf1);
         compute(g, (g & 1) ? buf1 : buf0);
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// wave-row kernel (uniform geometry)
+// ------------------------------------------------------------------------------------------------
+struct WParams {
+    const ItemDesc* items;
+    const float* lut;    // [3][256]
+    const XTab* xtab;    // [DW]
+    const YTab* ytab;    // [DH]
+    void* dst;
+    int DW, DH;
+    int TH, tiles_x, tiles_per_item;
+    int offBuf;          // LDS offset of the per-wave staging areas (after the LUT)
+    int segY, segC;      // bytes of one staged luma / chroma row segment (multiples of 16)
+    int wave_bytes;      // one wave's staging area (two buffers)
+    int color_rgb;
+    uint32_t fill;
+    int ablate;          // diagnostics only (EVAM_PP_ABLATE bits): 2 no pixel math, 4 no stores, 16 no DMA
+};
+
+typedef int evam_v2i __attribute__((ext_vector_type(2)));
+typedef int evam_v4i __attribute__((ext_vector_type(4)));
+
+// PX adjacent output pixels of one channel from one lane: a single buffer store of PX x 4 bytes (fp32)
+// or PX bytes (u8). lut == nullptr: u8 output.
+template <int OUT, int PX>
+__device__ __forceinline__ void store_vec(const __amdgpu_buffer_rsrc_t rs, uint32_t vo, int so, const float* lut,
+                                          const int (&v)[PX]) {
+    if constexpr (OUT == 1) {
+        if constexpr (PX == 4) {
+            evam_v4i q = {(int)__float_as_uint(lut[v[0]]), (int)__float_as_uint(lut[v[1]]),
+                          (int)__float_as_uint(lut[v[2]]), (int)__float_as_uint(lut[v[3]])};
+            __builtin_amdgcn_raw_buffer_store_b128(q, rs, vo, so, 0);
+        } else if constexpr (PX == 2) {
+            evam_v2i q = {(int)__float_as_uint(lut[v[0]]), (int)__float_as_uint(lut[v[1]])};
+            __builtin_amdgcn_raw_buffer_store_b64(q, rs, vo, so, 0);
+        } else {
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lut[v[0]]), rs, vo, so, 0);
+        }
+    } else {
+        if constexpr (PX == 4)
+            __builtin_amdgcn_raw_buffer_store_b32((uint32_t)v[0] | ((uint32_t)v[1] << 8) | ((uint32_t)v[2] << 16) |
+                                                      ((uint32_t)v[3] << 24), rs, vo, so, 0);
+        else if constexpr (PX == 2)
+            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(v[0] | (v[1] << 8)), rs, vo, so, 0);
+        else
+            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v[0], rs, vo, so, 0);
+    }
+}
+
+// Uniform-geometry kernel built around independent waves. A workgroup owns a 64·PX-column x TH-row
+// tile of one item; each of its four waves owns a contiguous quarter of the tile's rows and walks it
+// one output row at a time, every lane producing PX adjacent pixels:
+//  * The wave stages the source row segments its next row needs (luma taps, chroma taps; each the
+//    tile's 16 B-aligned footprint) into its own double-buffered LDS area by LDS-DMA while it converts
+//    the current row. Nothing is shared between waves, so there is no workgroup barrier in the loop:
+//    the wait for a row's DMA is this wave's vmcnt, with the previous row's three stores still in flight.
+//  * Horizontal results are kept per source row (H = 11-bit weighted sum of the two converted taps, per
+//    channel). With REUSE (vertical upscales, where consecutive output rows share source rows) a source
+//    row that the previous output row already filtered is neither staged nor converted again.
+//  * When both vertical taps read the same 4:2:0 chroma row, its BT.601 chroma terms are computed once.
+//  * Each channel of a row leaves as one PX-wide store per lane (dwordx4 for fp32 at PX = 4).
+template <int FMT, int OUT, int PX, bool REUSE>
+__global__ __launch_bounds__(kThreads) void evam_pp_wave(const WParams P) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    using T = FmtTraits<FMT>;
+    constexpr bool kYUV = FMT == kNV12 || FMT == kI420;
+    constexpr int TW = 64 * PX;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int t = blockIdx.x;
+    const int item = t / P.tiles_per_item;
+    const int tile = t - item * P.tiles_per_item;
+    const int ty = tile / P.tiles_x;
+    const int tx = tile - ty * P.tiles_x;
+    const __attribute__((address_space(4))) ItemDesc* it =
+        (const __attribute__((address_space(4))) ItemDesc*)(P.items) + item;
+    const __attribute__((address_space(4))) YTab* ytab = (const __attribute__((address_space(4))) YTab*)(P.ytab);
+    const __attribute__((address_space(4))) XTab* xtab_s = (const __attribute__((address_space(4))) XTab*)(P.xtab);
+    const uint8_t* p0 = it->plane[0];
+    const uint8_t* p1 = it->plane[1];
+    const uint8_t* p2 = it->plane[2];
+    const int pitch0 = it->pitch[0], pitch1 = it->pitch[1], pitch2 = it->pitch[2];
+    const int x0 = it->x0, y0 = it->y0, ox = it->ox, rw = it->rw;
+    const size_t plane = (size_t)P.DW * P.DH;
+    const size_t esz = OUT == 1 ? 4 : 1;
+    uint8_t* const d0 = reinterpret_cast<uint8_t*>(P.dst) + (size_t)it->slot * 3 * plane * esz;
+    uint8_t* const d1 = d0 + plane * esz;
+    uint8_t* const d2 = d1 + plane * esz;
+    const __amdgpu_buffer_rsrc_t rsY = __builtin_amdgcn_make_buffer_rsrc((void*)p0, (short)0, 0x7FFFFFFF, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsC = __builtin_amdgcn_make_buffer_rsrc((void*)(p1 ? p1 : p0), (short)0, 0x7FFFFFFF, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsV = __builtin_amdgcn_make_buffer_rsrc((void*)(p2 ? p2 : p0), (short)0, 0x7FFFFFFF, 0x00020000);
+    // output planes in store order (BGR, or RGB: planes 0 and 2 exchanged)
+    const __amdgpu_buffer_rsrc_t rsO0 = __builtin_amdgcn_make_buffer_rsrc((void*)(P.color_rgb ? d2 : d0), (short)0, 0x7FFFFFFF, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsO1 = __builtin_amdgcn_make_buffer_rsrc((void*)d1, (short)0, 0x7FFFFFFF, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsO2 = __builtin_amdgcn_make_buffer_rsrc((void*)(P.color_rgb ? d0 : d2), (short)0, 0x7FFFFFFF, 0x00020000);
+
+    float* lut_s = reinterpret_cast<float*>(smem);
+    if constexpr (OUT == 1) {
+        for (int i = tid; i < 768; i += kThreads) lut_s[i] = P.lut[i];
+        __syncthreads();
+    }
+    // fill values in output plane order (P.fill is already in output channel order)
+    const int fo0 = P.fill & 0xFF, fo1 = (P.fill >> 8) & 0xFF, fo2 = (P.fill >> 16) & 0xFF;
+    const int fb0 = P.color_rgb ? fo2 : fo0, fb2 = P.color_rgb ? fo0 : fo2;  // same, in BGR order
+
+    const int X0 = tx * TW, Y0 = ty * P.TH, Y1 = min(Y0 + P.TH, P.DH);
+    // visible (non-padding) columns of the tile -> source footprint (wave-uniform)
+    const int Xv0 = max(X0, ox), Xv1 = min(min(X0 + TW, P.DW), ox + rw) - 1;
+    const bool cols = Xv0 <= Xv1;
+    int fsY = 0, nY = 0, fsC = 0, nC = 0;
+    if (cols) {
+        const int xa = x0 + xtab_s[Xv0].s0, xb = x0 + xtab_s[Xv1].s1;
+        fsY = (xa * T::bpp) & ~15;
+        nY = (((xb * T::bpp + T::bpp + 15) & ~15) - fsY) >> 4;
+        if constexpr (FMT == kNV12) {
+            fsC = (2 * (xa >> 1)) & ~15;
+            nC = (((2 * (xb >> 1) + 2 + 15) & ~15) - fsC) >> 4;
+        } else if constexpr (FMT == kI420) {
+            fsC = (xa >> 1) & ~15;
+            nC = ((((xb >> 1) + 1 + 15) & ~15) - fsC) >> 4;
+        }
+    }
+    // per-lane column state for the PX pixels of this lane
+    const int Xl = X0 + lane * PX;
+    const bool xin = Xl < P.DW;  // DW % PX == 0: a lane's pixels are all in or all out
+    uint32_t lY[PX], lC[PX], wa[PX];
+#pragma unroll
+    for (int j = 0; j < PX; j++) {
+        const XTab xt = P.xtab[xin ? Xl + j : 0];
+        wa[j] = (uint32_t)xt.a0 | ((uint32_t)xt.a1 << 16);
+        lY[j] = lC[j] = 0;
+        if (xin && wa[j] != 0) {
+            const int ca = x0 + xt.s0, cb = x0 + xt.s1;
+            lY[j] = (uint32_t)(ca * T::bpp - fsY) | ((uint32_t)(cb * T::bpp - fsY) << 16);
+            if constexpr (FMT == kNV12)
+                lC[j] = (uint32_t)(2 * (ca >> 1) - fsC) | ((uint32_t)(2 * (cb >> 1) - fsC) << 16);
+            else if constexpr (FMT == kI420)
+                lC[j] = (uint32_t)((ca >> 1) - fsC) | ((uint32_t)((cb >> 1) - fsC) << 16);
+        }
+    }
+    const uint32_t vo = (uint32_t)(xin ? Xl : 0) * (uint32_t)esz;
+
+    // this wave's rows
+    const int thw = (P.TH + 3) >> 2;
+    const int Yw0 = Y0 + wave * thw, Yw1 = min(Yw0 + thw, Y1);
+    if (Yw0 >= Yw1) return;
+    uint8_t* const wbuf = smem + P.offBuf + wave * P.wave_bytes;
+    const int half = P.wave_bytes >> 1;
+    const int segY = P.segY, segC = P.segC;
+    // buffer layout: [Y tap0][Y tap1][C tap0][C tap1][V tap0][V tap1]
+    const int oY1 = segY, oC0 = 2 * segY, oC1 = 2 * segY + segC, oV0 = 2 * segY + 2 * segC, oV1 = oV0 + segC;
+
+    // Staging decision for output row Y, given the source rows (pa, pb) whose H the wave holds.
+    struct Plan {
+        int ya, yb, b0, b1;
+        bool pad, stA, stB, stCB;  // stage luma tap0 / tap1 rows; chroma of tap1 in its own slot
+    };
+    auto plan = [&](int Y, int pa, int pb) {
+        Plan q;
+        q.b0 = ytab[Y].b0;
+        q.b1 = ytab[Y].b1;
+        q.ya = y0 + ytab[Y].r0;
+        q.yb = y0 + ytab[Y].r1;
+        q.pad = (q.b0 | q.b1) == 0 || !cols;
+        if (REUSE) {
+            q.stA = q.ya != pa && q.ya != pb;
+            q.stB = q.yb != q.ya && q.yb != pa && q.yb != pb;
+        } else {
+            q.stA = true;
+            q.stB = q.yb != q.ya;
+        }
+        q.stCB = q.stB && !(q.stA && (q.ya >> 1) == (q.yb >> 1));
+        return q;
+    };
+    auto dma = [&](const __amdgpu_buffer_rsrc_t rs, uint8_t* dst, int nck, int soff) {
+        for (int c = 0; c < nck; c += 64) {
+            if (lane + c < nck)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(dst + c * 16), 16,
+                                                         (lane + c) * 16, soff, 0, 0);
+        }
+    };
+    auto issue = [&](const Plan& q, uint8_t* buf) {
+        if (q.pad || (P.ablate & 16)) return;
+        if (q.stA) {
+            dma(rsY, buf, nY, q.ya * pitch0 + fsY);
+            if constexpr (kYUV) dma(rsC, buf + oC0, nC, (q.ya >> 1) * pitch1 + fsC);
+            if constexpr (FMT == kI420) dma(rsV, buf + oV0, nC, (q.ya >> 1) * pitch2 + fsC);
+        }
+        if (q.stB) {
+            dma(rsY, buf + oY1, nY, q.yb * pitch0 + fsY);
+            if (q.stCB) {
+                if constexpr (kYUV) dma(rsC, buf + oC1, nC, (q.yb >> 1) * pitch1 + fsC);
+                if constexpr (FMT == kI420) dma(rsV, buf + oV1, nC, (q.yb >> 1) * pitch2 + fsC);
+            }
+        }
+    };
+
+    // Horizontal pass of one staged source row (or two sharing their chroma row).
+    auto hrow = [&](const uint8_t* sy, const uint8_t* sc, const uint8_t* sv, uint32_t (&H)[PX][3]) {
+#pragma unroll
+        for (int j = 0; j < PX; j++) {
+            const uint32_t tY0 = lY[j] & 0xFFFF, tY1 = lY[j] >> 16;
+            int c0[3], c1[3];
+            if constexpr (kYUV) {
+                const uint32_t tC0 = lC[j] & 0xFFFF, tC1 = lC[j] >> 16;
+                Chroma<FMT> cA, cB;
+                if constexpr (FMT == kNV12) {
+                    cA.u = *reinterpret_cast<const uint16_t*>(sc + tC0);
+                    cB.u = *reinterpret_cast<const uint16_t*>(sc + tC1);
+                } else {
+                    cA.u = sc[tC0]; cA.v = sv[tC0];
+                    cB.u = sc[tC1]; cB.v = sv[tC1];
+                }
+                y_plus_uv((int)sy[tY0], chroma_terms<FMT>(cA), c0[0], c0[1], c0[2]);
+                y_plus_uv((int)sy[tY1], chroma_terms<FMT>(cB), c1[0], c1[1], c1[2]);
+            } else if constexpr (FMT == kBGRX) {
+                const uint32_t q0 = *reinterpret_cast<const uint32_t*>(sy + tY0);
+                const uint32_t q1 = *reinterpret_cast<const uint32_t*>(sy + tY1);
+                c0[0] = q0 & 0xFF; c0[1] = (q0 >> 8) & 0xFF; c0[2] = (q0 >> 16) & 0xFF;
+                c1[0] = q1 & 0xFF; c1[1] = (q1 >> 8) & 0xFF; c1[2] = (q1 >> 16) & 0xFF;
+            } else {
+                c0[0] = sy[tY0]; c0[1] = sy[tY0 + 1]; c0[2] = sy[tY0 + 2];
+                c1[0] = sy[tY1]; c1[1] = sy[tY1 + 1]; c1[2] = sy[tY1 + 2];
+            }
+            const uint32_t a0 = wa[j] & 0xFFFF, a1 = wa[j] >> 16;
+#pragma unroll
+            for (int ch = 0; ch < 3; ch++) H[j][ch] = __umul24(c0[ch], a0) + __umul24(c1[ch], a1);
+        }
+    };
+    auto hrow2 = [&](const uint8_t* sya, const uint8_t* syb, const uint8_t* sc, const uint8_t* sv,
+                     uint32_t (&HA)[PX][3], uint32_t (&HB)[PX][3]) {
+#pragma unroll
+        for (int j = 0; j < PX; j++) {
+            const uint32_t tY0 = lY[j] & 0xFFFF, tY1 = lY[j] >> 16;
+            const uint32_t tC0 = lC[j] & 0xFFFF, tC1 = lC[j] >> 16;
+            Chroma<FMT> cA, cB;
+            if constexpr (FMT == kNV12) {
+                cA.u = *reinterpret_cast<const uint16_t*>(sc + tC0);
+                cB.u = *reinterpret_cast<const uint16_t*>(sc + tC1);
+            } else {
+                cA.u = sc[tC0]; cA.v = sv[tC0];
+                cB.u = sc[tC1]; cB.v = sv[tC1];
+            }
+            const UV3 tA = chroma_terms<FMT>(cA), tB = chroma_terms<FMT>(cB);
+            const uint32_t a0 = wa[j] & 0xFFFF, a1 = wa[j] >> 16;
+            int c0[3], c1[3];
+            y_plus_uv((int)sya[tY0], tA, c0[0], c0[1], c0[2]);
+            y_plus_uv((int)sya[tY1], tB, c1[0], c1[1], c1[2]);
+#pragma unroll
+            for (int ch = 0; ch < 3; ch++) HA[j][ch] = __umul24(c0[ch], a0) + __umul24(c1[ch], a1);
+            y_plus_uv((int)syb[tY0], tA, c0[0], c0[1], c0[2]);
+            y_plus_uv((int)syb[tY1], tB, c1[0], c1[1], c1[2]);
+#pragma unroll
+            for (int ch = 0; ch < 3; ch++) HB[j][ch] = __umul24(c0[ch], a0) + __umul24(c1[ch], a1);
+        }
+    };
+
+    auto store_row = [&](int Y, const int (&v)[3][PX]) {
+        if (!xin || (P.ablate & 4)) {
+            if (P.ablate & 4) asm volatile("" :: "v"(v[0][0]), "v"(v[1][0]), "v"(v[2][0]));
+            return;
+        }
+        const int so = (int)((uint32_t)(Y * P.DW) * (uint32_t)esz);
+        // the LUT is per output plane: B lands in plane 2 when the output is RGB
+        store_vec<OUT, PX>(rsO0, vo, so, lut_s + (P.color_rgb ? 512 : 0), v[0]);
+        store_vec<OUT, PX>(rsO1, vo, so, lut_s + 256, v[1]);
+        store_vec<OUT, PX>(rsO2, vo, so, lut_s + (P.color_rgb ? 0 : 512), v[2]);
+    };
+
+    uint32_t HA[PX][3], HB[PX][3];  // H of source rows pa, pb (REUSE) / of this row's taps
+#pragma unroll
+    for (int j = 0; j < PX; j++)
+#pragma unroll
+        for (int ch = 0; ch < 3; ch++) HA[j][ch] = HB[j][ch] = 0;
+    int pa = -1, pb = -1;
+    Plan cur = plan(Yw0, pa, pb);
+    issue(cur, wbuf);
+    int i = 0;
+    for (int Y = Yw0; Y < Yw1; Y++, i++) {
+        // this row's DMA landed; the previous row's three stores may stay in flight
+        if (i == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+        const uint8_t* buf = wbuf + (i & 1) * half;
+        const int na = cur.pad ? pa : cur.ya, nb = cur.pad ? pb : cur.yb;
+        Plan nxt{};
+        if (Y + 1 < Yw1) {
+            nxt = plan(Y + 1, na, nb);
+            issue(nxt, wbuf + ((i + 1) & 1) * half);  // that buffer was last read by row Y - 1
+        }
+        int v[3][PX];
+        if (cur.pad || (P.ablate & 2)) {
+#pragma unroll
+            for (int j = 0; j < PX; j++) { v[0][j] = fb0; v[1][j] = fo1; v[2][j] = fb2; }
+        } else {
+            uint32_t NA[PX][3], NB[PX][3];
+            const bool shareC = kYUV && cur.stA && cur.stB && !cur.stCB;
+            if (shareC) {
+                if constexpr (kYUV) hrow2(buf, buf + oY1, buf + oC0, buf + oV0, NA, NB);
+            } else {
+                if (cur.stA) hrow(buf, buf + oC0, buf + oV0, NA);
+                else {
+#pragma unroll
+                    for (int j = 0; j < PX; j++)
+#pragma unroll
+                        for (int ch = 0; ch < 3; ch++) NA[j][ch] = cur.ya == pa ? HA[j][ch] : HB[j][ch];
+                }
+                if (cur.stB) hrow(buf + oY1, buf + (cur.stCB ? oC1 : oC0), buf + (cur.stCB ? oV1 : oV0), NB);
+                else {
+#pragma unroll
+                    for (int j = 0; j < PX; j++)
+#pragma unroll
+                        for (int ch = 0; ch < 3; ch++)
+                            NB[j][ch] = cur.yb == cur.ya ? NA[j][ch] : (cur.yb == pa ? HA[j][ch] : HB[j][ch]);
+                }
+            }
+            const uint32_t wb0 = (uint32_t)cur.b0, wb1 = (uint32_t)cur.b1;
+#pragma unroll
+            for (int j = 0; j < PX; j++) {
+                const bool padc = wa[j] == 0;  // letterbox padding column
+#pragma unroll
+                for (int ch = 0; ch < 3; ch++) {
+                    const int r = vresize(NA[j][ch], NB[j][ch], wb0, wb1);
+                    v[ch][j] = padc ? (ch == 0 ? fb0 : (ch == 1 ? fo1 : fb2)) : r;
+                }
+            }
+            if (REUSE) {
+#pragma unroll
+                for (int j = 0; j < PX; j++)
+#pragma unroll
+                    for (int ch = 0; ch < 3; ch++) { HA[j][ch] = NA[j][ch]; HB[j][ch] = NB[j][ch]; }
+            }
+        }
+        store_row(Y, v);
+        pa = na;
+        pb = nb;
+        cur = nxt;
     }
 }
 
@@ -1546,6 +1890,98 @@ hipError_t launch_roi(int f, int out, const QParams& p, int grid, int lds, hipSt
     }
 }
 
+template <int FMT, int OUT, int PX>
+hipError_t launch_wave_r(bool reuse, const WParams& p, int grid, int lds, hipStream_t s) {
+    if (reuse) hipLaunchKernelGGL((evam_pp_wave<FMT, OUT, PX, true>), dim3(grid), dim3(kThreads), lds, s, p);
+    else hipLaunchKernelGGL((evam_pp_wave<FMT, OUT, PX, false>), dim3(grid), dim3(kThreads), lds, s, p);
+    return hipGetLastError();
+}
+
+template <int FMT, int OUT>
+hipError_t launch_wave_p(int px, bool reuse, const WParams& p, int grid, int lds, hipStream_t s) {
+    switch (px) {
+    case 4: return launch_wave_r<FMT, OUT, 4>(reuse, p, grid, lds, s);
+    case 2: return launch_wave_r<FMT, OUT, 2>(reuse, p, grid, lds, s);
+    default: return launch_wave_r<FMT, OUT, 1>(reuse, p, grid, lds, s);
+    }
+}
+
+hipError_t launch_wave(int f, int out, int px, bool reuse, const WParams& p, int grid, int lds, hipStream_t s) {
+    switch (f * 2 + out) {
+    case kNV12 * 2 + 0: return launch_wave_p<kNV12, 0>(px, reuse, p, grid, lds, s);
+    case kNV12 * 2 + 1: return launch_wave_p<kNV12, 1>(px, reuse, p, grid, lds, s);
+    case kI420 * 2 + 0: return launch_wave_p<kI420, 0>(px, reuse, p, grid, lds, s);
+    case kI420 * 2 + 1: return launch_wave_p<kI420, 1>(px, reuse, p, grid, lds, s);
+    case kBGRX * 2 + 0: return launch_wave_p<kBGRX, 0>(px, reuse, p, grid, lds, s);
+    case kBGRX * 2 + 1: return launch_wave_p<kBGRX, 1>(px, reuse, p, grid, lds, s);
+    case kBGR * 2 + 0: return launch_wave_p<kBGR, 0>(px, reuse, p, grid, lds, s);
+    default: return launch_wave_p<kBGR, 1>(px, reuse, p, grid, lds, s);
+    }
+}
+
+// Wave-row kernel plan for a uniform-geometry group: pixels per lane PX (the widest whose staging
+// fits the LDS budget and divides DW), the exact per-tile footprint from the host tables, REUSE when
+// consecutive output rows share source rows, and a tile height that gives every CU enough workgroups.
+bool plan_wave(int f, const Geom& g, int DW, int DH, int count, int out_dtype, int n_cu, const XTab* xt,
+               const YTab* yt, WParams& w, int& px, bool& reuse, int& lds, int& grid) {
+    const int bpp = fmt_bpp(f);
+    const int npc = f == kI420 ? 2 : (f == kNV12 ? 1 : 0);
+    const int lut = out_dtype == EVAM_DTYPE_F32 ? kLutBytes : 0;
+    const int budget = env_int("EVAM_PP_WAVE_LDS", 40 * 1024);
+    const int want_px = env_int("EVAM_PP_PX", 0);
+    px = 0;
+    for (int cand : {4, 2, 1}) {
+        if (want_px && cand != want_px) continue;
+        if (cand > 1 && DW % cand) continue;
+        const int tw = 64 * cand;
+        int mY = 0, mC = 0;
+        for (int X0 = 0; X0 < DW; X0 += tw) {
+            const int Xv0 = std::max(X0, g.ox), Xv1 = std::min(std::min(X0 + tw, DW), g.ox + g.rw) - 1;
+            if (Xv0 > Xv1) continue;
+            const int xa = g.x0 + xt[Xv0].s0, xb = g.x0 + xt[Xv1].s1;
+            const int fsY = (xa * bpp) & ~15;
+            mY = std::max(mY, (((xb * bpp + bpp + 15) & ~15) - fsY) >> 4);
+            if (f == kNV12) {
+                const int fsC = (2 * (xa >> 1)) & ~15;
+                mC = std::max(mC, (((2 * (xb >> 1) + 2 + 15) & ~15) - fsC) >> 4);
+            } else if (f == kI420) {
+                const int fsC = (xa >> 1) & ~15;
+                mC = std::max(mC, ((((xb >> 1) + 1 + 15) & ~15) - fsC) >> 4);
+            }
+        }
+        const int segY = std::max(16, 16 * mY), segC = npc ? std::max(16, 16 * mC) : 0;
+        const int wave_bytes = 2 * (2 * segY + 2 * npc * segC);
+        const int need = lut + 4 * wave_bytes;
+        if (need > budget && !(want_px && need <= 64 * 1024)) continue;
+        px = cand;
+        w.segY = segY;
+        w.segC = segC;
+        w.wave_bytes = wave_bytes;
+        w.offBuf = lut;
+        lds = need;
+        break;
+    }
+    if (!px) return false;
+    reuse = false;
+    for (int Y = 0; Y + 1 < DH; Y++) {
+        const bool pad0 = (yt[Y].b0 | yt[Y].b1) == 0, pad1 = (yt[Y + 1].b0 | yt[Y + 1].b1) == 0;
+        if (!pad0 && !pad1 && yt[Y + 1].r0 <= yt[Y].r1) { reuse = true; break; }
+    }
+    if (env_int("EVAM_PP_REUSE", 1) == 0) reuse = false;
+    w.DW = DW; w.DH = DH;
+    w.tiles_x = (DW + 64 * px - 1) / (64 * px);
+    const int per_cu = std::max(1, std::min(8, (160 * 1024) / std::max(lds, 1)));
+    const int64_t slots = (int64_t)n_cu * per_cu;
+    int64_t rpw = ((int64_t)count * w.tiles_x * DH) / (4 * slots);
+    rpw = std::max<int64_t>(2, std::min<int64_t>(32, rpw));
+    w.TH = std::max(1, std::min(DH, env_int("EVAM_PP_WTH", (int)(4 * rpw))));
+    w.tiles_per_item = w.tiles_x * ((DH + w.TH - 1) / w.TH);
+    const int64_t gr = (int64_t)count * w.tiles_per_item;
+    if (gr > 0x7FFFFFFF) return false;
+    grid = (int)gr;
+    return true;
+}
+
 // ROI-kernel plan for one format group with per-item geometry: the tile height, the LDS carve and the
 // staging buffer size, sized for the widest crop of the group (max_row_bytes = row_bytes_bound of it).
 // Returns false when the group needs the generic kernel (outputs wider than kRoiK x 256 pixels, or a
@@ -2058,6 +2494,27 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
         }
         if (path[f] == kPathUniform) {
             const Geom& g0 = geo[rep[f]];
+            if (env_int("EVAM_PP_WAVE", 1)) {
+                WParams w{};
+                int px = 0, lds = 0, grid = 0;
+                bool reuse = false;
+                const XTab* hx = reinterpret_cast<const XTab*>(h->h_block.data() + tab_off[f]);
+                if (plan_wave(f, g0, DW, DH, count[f], cfg->out_dtype, h->n_cu, hx,
+                              reinterpret_cast<const YTab*>(hx + DW), w, px, reuse, lds, grid)) {
+                    w.items = items_d;
+                    w.lut = lut_d;
+                    w.xtab = reinterpret_cast<const XTab*>(d_block + tab_off[f]);
+                    w.ytab = reinterpret_cast<const YTab*>(w.xtab + DW);
+                    w.dst = dst->data;
+                    w.color_rgb = color_rgb;
+                    w.fill = fill;
+                    w.ablate = env_int("EVAM_PP_ABLATE", 0);
+                    hipError_t e = launch_wave(f, cfg->out_dtype, px, reuse, w, grid, lds, h->stream);
+                    if (e != hipSuccess) return fail(EVAM_PP_ERR_HIP, "kernel launch failed: %s", hipGetErrorString(e));
+                    launches++;
+                    continue;
+                }
+            }
             const int nsegx = env_int("EVAM_PP_STAGED", 1) ? staged_nsegx(f, (double)g0.cw / g0.rw) : 0;
             if (nsegx) {
                 SParams sp{};
@@ -2148,8 +2605,10 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
         if (e != hipSuccess) return fail(EVAM_PP_ERR_HIP, "kernel launch failed: %s", hipGetErrorString(e));
         launches++;
     }
-    HIP_TRY(hipEventRecord(h->ring.used[h->ring.cur], h->stream));
-    h->ring.used_rec[h->ring.cur] = true;
+    if (!env_int("EVAM_PP_NO_EVENTS", 0)) {  // diagnostics only: unsafe once the ring wraps
+        HIP_TRY(hipEventRecord(h->ring.used[h->ring.cur], h->stream));
+        h->ring.used_rec[h->ring.cur] = true;
+    }
     if (any_roi) {
         HIP_TRY(hipEventRecord(h->pin.used[h->pin.cur], h->stream));
         h->pin.used_rec[h->pin.cur] = true;

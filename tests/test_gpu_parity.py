@@ -351,3 +351,37 @@ def test_stats_and_timing(evam, O, gpu):
     assert st.src_bytes == 2 * 3_002_880 and st.dst_bytes == 2 * 3_145_728
     assert st.n_launches == 1 and st.last_kernel_ms > 0
     pp.close()
+
+
+@pytest.mark.parametrize("fmt", FORMATS)
+@pytest.mark.parametrize("src,dst,resize", [
+    ((768, 432), (512, 512), "no-aspect-ratio"),    # C1 shape: vertical upscale -> REUSE
+    ((640, 360), (256, 128), "no-aspect-ratio"),    # downscale, DW % 4 == 0
+    ((320, 200), (226, 150), "aspect-ratio"),       # DW % 4 != 0 -> PX 2, letterbox rows
+    ((300, 180), (131, 97), "aspect-ratio"),        # odd DW -> PX 1, letterbox
+    ((480, 270), (224, 224), "aspect-crop"),        # C5 shape: central crop
+])
+@pytest.mark.parametrize("variant", ["auto", "px1", "px2", "noreuse", "staged"])
+def test_wave_kernel_variants(evam, O, coracle, gpu, fmt, src, dst, resize, variant, monkeypatch):
+    """Uniform-geometry batches through the wave-row kernel (every PX / REUSE choice) and the staged
+    kernel it replaced (EVAM_PP_WAVE=0), RGB order, fp32 with normalisation and u8."""
+    import torch
+
+    env = {"px1": {"EVAM_PP_PX": "1"}, "px2": {"EVAM_PP_PX": "2"}, "noreuse": {"EVAM_PP_REUSE": "0"},
+           "staged": {"EVAM_PP_WAVE": "0"}}.get(variant, {})
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    if variant == "px2" and dst[0] % 2:
+        pytest.skip("PX 2 needs an even output width")
+    rng = np.random.default_rng(zlib.crc32(repr((fmt, src, dst, resize)).encode()))
+    frames = [O.random_frame(rng, fc(O, fmt), src[0], src[1], pattern=p) for p in ("uniform", "gradient", "uniform")]
+    kw = {"resize": "aspect-ratio", "crop": "central"} if resize == "aspect-crop" else {"resize": resize}
+    for dtype in ("u8", "f32"):
+        info = evam.PreProcInfo(color_space="RGB", fill=(5, 50, 250), placement="center", **kw,
+                                **({"range": (0.0, 1.0), "mean": (0.1, 0.2, 0.3), "std": (0.3, 0.2, 0.1)}
+                                   if dtype == "f32" else {}))
+        shape = (3, 3, dst[1], dst[0])
+        got, _ = run_hip(evam, torch, upload(evam, frames, gpu), shape,
+                         torch.float32 if dtype == "f32" else torch.uint8, info)
+        ref, _ = run_oracle(O, coracle, frames, shape, dtype, info)
+        assert_same(got, ref, f"wave {fmt} {src}->{dst} {resize} {variant} {dtype}")
