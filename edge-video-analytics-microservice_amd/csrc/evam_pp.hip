@@ -867,7 +867,9 @@ __global__ __launch_bounds__(kThreads) void evam_pp_staged(const SParams P) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();  // every wave's DMA for g landed; every wave done reading g-1
         if (g + 1 < ngroups) issue(g + 1, (g & 1) ? buf0 : buf1);
+        asm volatile("" ::: "memory");  // the next group's DMA stays ahead of this group's stores
         compute(g, (g & 1) ? buf1 : buf0);
+        asm volatile("" ::: "memory");
     }
 }
 
@@ -1161,6 +1163,8 @@ __global__ __launch_bounds__(kThreads) void evam_pp_wave(const WParams P) {
             nxt = plan(Y + 1, na, nb);
             issue(nxt, wbuf + ((i + 1) & 1) * half);  // that buffer was last read by row Y - 1
         }
+        // Keep every DMA of row Y + 1 ahead of row Y's stores: the vmcnt(3) above relies on that order.
+        asm volatile("" ::: "memory");
         int v[3][PX];
         if (cur.pad || (P.ablate & 2)) {
 #pragma unroll
@@ -1205,6 +1209,7 @@ __global__ __launch_bounds__(kThreads) void evam_pp_wave(const WParams P) {
             }
         }
         store_row(Y, v);
+        asm volatile("" ::: "memory");
         pa = na;
         pb = nb;
         cur = nxt;
@@ -1608,7 +1613,9 @@ __global__ __launch_bounds__(kThreads) void evam_pp_roi(const QParams P) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();  // every wave's DMA for grp landed; every wave done reading grp-1
         if (grp + 1 < ngroups) issue(grp + 1, (grp & 1) ? buf0 : buf1);
+        asm volatile("" ::: "memory");  // the next group's DMA stays ahead of this group's stores
         compute(grp, (grp & 1) ? buf1 : buf0);
+        asm volatile("" ::: "memory");
     }
 }
 
