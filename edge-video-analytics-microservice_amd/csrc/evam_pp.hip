@@ -650,6 +650,22 @@ __global__ __launch_bounds__(kThreads) void evam_pp_rows(const RParams P) {
     }
 }
 
+// Row table of up to 64 consecutive output rows held one row per lane (r0, r1, b0, b1 in four VGPRs),
+// read back as wave-uniform values with v_readlane: the per-row lookups of the staging loops then cost
+// no scalar-memory round trip (a dependent s_load per row serialised the DMA issue).
+struct LaneRows {
+    int r0, r1, b0, b1;
+    __device__ __forceinline__ void load(const YTab* ytab, int Ybase, int n, int lane) {
+        const int Y = Ybase + (lane < n ? lane : 0);
+        const YTab e = ytab[Y];
+        r0 = e.r0; r1 = e.r1; b0 = e.b0; b1 = e.b1;
+    }
+    __device__ __forceinline__ int R0(int i) const { return __builtin_amdgcn_readlane(r0, i); }
+    __device__ __forceinline__ int R1(int i) const { return __builtin_amdgcn_readlane(r1, i); }
+    __device__ __forceinline__ int B0(int i) const { return __builtin_amdgcn_readlane(b0, i); }
+    __device__ __forceinline__ int B1(int i) const { return __builtin_amdgcn_readlane(b1, i); }
+};
+
 // Staged uniform-geometry kernel. A workgroup owns a TW x TH tile (TW = 64 x NSEGX) and walks it in
 // groups of R output rows. For each group the source row segments its taps need (two luma rows and
 // two chroma rows per output row, each at most kSlot bytes wide) are brought into LDS by LDS-DMA —
@@ -681,7 +697,6 @@ __global__ __launch_bounds__(kThreads) void evam_pp_staged(const SParams P) {
     const int tx = tile - ty * P.tiles_x;
     const __attribute__((address_space(4))) ItemDesc* it =
         (const __attribute__((address_space(4))) ItemDesc*)(P.items) + item;
-    const __attribute__((address_space(4))) YTab* ytab = (const __attribute__((address_space(4))) YTab*)(P.ytab);
     const __attribute__((address_space(4))) XTab* xtab_s = (const __attribute__((address_space(4))) XTab*)(P.xtab);
     const uint8_t* p0 = it->plane[0];
     const uint8_t* p1 = it->plane[1];
@@ -741,8 +756,10 @@ __global__ __launch_bounds__(kThreads) void evam_pp_staged(const SParams P) {
     }
     const uint32_t xo = (uint32_t)(xin ? X : 0) * (uint32_t)esz;
     const bool wave_stores = X0 + seg * 64 < P.DW;  // some lane of this wave stores (wave-uniform)
-    const int rows = Y1 - Y0;
+    const int rows = Y1 - Y0;  // <= 64 (host)
     const int ngroups = (rows + R - 1) / R;
+    LaneRows lr;
+    lr.load(P.ytab, Y0, rows, lane);
 
     // ---- LDS-DMA of group g into buffer `buf` (slot s = plane * 2R + 2 * row + tap) ----
     auto issue = [&](int g, uint8_t* buf) {
@@ -753,9 +770,9 @@ __global__ __launch_bounds__(kThreads) void evam_pp_staged(const SParams P) {
             const int pl = s / (2 * R), loc = s - pl * 2 * R, r = loc >> 1, tap = loc & 1;
             const int Y = Y0 + g * R + r;
             if (Y >= Y1) continue;
-            const int b0 = ytab[Y].b0, b1 = ytab[Y].b1;
+            const int b0 = lr.B0(Y - Y0), b1 = lr.B1(Y - Y0);
             if ((b0 | b1) == 0) continue;  // padding row: nothing to stage
-            const int ya = y0 + ytab[Y].r0, yb = y0 + ytab[Y].r1;
+            const int ya = y0 + lr.R0(Y - Y0), yb = y0 + lr.R1(Y - Y0);
             const int yr = tap ? yb : ya;
             if (pl > 0 && tap && (ya >> 1) == (yb >> 1)) continue;  // chroma row shared by both taps
             const int nck = pl == 0 ? nY : nC;
@@ -779,7 +796,7 @@ __global__ __launch_bounds__(kThreads) void evam_pp_staged(const SParams P) {
             const int r = rph + k * RSTEP;
             const int Y = Y0 + g * R + r;
             if (Y >= Y1) continue;
-            const int b0 = ytab[Y].b0, b1 = ytab[Y].b1;
+            const int b0 = lr.B0(Y - Y0), b1 = lr.B1(Y - Y0);
             const int sO = (int)((uint32_t)(Y * P.DW) * (uint32_t)esz);
             int v[3];
             if ((b0 | b1) == 0 || wa == 0 || (P.ablate & 2)) {  // padding row / column
@@ -792,7 +809,7 @@ __global__ __launch_bounds__(kThreads) void evam_pp_staged(const SParams P) {
                 const uint8_t* sc0 = buf + (2 * R + 2 * r) * kSlot;
                 int c[4][3];
                 if constexpr (kYUV) {
-                    const int ya = y0 + ytab[Y].r0, yb = y0 + ytab[Y].r1;
+                    const int ya = y0 + lr.R0(Y - Y0), yb = y0 + lr.R1(Y - Y0);
                     const bool share = (ya >> 1) == (yb >> 1);
                     const uint8_t* sc1 = share ? sc0 : sc0 + kSlot;
                     Chroma<FMT> cA, cB, cC, cD;
@@ -950,7 +967,6 @@ __global__ __launch_bounds__(kThreads) void evam_pp_wave(const WParams P) {
     const int tx = tile - ty * P.tiles_x;
     const __attribute__((address_space(4))) ItemDesc* it =
         (const __attribute__((address_space(4))) ItemDesc*)(P.items) + item;
-    const __attribute__((address_space(4))) YTab* ytab = (const __attribute__((address_space(4))) YTab*)(P.ytab);
     const __attribute__((address_space(4))) XTab* xtab_s = (const __attribute__((address_space(4))) XTab*)(P.xtab);
     const uint8_t* p0 = it->plane[0];
     const uint8_t* p1 = it->plane[1];
@@ -1026,6 +1042,8 @@ __global__ __launch_bounds__(kThreads) void evam_pp_wave(const WParams P) {
     // buffer layout: [Y tap0][Y tap1][C tap0][C tap1][V tap0][V tap1]
     const int oY1 = segY, oC0 = 2 * segY, oC1 = 2 * segY + segC, oV0 = 2 * segY + 2 * segC, oV1 = oV0 + segC;
 
+    LaneRows lr;  // this wave's rows (<= 64, host)
+    lr.load(P.ytab, Yw0, Yw1 - Yw0, lane);
     // Staging decision for output row Y, given the source rows (pa, pb) whose H the wave holds.
     struct Plan {
         int ya, yb, b0, b1;
@@ -1033,10 +1051,10 @@ __global__ __launch_bounds__(kThreads) void evam_pp_wave(const WParams P) {
     };
     auto plan = [&](int Y, int pa, int pb) {
         Plan q;
-        q.b0 = ytab[Y].b0;
-        q.b1 = ytab[Y].b1;
-        q.ya = y0 + ytab[Y].r0;
-        q.yb = y0 + ytab[Y].r1;
+        q.b0 = lr.B0(Y - Yw0);
+        q.b1 = lr.B1(Y - Yw0);
+        q.ya = y0 + lr.R0(Y - Yw0);
+        q.yb = y0 + lr.R1(Y - Yw0);
         q.pad = (q.b0 | q.b1) == 0 || !cols;
         if (REUSE) {
             q.stA = q.ya != pa && q.ya != pb;
@@ -1368,7 +1386,6 @@ __global__ __launch_bounds__(kThreads) void evam_pp_roi(const QParams P) {
     using T = FmtTraits<FMT>;
     constexpr bool kYUV = FMT == kNV12 || FMT == kI420;
     constexpr int NP = FMT == kI420 ? 3 : (FMT == kNV12 ? 2 : 1);
-    constexpr int NKIND = 2 * NP;  // segments per output row: (plane, tap)
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -1985,7 +2002,7 @@ bool plan_wave(int f, const Geom& g, int DW, int DH, int count, int out_dtype, i
     const int64_t slots = (int64_t)n_cu * per_cu;
     int64_t rpw = ((int64_t)count * w.tiles_x * DH) / (4 * slots);
     rpw = std::max<int64_t>(2, std::min<int64_t>(32, rpw));
-    w.TH = std::max(1, std::min(DH, env_int("EVAM_PP_WTH", (int)(4 * rpw))));
+    w.TH = std::max(1, std::min(std::min(DH, 4 * 64), env_int("EVAM_PP_WTH", (int)(4 * rpw))));  // <= 64 rows per wave
     w.tiles_per_item = w.tiles_x * ((DH + w.TH - 1) / w.TH);
     const int64_t gr = (int64_t)count * w.tiles_per_item;
     if (gr > 0x7FFFFFFF) return false;
@@ -2543,7 +2560,7 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
                 const int64_t cols = (int64_t)count[f] * sp.tiles_x;
                 const int64_t want = 8 * (int64_t)h->n_cu;
                 if (cols * ((DH + th - 1) / th) < want) th = (int)std::max<int64_t>(kStageRows, cols * DH / want);
-                sp.TH = std::max(1, std::min(DH, env_int("EVAM_PP_TH", th)));
+                sp.TH = std::max(1, std::min(std::min(DH, 64), env_int("EVAM_PP_TH", th)));  // rows live one per lane
                 sp.TH = (sp.TH + kStageRows - 1) / kStageRows * kStageRows;
                 sp.tiles_per_item = sp.tiles_x * ((DH + sp.TH - 1) / sp.TH);
                 const int np = f == kI420 ? 3 : (f == kNV12 ? 2 : 1);
