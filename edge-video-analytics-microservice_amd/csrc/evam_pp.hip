@@ -697,6 +697,7 @@ __global__ __launch_bounds__(kThreads) void evam_pp_staged(const SParams P) {
     const int tx = tile - ty * P.tiles_x;
     const __attribute__((address_space(4))) ItemDesc* it =
         (const __attribute__((address_space(4))) ItemDesc*)(P.items) + item;
+    const __attribute__((address_space(4))) YTab* ytab = (const __attribute__((address_space(4))) YTab*)(P.ytab);
     const __attribute__((address_space(4))) XTab* xtab_s = (const __attribute__((address_space(4))) XTab*)(P.xtab);
     const uint8_t* p0 = it->plane[0];
     const uint8_t* p1 = it->plane[1];
@@ -756,10 +757,8 @@ __global__ __launch_bounds__(kThreads) void evam_pp_staged(const SParams P) {
     }
     const uint32_t xo = (uint32_t)(xin ? X : 0) * (uint32_t)esz;
     const bool wave_stores = X0 + seg * 64 < P.DW;  // some lane of this wave stores (wave-uniform)
-    const int rows = Y1 - Y0;  // <= 64 (host)
+    const int rows = Y1 - Y0;
     const int ngroups = (rows + R - 1) / R;
-    LaneRows lr;
-    lr.load(P.ytab, Y0, rows, lane);
 
     // ---- LDS-DMA of group g into buffer `buf` (slot s = plane * 2R + 2 * row + tap) ----
     auto issue = [&](int g, uint8_t* buf) {
@@ -770,9 +769,9 @@ __global__ __launch_bounds__(kThreads) void evam_pp_staged(const SParams P) {
             const int pl = s / (2 * R), loc = s - pl * 2 * R, r = loc >> 1, tap = loc & 1;
             const int Y = Y0 + g * R + r;
             if (Y >= Y1) continue;
-            const int b0 = lr.B0(Y - Y0), b1 = lr.B1(Y - Y0);
+            const int b0 = ytab[Y].b0, b1 = ytab[Y].b1;
             if ((b0 | b1) == 0) continue;  // padding row: nothing to stage
-            const int ya = y0 + lr.R0(Y - Y0), yb = y0 + lr.R1(Y - Y0);
+            const int ya = y0 + ytab[Y].r0, yb = y0 + ytab[Y].r1;
             const int yr = tap ? yb : ya;
             if (pl > 0 && tap && (ya >> 1) == (yb >> 1)) continue;  // chroma row shared by both taps
             const int nck = pl == 0 ? nY : nC;
@@ -796,7 +795,7 @@ __global__ __launch_bounds__(kThreads) void evam_pp_staged(const SParams P) {
             const int r = rph + k * RSTEP;
             const int Y = Y0 + g * R + r;
             if (Y >= Y1) continue;
-            const int b0 = lr.B0(Y - Y0), b1 = lr.B1(Y - Y0);
+            const int b0 = ytab[Y].b0, b1 = ytab[Y].b1;
             const int sO = (int)((uint32_t)(Y * P.DW) * (uint32_t)esz);
             int v[3];
             if ((b0 | b1) == 0 || wa == 0 || (P.ablate & 2)) {  // padding row / column
@@ -809,7 +808,7 @@ __global__ __launch_bounds__(kThreads) void evam_pp_staged(const SParams P) {
                 const uint8_t* sc0 = buf + (2 * R + 2 * r) * kSlot;
                 int c[4][3];
                 if constexpr (kYUV) {
-                    const int ya = y0 + lr.R0(Y - Y0), yb = y0 + lr.R1(Y - Y0);
+                    const int ya = y0 + ytab[Y].r0, yb = y0 + ytab[Y].r1;
                     const bool share = (ya >> 1) == (yb >> 1);
                     const uint8_t* sc1 = share ? sc0 : sc0 + kSlot;
                     Chroma<FMT> cA, cB, cC, cD;
@@ -2527,8 +2526,11 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
                 int px = 0, lds = 0, grid = 0;
                 bool reuse = false;
                 const XTab* hx = reinterpret_cast<const XTab*>(h->h_block.data() + tab_off[f]);
+                // The wave kernel wins where consecutive output rows share source rows (vertical
+                // upscale: REUSE); for downscales the staged kernel's deeper shared staging is faster.
                 if (plan_wave(f, g0, DW, DH, count[f], cfg->out_dtype, h->n_cu, hx,
-                              reinterpret_cast<const YTab*>(hx + DW), w, px, reuse, lds, grid)) {
+                              reinterpret_cast<const YTab*>(hx + DW), w, px, reuse, lds, grid) &&
+                    (reuse || env_int("EVAM_PP_WAVE", 1) == 2)) {
                     w.items = items_d;
                     w.lut = lut_d;
                     w.xtab = reinterpret_cast<const XTab*>(d_block + tab_off[f]);
@@ -2560,7 +2562,7 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
                 const int64_t cols = (int64_t)count[f] * sp.tiles_x;
                 const int64_t want = 8 * (int64_t)h->n_cu;
                 if (cols * ((DH + th - 1) / th) < want) th = (int)std::max<int64_t>(kStageRows, cols * DH / want);
-                sp.TH = std::max(1, std::min(std::min(DH, 64), env_int("EVAM_PP_TH", th)));  // rows live one per lane
+                sp.TH = std::max(1, std::min(DH, env_int("EVAM_PP_TH", th)));
                 sp.TH = (sp.TH + kStageRows - 1) / kStageRows * kStageRows;
                 sp.tiles_per_item = sp.tiles_x * ((DH + sp.TH - 1) / sp.TH);
                 const int np = f == kI420 ? 3 : (f == kNV12 ? 2 : 1);

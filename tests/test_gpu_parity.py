@@ -361,13 +361,15 @@ def test_stats_and_timing(evam, O, gpu):
     ((300, 180), (131, 97), "aspect-ratio"),        # odd DW -> PX 1, letterbox
     ((480, 270), (224, 224), "aspect-crop"),        # C5 shape: central crop
 ])
-@pytest.mark.parametrize("variant", ["auto", "px1", "px2", "noreuse", "staged"])
+@pytest.mark.parametrize("variant", ["auto", "wave", "px1", "px2", "noreuse", "staged"])
 def test_wave_kernel_variants(evam, O, coracle, gpu, fmt, src, dst, resize, variant, monkeypatch):
-    """Uniform-geometry batches through the wave-row kernel (every PX / REUSE choice) and the staged
-    kernel it replaced (EVAM_PP_WAVE=0), RGB order, fp32 with normalisation and u8."""
+    """Uniform-geometry batches through the default kernel choice, the wave-row kernel forced
+    (EVAM_PP_WAVE=2; every PX / REUSE choice) and the staged kernel (EVAM_PP_WAVE=0), RGB order, fp32
+    with normalisation and u8."""
     import torch
 
-    env = {"px1": {"EVAM_PP_PX": "1"}, "px2": {"EVAM_PP_PX": "2"}, "noreuse": {"EVAM_PP_REUSE": "0"},
+    env = {"wave": {"EVAM_PP_WAVE": "2"}, "px1": {"EVAM_PP_WAVE": "2", "EVAM_PP_PX": "1"},
+           "px2": {"EVAM_PP_WAVE": "2", "EVAM_PP_PX": "2"}, "noreuse": {"EVAM_PP_WAVE": "2", "EVAM_PP_REUSE": "0"},
            "staged": {"EVAM_PP_WAVE": "0"}}.get(variant, {})
     for k, v in env.items():
         monkeypatch.setenv(k, v)
