@@ -883,9 +883,13 @@ __global__ __launch_bounds__(kThreads) void evam_pp_staged(const SParams P) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();  // every wave's DMA for g landed; every wave done reading g-1
         if (g + 1 < ngroups) issue(g + 1, (g & 1) ? buf0 : buf1);
+#ifndef EVAM_PP_NO_FENCE_TEST
         asm volatile("" ::: "memory");  // the next group's DMA stays ahead of this group's stores
+#endif
         compute(g, (g & 1) ? buf1 : buf0);
+#ifndef EVAM_PP_NO_FENCE_TEST
         asm volatile("" ::: "memory");
+#endif
     }
 }
 
@@ -1332,7 +1336,10 @@ struct alignas(16) SrcDesc {  // 48 B
 static_assert(sizeof(SrcDesc) == 48, "SrcDesc layout");
 static_assert(sizeof(evam_roi) == 20, "evam_roi layout");
 
-constexpr int kRoiK = 8;  // max pixels per lane per row group in the ROI kernel
+#ifndef EVAM_PP_ROI_K
+#define EVAM_PP_ROI_K 8
+#endif
+constexpr int kRoiK = EVAM_PP_ROI_K;  // max pixels per lane per row group in the ROI kernel
 
 struct QParams {
     const SrcDesc* srcs;
@@ -2072,6 +2079,7 @@ struct evam_pp {
     DescRing ring;
     PinRing pin;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    hipEvent_t ev_switch = nullptr;
     bool timed = false;
     TabCache tab_cache;
     evam_preproc lut_key{};        // cfg the cached LUT was built from (norm fields + dtype)
@@ -2151,6 +2159,13 @@ int ring_upload(evam_pp* h, const uint8_t** out) {
             HIP_TRY(hipEventCreateWithFlags(&r.used[k], hipEventDisableTiming));
         }
     }
+    // Fence the slot being retired: every kernel that read it is already on h->stream (a stream
+    // switch orders the new stream behind the old one, evam_pp_set_stream), so one event recorded now
+    // covers them all. Calls that reuse the resident block record nothing.
+    if (r.cur >= 0) {
+        HIP_TRY(hipEventRecord(r.used[r.cur], h->stream));
+        r.used_rec[r.cur] = true;
+    }
     const int k = (r.cur + 1) % DescRing::N;
     if (r.copied_rec[k]) HIP_TRY(hipEventSynchronize(r.copied[k]));  // host slot free
     if (r.cap[k] < n) {
@@ -2218,6 +2233,7 @@ void evam_pp_destroy(evam_pp* h) {
     }
     ring_release(h->ring);
     pin_release(h->pin);
+    if (h->ev_switch) (void)hipEventDestroy(h->ev_switch);
     if (h->ev0) (void)hipEventDestroy(h->ev0);
     if (h->ev1) (void)hipEventDestroy(h->ev1);
     delete h;
@@ -2225,7 +2241,16 @@ void evam_pp_destroy(evam_pp* h) {
 
 int evam_pp_set_stream(evam_pp* h, void* hip_stream) {
     if (!h) return fail(EVAM_PP_ERR_INVALID_ARG, "evam_pp_set_stream: NULL handle");
-    h->stream = reinterpret_cast<hipStream_t>(hip_stream);
+    hipStream_t ns = reinterpret_cast<hipStream_t>(hip_stream);
+    if (ns != h->stream && (h->ring.cur >= 0 || h->pin.cur >= 0)) {
+        // Order the new stream behind everything already launched on the old one, so the descriptor
+        // slots' fences (recorded on the current stream) keep covering earlier kernels.
+        HIP_TRY(hipSetDevice(h->device));
+        if (!h->ev_switch) HIP_TRY(hipEventCreateWithFlags(&h->ev_switch, hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(h->ev_switch, h->stream));
+        HIP_TRY(hipStreamWaitEvent(ns, h->ev_switch, 0));
+    }
+    h->stream = ns;
     return EVAM_PP_OK;
 }
 
@@ -2634,10 +2659,6 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
         hipError_t e = launch(f, cfg->out_dtype, p, (int)n_tiles, lds, h->stream);
         if (e != hipSuccess) return fail(EVAM_PP_ERR_HIP, "kernel launch failed: %s", hipGetErrorString(e));
         launches++;
-    }
-    if (!env_int("EVAM_PP_NO_EVENTS", 0)) {  // diagnostics only: unsafe once the ring wraps
-        HIP_TRY(hipEventRecord(h->ring.used[h->ring.cur], h->stream));
-        h->ring.used_rec[h->ring.cur] = true;
     }
     if (any_roi) {
         HIP_TRY(hipEventRecord(h->pin.used[h->pin.cur], h->stream));

@@ -387,3 +387,38 @@ def test_wave_kernel_variants(evam, O, coracle, gpu, fmt, src, dst, resize, vari
                          torch.float32 if dtype == "f32" else torch.uint8, info)
         ref, _ = run_oracle(O, coracle, frames, shape, dtype, info)
         assert_same(got, ref, f"wave {fmt} {src}->{dst} {resize} {variant} {dtype}")
+
+
+def test_stream_switch_and_descriptor_churn(evam, O, coracle, gpu):
+    """Descriptor slots stay valid across torch stream switches and many changing ROI sets / geometries
+    (the upload ring and the pinned ROI ring wrap several times; slot fences follow the stream)."""
+    import torch
+
+    rng = np.random.default_rng(11)
+    frames = [O.random_frame(rng, O.NV12, 320, 180) for _ in range(2)]
+    imgs = upload(evam, frames, gpu)
+    pp = evam.HipPreProcessor(device=0)
+    streams = [torch.cuda.Stream(device=gpu) for _ in range(3)]
+    outs, refs = [], []
+    for it in range(12):
+        s = streams[it % 3]
+        with torch.cuda.stream(s):
+            if it % 2:
+                rois = [(int(rng.integers(0, 2)), int(rng.integers(0, 200)), int(rng.integers(0, 100)),
+                         int(rng.integers(8, 120)), int(rng.integers(8, 80))) for _ in range(9)]
+                shape = (9, 3, 24, 40)
+                out = torch.full(shape, 7, dtype=torch.uint8, device=gpu)
+                pp.convert(imgs, out, None, rois=[evam.Roi(*r) for r in rois])
+                ref, _ = run_oracle(O, coracle, frames, shape, "u8", None, rois=rois)
+            else:
+                dw, dh = 32 + 8 * it, 16 + 4 * it  # a new uniform geometry (new tables) every time
+                shape = (2, 3, dh, dw)
+                out = torch.full(shape, 7, dtype=torch.uint8, device=gpu)
+                pp.convert(imgs, out)
+                ref, _ = run_oracle(O, coracle, frames, shape, "u8")
+            outs.append((out, s))
+            refs.append(ref)
+    torch.cuda.synchronize()
+    for i, ((out, _), ref) in enumerate(zip(outs, refs)):
+        assert_same(out.cpu().numpy(), ref, f"call {i}")
+    pp.close()
