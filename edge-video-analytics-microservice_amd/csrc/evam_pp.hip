@@ -717,9 +717,6 @@ __global__ __launch_bounds__(kThreads) void evam_pp_staged(const SParams P) {
     const __amdgpu_buffer_rsrc_t rsD2 = __builtin_amdgcn_make_buffer_rsrc((void*)d2, (short)0, 0x7FFFFFFF, 0x00020000);
 
     float* lut_s = reinterpret_cast<float*>(smem);
-    if constexpr (OUT == 1) {
-        for (int i = tid; i < 768; i += kThreads) lut_s[i] = P.lut[i];
-    }
     const int f0 = P.fill & 0xFF, f1 = (P.fill >> 8) & 0xFF, f2 = (P.fill >> 16) & 0xFF;
 
     const int X0 = tx * TW, Y0 = ty * P.TH, Y1 = min(Y0 + P.TH, P.DH);
@@ -740,21 +737,11 @@ __global__ __launch_bounds__(kThreads) void evam_pp_staged(const SParams P) {
             nC = ((((xb >> 1) + 1 + 15) & ~15) - fsC) >> 4;
         }
     }
-    // per-lane column state: LDS byte offsets of the taps inside a slot, weights
+    // per-lane column state (filled once the first DMA is in flight): LDS byte offsets of the taps
+    // inside a slot, weights
     const int X = X0 + seg * 64 + lane;
     const bool xin = X < P.DW;
     uint32_t lY0 = 0, lY1 = 0, lC0 = 0, lC1 = 0, wa = 0;
-    {
-        const XTab xt = P.xtab[xin ? X : 0];
-        wa = (uint32_t)xt.a0 | ((uint32_t)xt.a1 << 16);
-        if (xin && wa != 0) {
-            const int ca = x0 + xt.s0, cb = x0 + xt.s1;
-            lY0 = (uint32_t)(ca * T::bpp - fsY);
-            lY1 = (uint32_t)(cb * T::bpp - fsY);
-            lC0 = FMT == kNV12 ? (uint32_t)(2 * (ca >> 1) - fsC) : (uint32_t)((ca >> 1) - fsC);
-            lC1 = FMT == kNV12 ? (uint32_t)(2 * (cb >> 1) - fsC) : (uint32_t)((cb >> 1) - fsC);
-        }
-    }
     const uint32_t xo = (uint32_t)(xin ? X : 0) * (uint32_t)esz;
     const bool wave_stores = X0 + seg * 64 < P.DW;  // some lane of this wave stores (wave-uniform)
     const int rows = Y1 - Y0;
@@ -873,7 +860,24 @@ __global__ __launch_bounds__(kThreads) void evam_pp_staged(const SParams P) {
 
     uint8_t* const buf0 = smem + P.offBuf;
     uint8_t* const buf1 = buf0 + P.buf_bytes;
+    // Prologue: the first group's DMA goes out before the LUT and column-table loads, so their
+    // latencies overlap instead of adding up.
     issue(0, buf0);
+    asm volatile("" ::: "memory");
+    if constexpr (OUT == 1) {
+        for (int i = tid; i < 768; i += kThreads) lut_s[i] = P.lut[i];
+    }
+    {
+        const XTab xt = P.xtab[xin ? X : 0];
+        wa = (uint32_t)xt.a0 | ((uint32_t)xt.a1 << 16);
+        if (xin && wa != 0) {
+            const int ca = x0 + xt.s0, cb = x0 + xt.s1;
+            lY0 = (uint32_t)(ca * T::bpp - fsY);
+            lY1 = (uint32_t)(cb * T::bpp - fsY);
+            lC0 = FMT == kNV12 ? (uint32_t)(2 * (ca >> 1) - fsC) : (uint32_t)((ca >> 1) - fsC);
+            lC1 = FMT == kNV12 ? (uint32_t)(2 * (cb >> 1) - fsC) : (uint32_t)((cb >> 1) - fsC);
+        }
+    }
     for (int g = 0; g < ngroups; g++) {
         // DMA of group g landed (this wave's share), while the previous group's stores stay in flight
         // — unless that group was partial or its lanes skipped stores: then drain everything.
