@@ -40,6 +40,16 @@ namespace {
 // constants
 // ------------------------------------------------------------------------------------------------
 constexpr int kThreads = 256;
+
+// Optional SGPR cap (diagnostics). A CU admits floor(800 / (ceil(sgpr/16)*16 + 16)) 256-thread
+// workgroups (MI355X_MICROARCH.md, Residency), so the staged kernel's ~102 SGPRs allow 6. Capping at
+// 80 (8 per CU; the excess spills to VGPR lanes) measured 2-8 % SLOWER on every config
+// (profiles/r01_sweeps.txt, r01t), so the default leaves the allocation to the compiler.
+#ifdef EVAM_PP_SGPR_CAP
+#define EVAM_KERNEL_BOUNDS __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(EVAM_PP_SGPR_CAP)))
+#else
+#define EVAM_KERNEL_BOUNDS __launch_bounds__(kThreads)
+#endif
 constexpr int kLutBytes = 3 * 256 * 4;
 
 // OpenCV color_yuv.simd.hpp ITUR_BT_601_*; the -128 chroma bias is folded into the constants.
@@ -446,7 +456,7 @@ __device__ __forceinline__ UV3 chroma_terms(const Chroma<FMT>& c) {
 // both vertical taps read the same chroma row (4:2:0, ~half the rows) their chroma is loaded and
 // converted once.
 template <int FMT, int OUT>
-__global__ __launch_bounds__(kThreads) void evam_pp_rows(const RParams P) {
+__global__ EVAM_KERNEL_BOUNDS void evam_pp_rows(const RParams P) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     using T = FmtTraits<FMT>;
     constexpr bool kYUV = FMT == kNV12 || FMT == kI420;
@@ -675,7 +685,7 @@ struct LaneRows {
 // and VMEM carries only wide loads and the planar stores. Only the stores and the DMA use vmcnt; the
 // wait for group g+1 is vmcnt(stores issued after it), so the stores are never drained in the loop.
 template <int FMT, int OUT, int R, int NSEGX>
-__global__ __launch_bounds__(kThreads) void evam_pp_staged(const SParams P) {
+__global__ EVAM_KERNEL_BOUNDS void evam_pp_staged(const SParams P) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     using T = FmtTraits<FMT>;
     constexpr bool kYUV = FMT == kNV12 || FMT == kI420;
@@ -959,7 +969,7 @@ __device__ __forceinline__ void store_vec(const __amdgpu_buffer_rsrc_t rs, uint3
 //  * When both vertical taps read the same 4:2:0 chroma row, its BT.601 chroma terms are computed once.
 //  * Each channel of a row leaves as one PX-wide store per lane (dwordx4 for fp32 at PX = 4).
 template <int FMT, int OUT, int PX, bool REUSE>
-__global__ __launch_bounds__(kThreads) void evam_pp_wave(const WParams P) {
+__global__ EVAM_KERNEL_BOUNDS void evam_pp_wave(const WParams P) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     using T = FmtTraits<FMT>;
     constexpr bool kYUV = FMT == kNV12 || FMT == kI420;
@@ -1391,7 +1401,7 @@ __device__ __forceinline__ void wait_vmcnt_stores(int nk) {
 //  * the group's R x DW output pixels are packed densely onto the lanes (pixel p = tid + 256 k), so a
 //    72-wide classifier row keeps every lane busy and every store is row-contiguous.
 template <int FMT, int OUT>
-__global__ __launch_bounds__(kThreads) void evam_pp_roi(const QParams P) {
+__global__ EVAM_KERNEL_BOUNDS void evam_pp_roi(const QParams P) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     using T = FmtTraits<FMT>;
     constexpr bool kYUV = FMT == kNV12 || FMT == kI420;
