@@ -758,8 +758,38 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_staged(const SParams P) {
     const int ngroups = (rows + R - 1) / R;
 
     // ---- LDS-DMA of group g into buffer `buf` (slot s = plane * 2R + 2 * row + tap) ----
+    // Static DMA roles: with R = 2 the 2R (row, tap) pairs of a group are exactly the four waves, so
+    // wave w stages row w >> 1, tap w & 1 of every plane. One row-table fetch per group and no
+    // per-slot plane / resource selection in the scalar unit.
+    const int dr = wave >> 1, dtap = wave & 1;
     auto issue = [&](int g, uint8_t* buf) {
         if (!cols || (P.ablate & 16)) return;
+#ifndef EVAM_PP_DYN_ROLES
+        if constexpr (2 * R == 4) {
+            const int Y = Y0 + g * R + dr;
+            if (Y >= Y1) return;
+            const int b0 = ytab[Y].b0, b1 = ytab[Y].b1;
+            if ((b0 | b1) == 0) return;  // padding row: nothing to stage
+            const int ya = y0 + ytab[Y].r0, yb = y0 + ytab[Y].r1;
+            const int yr = dtap ? yb : ya;
+            if (lane < nY)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                    rsY, (__attribute__((address_space(3))) void*)(buf + wave * kSlot), 16, lane * 16, yr * pitch0 + fsY, 0, 0);
+            if constexpr (NP >= 2) {
+                if (dtap && (ya >> 1) == (yb >> 1)) return;  // chroma row shared by both taps
+                if (lane < nC) {
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                        rsC, (__attribute__((address_space(3))) void*)(buf + (2 * R + wave) * kSlot), 16, lane * 16,
+                        (yr >> 1) * pitch1 + fsC, 0, 0);
+                    if constexpr (NP >= 3)
+                        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                            rsV, (__attribute__((address_space(3))) void*)(buf + (4 * R + wave) * kSlot), 16, lane * 16,
+                            (yr >> 1) * pitch2 + fsC, 0, 0);
+                }
+            }
+            return;
+        }
+#endif
 #pragma unroll
         for (int s0 = 0; s0 < NS; s0 += 4) {
             const int s = s0 + wave;
