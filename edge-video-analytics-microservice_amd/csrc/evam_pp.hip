@@ -69,7 +69,7 @@ struct alignas(16) ItemDesc {
     int32_t pitch[3];
     int32_t x0, y0, cw, ch;  // effective crop in source pixels
     int32_t rw, rh, ox, oy;  // resized size, placement in the DW x DH plane
-    int32_t slot;
+    int32_t index;    // item index in the call: output slot = slot_offset + index * slot_stride
     int32_t pad_;
     double scale_x, scale_y; // OpenCV: 1. / ((double)rw / cw)
 };
@@ -79,6 +79,7 @@ struct KParams {
     const ItemDesc* items;
     const float* lut;  // [3][256]
     void* dst;
+    int slot_offset, slot_stride;  // output slot of item i = slot_offset + i * slot_stride
     int DW, DH;
     int TW, TH, tiles_x, tiles_per_item, n_tiles;
     uint32_t tw_magic;  // ceil(2^32 / TW) (TW > 1)
@@ -120,6 +121,7 @@ struct RParams {
     const XTab* xtab;    // [DW]
     const YTab* ytab;    // [DH]
     void* dst;
+    int slot_offset, slot_stride;  // output slot of item i = slot_offset + i * slot_stride
     int DW, DH;
     int TW, TH, tiles_x, tiles_per_item;
     int nsegx;           // TW / 64 column segments per tile row
@@ -140,6 +142,7 @@ struct SParams {
     const XTab* xtab;    // [DW]
     const YTab* ytab;    // [DH]
     void* dst;
+    int slot_offset, slot_stride;  // output slot of item i = slot_offset + i * slot_stride
     int DW, DH;
     int TH, tiles_x, tiles_per_item;
     int offBuf;          // LDS offset of staging buffer 0 (after the LUT)
@@ -289,7 +292,7 @@ __global__ __launch_bounds__(kThreads) void evam_pp_kernel(const KParams P) {
     const int X1 = min(X0 + P.TW, P.DW), Y1 = min(Y0 + P.TH, P.DH);
     const size_t plane = (size_t)P.DW * P.DH;
     const size_t esz = OUT == 1 ? 4 : 1;
-    uint8_t* const d0 = reinterpret_cast<uint8_t*>(P.dst) + (size_t)it->slot * 3 * plane * esz;
+    uint8_t* const d0 = reinterpret_cast<uint8_t*>(P.dst) + (size_t)(P.slot_offset + it->index * P.slot_stride) * 3 * plane * esz;
     uint8_t* const d1 = d0 + plane * esz;
     uint8_t* const d2 = d1 + plane * esz;
 
@@ -478,7 +481,7 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_rows(const RParams P) {
     const int x0 = it->x0, y0 = it->y0;
     const size_t plane = (size_t)P.DW * P.DH;
     const size_t esz = OUT == 1 ? 4 : 1;
-    uint8_t* const d0 = reinterpret_cast<uint8_t*>(P.dst) + (size_t)it->slot * 3 * plane * esz;
+    uint8_t* const d0 = reinterpret_cast<uint8_t*>(P.dst) + (size_t)(P.slot_offset + it->index * P.slot_stride) * 3 * plane * esz;
     uint8_t* const d1 = d0 + plane * esz;
     uint8_t* const d2 = d1 + plane * esz;
     // Buffer resources (wave-uniform). Offsets are always in range by construction, so the range
@@ -716,7 +719,7 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_staged(const SParams P) {
     const int x0 = it->x0, y0 = it->y0, ox = it->ox, rw = it->rw;
     const size_t plane = (size_t)P.DW * P.DH;
     const size_t esz = OUT == 1 ? 4 : 1;
-    uint8_t* const d0 = reinterpret_cast<uint8_t*>(P.dst) + (size_t)it->slot * 3 * plane * esz;
+    uint8_t* const d0 = reinterpret_cast<uint8_t*>(P.dst) + (size_t)(P.slot_offset + it->index * P.slot_stride) * 3 * plane * esz;
     uint8_t* const d1 = d0 + plane * esz;
     uint8_t* const d2 = d1 + plane * esz;
     const __amdgpu_buffer_rsrc_t rsY = __builtin_amdgcn_make_buffer_rsrc((void*)p0, (short)0, 0x7FFFFFFF, 0x00020000);
@@ -946,6 +949,7 @@ struct WParams {
     const XTab* xtab;    // [DW]
     const YTab* ytab;    // [DH]
     void* dst;
+    int slot_offset, slot_stride;  // output slot of item i = slot_offset + i * slot_stride
     int DW, DH;
     int TH, tiles_x, tiles_per_item;
     int offBuf;          // LDS offset of the per-wave staging areas (after the LUT)
@@ -1022,7 +1026,7 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_wave(const WParams P) {
     const int x0 = it->x0, y0 = it->y0, ox = it->ox, rw = it->rw;
     const size_t plane = (size_t)P.DW * P.DH;
     const size_t esz = OUT == 1 ? 4 : 1;
-    uint8_t* const d0 = reinterpret_cast<uint8_t*>(P.dst) + (size_t)it->slot * 3 * plane * esz;
+    uint8_t* const d0 = reinterpret_cast<uint8_t*>(P.dst) + (size_t)(P.slot_offset + it->index * P.slot_stride) * 3 * plane * esz;
     uint8_t* const d1 = d0 + plane * esz;
     uint8_t* const d2 = d1 + plane * esz;
     const __amdgpu_buffer_rsrc_t rsY = __builtin_amdgcn_make_buffer_rsrc((void*)p0, (short)0, 0x7FFFFFFF, 0x00020000);
@@ -2521,7 +2525,7 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
                 const Geom& g = geo[i];
                 d.x0 = g.x0; d.y0 = g.y0; d.cw = g.cw; d.ch = g.ch;
                 d.rw = g.rw; d.rh = g.rh; d.ox = g.ox; d.oy = g.oy;
-                d.slot = dst->slot_offset + i * dst->slot_stride;
+                d.index = i;  // the slot offset / stride are launch parameters: the block survives clip-ring steps
                 d.pad_ = 0;
                 d.scale_x = 1. / ((double)g.rw / g.cw);
                 d.scale_y = 1. / ((double)g.rh / g.ch);
@@ -2605,6 +2609,8 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
                     w.xtab = reinterpret_cast<const XTab*>(d_block + tab_off[f]);
                     w.ytab = reinterpret_cast<const YTab*>(w.xtab + DW);
                     w.dst = dst->data;
+                    w.slot_offset = dst->slot_offset;
+                    w.slot_stride = dst->slot_stride;
                     w.color_rgb = color_rgb;
                     w.fill = fill;
                     w.ablate = env_int("EVAM_PP_ABLATE", 0);
@@ -2622,6 +2628,8 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
                 sp.xtab = reinterpret_cast<const XTab*>(d_block + tab_off[f]);
                 sp.ytab = reinterpret_cast<const YTab*>(sp.xtab + DW);
                 sp.dst = dst->data;
+                sp.slot_offset = dst->slot_offset;
+                sp.slot_stride = dst->slot_stride;
                 sp.DW = DW; sp.DH = DH;
                 const int tw = 64 * nsegx;
                 sp.tiles_x = (DW + tw - 1) / tw;
@@ -2655,6 +2663,8 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
             r.xtab = reinterpret_cast<const XTab*>(d_block + tab_off[f]);
             r.ytab = reinterpret_cast<const YTab*>(r.xtab + DW);
             r.dst = dst->data;
+            r.slot_offset = dst->slot_offset;
+            r.slot_stride = dst->slot_stride;
             r.DW = DW; r.DH = DH;
             r.TW = rc.TW; r.TH = rc.TH;
             r.tiles_x = (DW + rc.TW - 1) / rc.TW;
@@ -2676,6 +2686,8 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
         p.items = items_d;
         p.lut = lut_d;
         p.dst = dst->data;
+        p.slot_offset = dst->slot_offset;
+        p.slot_stride = dst->slot_stride;
         p.DW = DW; p.DH = DH;
         p.TW = t.TW; p.TH = t.TH;
         p.tiles_x = (DW + t.TW - 1) / t.TW;
