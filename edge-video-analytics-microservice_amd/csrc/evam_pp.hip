@@ -1434,7 +1434,7 @@ __device__ __forceinline__ void wait_vmcnt_stores(int nk) {
 //    are packed back to back in LDS and arrive by LDS-DMA while the previous group is converted;
 //  * the group's R x DW output pixels are packed densely onto the lanes (pixel p = tid + 256 k), so a
 //    72-wide classifier row keeps every lane busy and every store is row-contiguous.
-template <int FMT, int OUT>
+template <int FMT, int OUT, int PX>
 __global__ EVAM_KERNEL_BOUNDS void evam_pp_roi(const QParams P) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     using T = FmtTraits<FMT>;
@@ -1526,42 +1526,49 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_roi(const QParams P) {
     // per-lane source offset each: 64 chunks (of any rows and taps) per instruction.
     const int segY = nY * 16, segC = nC * 16;
     const int rowb = 2 * segY + 2 * (NP - 1) * segC;
+    // Lanes own runs of PX adjacent pixels of one row (DW % PX == 0, host): a "quad" q of the
+    // group's R x QW quads covers row q / QW, columns PX * (q % QW) ...
+    constexpr int KQ = kRoiK / PX;                // max quads per lane per group
+    const int QW = DW / PX;
     int R = rowb > 0 ? P.buf_bytes / rowb : rows;
-    R = min(R, (kRoiK * kThreads) / DW);
+    R = min(R, (KQ * kThreads) / QW);
     R = max(1, min(R, rows));
     const int offC = 2 * R * segY;
-    const int npx = R * DW;                       // pixels per full group
-    const int K = (npx + kThreads - 1) / kThreads;
-    // store steps this wave issues in a full group: k with some lane of the wave holding a pixel
+    const int nq = R * QW;                        // quads per full group
+    const int K = (nq + kThreads - 1) / kThreads;
+    // store steps this wave issues in a full group: k with some lane of the wave holding a quad
     int nk_w = 0;
-    for (int k = 0; k < K; k++) nk_w += (k * kThreads + wave * 64 < npx) ? 1 : 0;
+    for (int k = 0; k < K; k++) nk_w += (k * kThreads + wave * 64 < nq) ? 1 : 0;
     // q / n for q < 2^16 by one mul_hi: m = ceil(2^32 / n) is exact there (n = 1: the identity).
     const uint32_t mY = nY > 1 ? (uint32_t)((0x100000000ull + nY - 1) / nY) : 0u;
     const uint32_t mC = nC > 1 ? (uint32_t)((0x100000000ull + nC - 1) / nC) : 0u;
     __syncthreads();
 
     const int f0 = P.fill & 0xFF, f1 = (P.fill >> 8) & 0xFF, f2 = (P.fill >> 16) & 0xFF;
-    // Per-lane pixel state for k < K, identical for every group: row of the pixel inside the group,
-    // packed LDS tap offsets (tap 0 low, tap 1 high half), horizontal weights.
-    uint32_t lY[kRoiK], lC[kRoiK], wa[kRoiK];
-    int rr[kRoiK];
+    // Per-lane state for quad steps k < K, identical for every group: row of the quad inside the
+    // group; per pixel packed LDS tap offsets (tap 0 low, tap 1 high half) and horizontal weights.
+    uint32_t lY[KQ][PX], lC[KQ][PX], wa[KQ][PX];
+    int rr[KQ];
 #pragma unroll
-    for (int k = 0; k < kRoiK; k++) {
-        const int p = tid + k * kThreads;
-        const bool v = k < K && p < npx;
-        const int r = v ? p / DW : 0;
-        const int c = v ? p - r * DW : 0;
+    for (int k = 0; k < KQ; k++) {
+        const int q = tid + k * kThreads;
+        const bool v = k < K && q < nq;
+        const int r = v ? q / QW : 0;
+        const int c0 = v ? (q - r * QW) * PX : 0;
         rr[k] = v ? r : -1;
-        const XTab e = xt[c];
-        wa[k] = (uint32_t)e.a0 | ((uint32_t)e.a1 << 16);
-        lY[k] = lC[k] = 0;
-        if (v && wa[k] != 0) {
-            const int ca = x0 + e.s0, cb = x0 + e.s1;
-            lY[k] = (uint32_t)(ca * T::bpp - fsY) | ((uint32_t)(cb * T::bpp - fsY) << 16);
-            if constexpr (FMT == kNV12)
-                lC[k] = (uint32_t)(2 * (ca >> 1) - fsC) | ((uint32_t)(2 * (cb >> 1) - fsC) << 16);
-            else if constexpr (FMT == kI420)
-                lC[k] = (uint32_t)((ca >> 1) - fsC) | ((uint32_t)((cb >> 1) - fsC) << 16);
+#pragma unroll
+        for (int j = 0; j < PX; j++) {
+            const XTab e = xt[c0 + j];
+            wa[k][j] = (uint32_t)e.a0 | ((uint32_t)e.a1 << 16);
+            lY[k][j] = lC[k][j] = 0;
+            if (v && wa[k][j] != 0) {
+                const int ca = x0 + e.s0, cb = x0 + e.s1;
+                lY[k][j] = (uint32_t)(ca * T::bpp - fsY) | ((uint32_t)(cb * T::bpp - fsY) << 16);
+                if constexpr (FMT == kNV12)
+                    lC[k][j] = (uint32_t)(2 * (ca >> 1) - fsC) | ((uint32_t)(2 * (cb >> 1) - fsC) << 16);
+                else if constexpr (FMT == kI420)
+                    lC[k][j] = (uint32_t)((ca >> 1) - fsC) | ((uint32_t)((cb >> 1) - fsC) << 16);
+            }
         }
     }
     const int ngroups = (rows + R - 1) / R;
@@ -1601,25 +1608,33 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_roi(const QParams P) {
     auto compute = [&](int grp, const uint8_t* buf) {
         const uint32_t gbase = (uint32_t)((Y0 + grp * R) * DW);
 #pragma unroll
-        for (int k = 0; k < kRoiK; k++) {
+        for (int k = 0; k < KQ; k++) {
             if (k >= K) break;
             const int ly = grp * R + rr[k];
             if (rr[k] < 0 || ly >= rows) continue;
             const YTab e = yt[ly];
-            int v[3];
-            if ((e.b0 | e.b1) == 0 || wa[k] == 0 || (P.ablate & 2)) {  // letterbox padding row / column
-                v[0] = f0; v[1] = f1; v[2] = f2;
-            } else {
-                const uint32_t a0 = wa[k] & 0xFFFF, a1 = wa[k] >> 16;
-                const uint32_t tY0 = lY[k] & 0xFFFF, tY1 = lY[k] >> 16;
-                const uint8_t* sy0 = buf + 2 * rr[k] * segY;
-                const uint8_t* sy1 = sy0 + segY;
+            const bool padrow = (e.b0 | e.b1) == 0 || (P.ablate & 2);  // letterbox padding row
+            const uint8_t* sy0 = buf + 2 * rr[k] * segY;
+            const uint8_t* sy1 = sy0 + segY;
+            const uint8_t* sc0 = buf + offC + 2 * rr[k] * segC;
+            const uint8_t* sc1 = sc0;
+            if constexpr (kYUV) {
+                const int ya = y0 + e.r0, yb = y0 + e.r1;
+                sc1 = (ya >> 1) == (yb >> 1) ? sc0 : sc0 + segC;
+            }
+            const uint32_t wb0 = (uint32_t)e.b0, wb1 = (uint32_t)e.b1;
+            int v[3][PX];
+#pragma unroll
+            for (int j = 0; j < PX; j++) {
+                if (padrow || wa[k][j] == 0) {  // padding row / column
+                    v[0][j] = f0; v[1][j] = f1; v[2][j] = f2;
+                    continue;
+                }
+                const uint32_t a0 = wa[k][j] & 0xFFFF, a1 = wa[k][j] >> 16;
+                const uint32_t tY0 = lY[k][j] & 0xFFFF, tY1 = lY[k][j] >> 16;
                 int c[4][3];
                 if constexpr (kYUV) {
-                    const uint32_t tC0 = lC[k] & 0xFFFF, tC1 = lC[k] >> 16;
-                    const int ya = y0 + e.r0, yb = y0 + e.r1;
-                    const uint8_t* sc0 = buf + offC + 2 * rr[k] * segC;
-                    const uint8_t* sc1 = (ya >> 1) == (yb >> 1) ? sc0 : sc0 + segC;
+                    const uint32_t tC0 = lC[k][j] & 0xFFFF, tC1 = lC[k][j] >> 16;
                     Chroma<FMT> cA, cB, cC, cD;
                     if constexpr (FMT == kNV12) {
                         cA.u = *reinterpret_cast<const uint16_t*>(sc0 + tC0);
@@ -1650,29 +1665,24 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_roi(const QParams P) {
                         }
                     }
                 }
-                const uint32_t wb0 = (uint32_t)e.b0, wb1 = (uint32_t)e.b1;
 #pragma unroll
                 for (int ch3 = 0; ch3 < 3; ch3++) {
                     const uint32_t D0 = __umul24(c[0][ch3], a0) + __umul24(c[1][ch3], a1);
                     const uint32_t D1 = __umul24(c[2][ch3], a0) + __umul24(c[3][ch3], a1);
-                    v[ch3] = vresize(D0, D1, wb0, wb1);
+                    v[ch3][j] = vresize(D0, D1, wb0, wb1);
                 }
-                if (P.color_rgb) { const int tmp = v[0]; v[0] = v[2]; v[2] = tmp; }
+                if (P.color_rgb) { const int tmp = v[0][j]; v[0][j] = v[2][j]; v[2][j] = tmp; }
             }
-            const uint32_t vo = (gbase + (uint32_t)(tid + k * kThreads)) * (uint32_t)esz;
+            // soffset 0: the row offset is in voffset (a > 8-byte store with an SGPR soffset misses
+            // the compiler's store-data hazard wait on gfx950, see evam_pp_wave)
+            const uint32_t vo = (gbase + (uint32_t)(tid + k * kThreads) * PX) * (uint32_t)esz;
             if (P.ablate & 4) {
-                asm volatile("" :: "v"(v[0]), "v"(v[1]), "v"(v[2]));
+                asm volatile("" :: "v"(v[0][0]), "v"(v[1][0]), "v"(v[2][0]));
                 continue;
             }
-            if constexpr (OUT == 1) {
-                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lut_s[v[0]]), rsD0, vo, 0, 0);
-                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lut_s[256 + v[1]]), rsD1, vo, 0, 0);
-                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lut_s[512 + v[2]]), rsD2, vo, 0, 0);
-            } else {
-                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v[0], rsD0, vo, 0, 0);
-                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v[1], rsD1, vo, 0, 0);
-                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v[2], rsD2, vo, 0, 0);
-            }
+            store_vec<OUT, PX>(rsD0, vo, 0, lut_s, v[0]);
+            store_vec<OUT, PX>(rsD1, vo, 0, lut_s + 256, v[1]);
+            store_vec<OUT, PX>(rsD2, vo, 0, lut_s + 512, v[2]);
         }
     };
 
@@ -1949,14 +1959,23 @@ hipError_t launch(int f, int out, const KParams& p, int grid, int lds, hipStream
     }
 }
 
-template <int FMT, int OUT>
-hipError_t launch_roi_t(const QParams& p, int grid, int lds, hipStream_t s) {
+template <int FMT, int OUT, int PX>
+hipError_t launch_roi_px(const QParams& p, int grid, int lds, hipStream_t s) {
     if (lds > 64 * 1024) {
-        hipError_t e = hipFuncSetAttribute((const void*)evam_pp_roi<FMT, OUT>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        hipError_t e = hipFuncSetAttribute((const void*)evam_pp_roi<FMT, OUT, PX>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL((evam_pp_roi<FMT, OUT>), dim3(grid), dim3(kThreads), lds, s, p);
+    hipLaunchKernelGGL((evam_pp_roi<FMT, OUT, PX>), dim3(grid), dim3(kThreads), lds, s, p);
     return hipGetLastError();
+}
+
+// PX = 4 adjacent pixels per lane when the output width allows it (one dwordx4 / dword store per
+// channel, one row-table read and row setup per 4 pixels), else 1.
+template <int FMT, int OUT>
+hipError_t launch_roi_t(const QParams& p, int grid, int lds, hipStream_t s) {
+    const int want = env_int("EVAM_PP_ROI_PX", 4);
+    if (want == 4 && p.DW % 4 == 0) return launch_roi_px<FMT, OUT, 4>(p, grid, lds, s);
+    return launch_roi_px<FMT, OUT, 1>(p, grid, lds, s);
 }
 
 hipError_t launch_roi(int f, int out, const QParams& p, int grid, int lds, hipStream_t s) {
