@@ -1969,11 +1969,12 @@ hipError_t launch_roi_px(const QParams& p, int grid, int lds, hipStream_t s) {
     return hipGetLastError();
 }
 
-// PX = 4 adjacent pixels per lane when the output width allows it (one dwordx4 / dword store per
-// channel, one row-table read and row setup per 4 pixels), else 1.
+// PX = 1 (adjacent lanes, adjacent pixels) by default. PX = 4 (one dwordx4 store per channel and
+// one row setup per 4 pixels; EVAM_PP_ROI_PX=4) measured 8 % slower on C3: lanes 4 pixels apart
+// spread their LDS tap reads over 4x more dwords, so the byte reads bank-conflict.
 template <int FMT, int OUT>
 hipError_t launch_roi_t(const QParams& p, int grid, int lds, hipStream_t s) {
-    const int want = env_int("EVAM_PP_ROI_PX", 4);
+    const int want = env_int("EVAM_PP_ROI_PX", 1);
     if (want == 4 && p.DW % 4 == 0) return launch_roi_px<FMT, OUT, 4>(p, grid, lds, s);
     return launch_roi_px<FMT, OUT, 1>(p, grid, lds, s);
 }
