@@ -422,3 +422,26 @@ def test_stream_switch_and_descriptor_churn(evam, O, coracle, gpu):
     for i, ((out, _), ref) in enumerate(zip(outs, refs)):
         assert_same(out.cpu().numpy(), ref, f"call {i}")
     pp.close()
+
+
+@pytest.mark.parametrize("fmt", FORMATS)
+@pytest.mark.parametrize("dst,dtype", [((72, 72), "f32"), ((64, 36), "u8")])
+def test_roi_kernel_px4(evam, O, coracle, gpu, fmt, dst, dtype, monkeypatch):
+    """The ROI kernel's 4-pixels-per-lane variant (EVAM_PP_ROI_PX=4) on a ROI batch."""
+    import torch
+
+    monkeypatch.setenv("EVAM_PP_ROI_PX", "4")
+    rng = np.random.default_rng(zlib.crc32(f"px4{fmt}{dst}".encode()))
+    W, H = 320, 200
+    frames = [O.random_frame(rng, fc(O, fmt), W, H, pattern="gradient" if i else "uniform") for i in range(2)]
+    rois = [(int(rng.integers(0, 2)), int(rng.integers(-10, W - 4)), int(rng.integers(-10, H - 4)),
+             int(rng.integers(4, 260)), int(rng.integers(4, 180))) for _ in range(20)]
+    rois = [(s, x, y, max(w, 4 - x), max(h, 4 - y)) for s, x, y, w, h in rois]
+    info = evam.PreProcInfo(resize="aspect-ratio", placement="center", fill=(1, 2, 3), color_space="RGB",
+                            **({"range": (0.0, 1.0), "mean": (0.1, 0.2, 0.3), "std": (0.3, 0.2, 0.1)}
+                               if dtype == "f32" else {}))
+    shape = (len(rois), 3, dst[1], dst[0])
+    got, _ = run_hip(evam, torch, upload(evam, frames, gpu), shape,
+                     torch.float32 if dtype == "f32" else torch.uint8, info, rois=[evam.Roi(*r) for r in rois])
+    ref, _ = run_oracle(O, coracle, frames, shape, dtype, info, rois=rois)
+    assert_same(got, ref, f"roi px4 {fmt} {dst} {dtype}")
