@@ -161,9 +161,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # EVAM_BENCH_BACKEND=gloo: rehearse the multi-process path with more ranks than GPUs (ranks share
+    # devices round-robin; the post-run exchange goes over gloo on CPU tensors). Default: RCCL.
+    backend = os.environ.get("EVAM_BENCH_BACKEND", "nccl")
+    if backend == "gloo":
+        local = local % max(1, torch.cuda.device_count())
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        else:
+            dist.init_process_group(backend)
     device = torch.device(f"cuda:{local}")
     torch.cuda.set_device(device)
 
@@ -241,7 +249,7 @@ def main():
     wall = time.perf_counter() - t0
     kern_ms = e0.elapsed_time(e1) / args.steps  # one launch per step
     tot = evam.streams.reduce_run(wall, n * args.steps, alg_bytes * args.steps,
-                                  device=device if world > 1 else None)
+                                  device=device if world > 1 and backend == "nccl" else None)
     wall_max = tot.elapsed_max_s
     value = tot.frames / wall_max
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
