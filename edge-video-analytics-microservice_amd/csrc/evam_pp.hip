@@ -1384,6 +1384,13 @@ struct alignas(16) SrcDesc {  // 48 B
 static_assert(sizeof(SrcDesc) == 48, "SrcDesc layout");
 static_assert(sizeof(evam_roi) == 20, "evam_roi layout");
 
+// One ROI in launch order: the caller's rect plus its item index (output slot, transform).
+struct RoiRec {  // 24 B
+    int32_t src_index, x, y, w, h;
+    int32_t item;
+};
+static_assert(sizeof(RoiRec) == 24, "RoiRec layout");
+
 #ifndef EVAM_PP_ROI_K
 #define EVAM_PP_ROI_K 8
 #endif
@@ -1391,8 +1398,7 @@ constexpr int kRoiK = EVAM_PP_ROI_K;  // max pixels per lane per row group in th
 
 struct QParams {
     const SrcDesc* srcs;
-    const evam_roi* rois;     // the caller's ROI array, as passed to evam_pp_run
-    const int32_t* index;     // item indices handled by this launch (NULL: 0..n-1)
+    const RoiRec* recs;       // this launch's ROIs in launch order (largest work first)
     const float* lut;         // [3][256]
     void* dst;
     int DW, DH;
@@ -1447,9 +1453,8 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_roi(const QParams P) {
     const int t = blockIdx.x;
     const int li = t / P.tiles_per_item;
     const int ty = t - li * P.tiles_per_item;
-    const int item = P.index ? ((const __attribute__((address_space(4))) int32_t*)P.index)[li] : li;
-    const __attribute__((address_space(4))) evam_roi* roi =
-        (const __attribute__((address_space(4))) evam_roi*)(P.rois) + item;
+    const __attribute__((address_space(4))) RoiRec* roi = (const __attribute__((address_space(4))) RoiRec*)(P.recs) + li;
+    const int item = roi->item;
     const __attribute__((address_space(4))) SrcDesc* src =
         (const __attribute__((address_space(4))) SrcDesc*)(P.srcs) + roi->src_index;
     Geom g;
@@ -2154,6 +2159,7 @@ struct evam_pp {
     bool lut_valid = false;
     float lut[768];
     std::vector<int> sc_fmt;       // per-call scratch, kept to avoid reallocation
+    std::vector<int> sc_bucket;
     std::vector<Geom> sc_geo;
 };
 
@@ -2446,11 +2452,9 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
     QParams qp[4];
     int qlds[4] = {0, 0, 0, 0};
     bool any_desc = false, any_roi = false;
-    int nfmt = 0;
     for (int f = 0; f < 4; f++) {
         path[f] = kPathNone;
         if (!count[f]) continue;
-        nfmt++;
         if (uniform[f] && rows_enabled) path[f] = kPathUniform;
         else if (roi_enabled && plan_roi(DW, DH, cfg->out_dtype, row_bytes_bound(f, max_cw[f]), qp[f], qlds[f])) path[f] = kPathRoi;
         else path[f] = kPathGeneric;
@@ -2495,21 +2499,18 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
         tab_off[f] = nbytes;
         nbytes += sizeof(XTab) * (size_t)DW + sizeof(YTab) * (size_t)DH;
     }
-    // ROI groups: [SrcDesc x n_srcs][evam_roi x n_items][per ROI group of a mixed-format batch: indices],
-    // in a pinned zero-copy slot (PinRing).
-    size_t src_off = 0, roi_off = 0, idx_off[4] = {0, 0, 0, 0}, dyn_bytes = 0;
+    // ROI groups: [SrcDesc x n_srcs][per ROI group: RoiRec x count], in a pinned zero-copy slot
+    // (PinRing).
+    size_t src_off = 0, rec_off[4] = {0, 0, 0, 0}, dyn_bytes = 0;
     if (any_roi) {
         src_off = 0;
         dyn_bytes = sizeof(SrcDesc) * (size_t)n_srcs;
-        roi_off = dyn_bytes;
-        dyn_bytes += sizeof(evam_roi) * (size_t)n_items;
-        if (nfmt > 1)
-            for (int f = 0; f < 4; f++) {
-                if (path[f] != kPathRoi) continue;
-                dyn_bytes = (dyn_bytes + 15) & ~(size_t)15;
-                idx_off[f] = dyn_bytes;
-                dyn_bytes += sizeof(int32_t) * (size_t)count[f];
-            }
+        for (int f = 0; f < 4; f++) {
+            if (path[f] != kPathRoi) continue;
+            dyn_bytes = (dyn_bytes + 15) & ~(size_t)15;
+            rec_off[f] = dyn_bytes;
+            dyn_bytes += sizeof(RoiRec) * (size_t)count[f];
+        }
     }
     h->h_block.resize(nbytes);
     uint8_t* blk = h->h_block.data();
@@ -2567,16 +2568,37 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
             for (int p = 0; p < 3; p++) { sd[i].plane[p] = srcs[i].planes[p]; sd[i].pitch[p] = srcs[i].pitch[p]; }
             sd[i].width = srcs[i].width; sd[i].height = srcs[i].height; sd[i].pad_ = 0;
         }
-        evam_roi* rd = reinterpret_cast<evam_roi*>(dyn + roi_off);
-        if (items) memcpy(rd, items, sizeof(evam_roi) * (size_t)n_items);
-        else
-            for (int i = 0; i < n_items; i++) rd[i] = evam_roi{i, 0, 0, 0, 0};  // w <= 0: the full frame
+        // Launch order: largest estimated work first (counting sort on 64 buckets of the staged
+        // bytes, crop width x touched rows). Workgroups are dispatched in order as slots free, so
+        // the long ROIs start first and the short ones fill the tail.
+        const bool sort = env_int("EVAM_PP_ROI_SORT", 1) != 0;
+        std::vector<int>& bucket = h->sc_bucket;
+        bucket.resize(n_items);
         for (int f = 0; f < 4; f++) {
-            if (!idx_off[f]) continue;
-            int32_t* ix = reinterpret_cast<int32_t*>(dyn + idx_off[f]);
-            int o = 0;
-            for (int i = 0; i < n_items; i++)
-                if (fmt[i] == f) ix[o++] = i;
+            if (!rec_off[f]) continue;
+            RoiRec* rr = reinterpret_cast<RoiRec*>(dyn + rec_off[f]);
+            int64_t maxw = 1;
+            if (sort)
+                for (int i = 0; i < n_items; i++) {
+                    if (fmt[i] != f) continue;
+                    const int64_t w = (int64_t)geo[i].cw * std::min(geo[i].ch, 2 * DH);
+                    maxw = std::max(maxw, w);
+                }
+            int start[65] = {0};
+            for (int i = 0; i < n_items; i++) {
+                if (fmt[i] != f) continue;
+                const int64_t w = (int64_t)geo[i].cw * std::min(geo[i].ch, 2 * DH);
+                bucket[i] = sort ? 63 - (int)(w * 63 / maxw) : 0;  // 0 = largest
+                start[bucket[i] + 1]++;
+            }
+            for (int b = 0; b < 64; b++) start[b + 1] += start[b];
+            for (int i = 0; i < n_items; i++) {
+                if (fmt[i] != f) continue;
+                RoiRec& r = rr[start[bucket[i]]++];
+                if (items) { r.src_index = items[i].src_index; r.x = items[i].x; r.y = items[i].y; r.w = items[i].w; r.h = items[i].h; }
+                else { r.src_index = i; r.x = r.y = r.w = r.h = 0; }  // w <= 0: the full frame
+                r.item = i;
+            }
         }
     }
     const uint8_t* d_block = nullptr;
@@ -2594,8 +2616,7 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
         if (path[f] == kPathRoi) {
             QParams q = qp[f];
             q.srcs = reinterpret_cast<const SrcDesc*>(d_dyn + src_off);
-            q.rois = reinterpret_cast<const evam_roi*>(d_dyn + roi_off);
-            q.index = idx_off[f] ? reinterpret_cast<const int32_t*>(d_dyn + idx_off[f]) : nullptr;
+            q.recs = reinterpret_cast<const RoiRec*>(d_dyn + rec_off[f]);
             q.lut = lut_d;
             q.dst = dst->data;
             q.mode = cfg->resize_mode;
