@@ -1374,22 +1374,19 @@ inline int row_bytes_bound(int f, int cw) {
     return 2 * segY + 2 * npc * segC;
 }
 
-// One decoded source, for kernels that resolve items on the device.
-struct alignas(16) SrcDesc {  // 48 B
+static_assert(sizeof(evam_roi) == 20, "evam_roi layout");
+
+// One ROI in launch order, self-contained: its source frame's planes and size next to the caller's
+// rect and the item index (output slot), so a workgroup needs one 64-byte scalar load (one round
+// trip over PCIe from the pinned descriptor slot) before it can resolve the geometry.
+struct alignas(64) RoiRec {  // 64 B
     const uint8_t* plane[3];
     int32_t pitch[3];
     int32_t width, height;
-    int32_t pad_;
-};
-static_assert(sizeof(SrcDesc) == 48, "SrcDesc layout");
-static_assert(sizeof(evam_roi) == 20, "evam_roi layout");
-
-// One ROI in launch order: the caller's rect plus its item index (output slot, transform).
-struct RoiRec {  // 24 B
-    int32_t src_index, x, y, w, h;
+    int32_t x, y, w, h;
     int32_t item;
 };
-static_assert(sizeof(RoiRec) == 24, "RoiRec layout");
+static_assert(sizeof(RoiRec) == 64, "RoiRec layout");
 
 #ifndef EVAM_PP_ROI_K
 #define EVAM_PP_ROI_K 8
@@ -1397,7 +1394,6 @@ static_assert(sizeof(RoiRec) == 24, "RoiRec layout");
 constexpr int kRoiK = EVAM_PP_ROI_K;  // max pixels per lane per row group in the ROI kernel
 
 struct QParams {
-    const SrcDesc* srcs;
     const RoiRec* recs;       // this launch's ROIs in launch order (largest work first)
     const float* lut;         // [3][256]
     void* dst;
@@ -1455,8 +1451,7 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_roi(const QParams P) {
     const int ty = t - li * P.tiles_per_item;
     const __attribute__((address_space(4))) RoiRec* roi = (const __attribute__((address_space(4))) RoiRec*)(P.recs) + li;
     const int item = roi->item;
-    const __attribute__((address_space(4))) SrcDesc* src =
-        (const __attribute__((address_space(4))) SrcDesc*)(P.srcs) + roi->src_index;
+    const __attribute__((address_space(4))) RoiRec* src = roi;
     Geom g;
     roi_geometry(FMT, src->width, src->height, true, roi->x, roi->y, roi->w, roi->h, P.mode, P.placement, P.DW,
                  P.DH, g);  // never empty: the host validated every item
@@ -2098,6 +2093,7 @@ bool plan_roi(int DW, int DH, int out_dtype, int max_row_bytes, QParams& q, int&
     const int def_buf = env_int("EVAM_PP_ROI_BUF", 12 * 1024);
     q.DW = DW; q.DH = DH;
     q.TH = (int64_t)DW * DH <= 32768 ? DH : std::max(8, std::min(DH, 16384 / DW));
+    q.TH = std::max(1, std::min(DH, env_int("EVAM_PP_ROI_TH", q.TH)));
     q.tiles_per_item = (DH + q.TH - 1) / q.TH;
     q.offXT = out_dtype == EVAM_DTYPE_F32 ? kLutBytes : 0;
     q.offYT = q.offXT + (int)sizeof(XTab) * DW;
@@ -2126,7 +2122,7 @@ struct DescRing {
     std::vector<uint8_t> last;  // bytes currently held by dev[cur]
 };
 
-// Per-call ROI descriptors ([SrcDesc x n_srcs][evam_roi x n][item indices]) change with every
+// Per-call ROI descriptors ([RoiRec x n], launch order) change with every
 // detection result. They are written into a slot of pinned, coherent (fine-grained) host memory that
 // the ROI kernel reads directly over PCIe: each workgroup fetches only its own ~70 bytes, so a call
 // costs one memcpy and no copy command. `used[k]` fences the reuse of slot k.
@@ -2443,7 +2439,7 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
 
     // ---- per format group: kernel choice ----
     //   uniform geometry        -> staged / row kernels, host-built tables, per-item ItemDesc
-    //   per-item geometry       -> ROI kernel: raw evam_roi + SrcDesc, geometry resolved on the device
+    //   per-item geometry       -> ROI kernel: raw ROI rect + source (RoiRec), geometry resolved on the device
     //   ROI plan impossible     -> generic kernel, per-item ItemDesc
     enum { kPathNone, kPathUniform, kPathRoi, kPathGeneric };
     const bool rows_enabled = env_int("EVAM_PP_ROWS", 1) != 0;
@@ -2485,7 +2481,6 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
 
     // ---- descriptor block ----
     // [LUT][ItemDesc x (items of uniform/generic groups)][per uniform group: XTab x DW, YTab x DH]
-    // [SrcDesc x n_srcs][evam_roi x n_items][per ROI group of a mixed-format batch: int32 item index x count]
     size_t nbytes = kLutBytes;
     size_t desc_off = nbytes;
     int n_desc = 0;
@@ -2499,15 +2494,11 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
         tab_off[f] = nbytes;
         nbytes += sizeof(XTab) * (size_t)DW + sizeof(YTab) * (size_t)DH;
     }
-    // ROI groups: [SrcDesc x n_srcs][per ROI group: RoiRec x count], in a pinned zero-copy slot
-    // (PinRing).
-    size_t src_off = 0, rec_off[4] = {0, 0, 0, 0}, dyn_bytes = 0;
+    // ROI groups: [per ROI group: RoiRec x count], in a pinned zero-copy slot (PinRing).
+    size_t rec_off[4] = {0, 0, 0, 0}, dyn_bytes = 0;
     if (any_roi) {
-        src_off = 0;
-        dyn_bytes = sizeof(SrcDesc) * (size_t)n_srcs;
         for (int f = 0; f < 4; f++) {
             if (path[f] != kPathRoi) continue;
-            dyn_bytes = (dyn_bytes + 15) & ~(size_t)15;
             rec_off[f] = dyn_bytes;
             dyn_bytes += sizeof(RoiRec) * (size_t)count[f];
         }
@@ -2563,11 +2554,6 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
     const uint8_t* d_dyn = nullptr;
     if (any_roi) {
         if (int rc = pin_acquire(h, dyn_bytes, &dyn, &d_dyn)) return rc;
-        SrcDesc* sd = reinterpret_cast<SrcDesc*>(dyn + src_off);
-        for (int i = 0; i < n_srcs; i++) {
-            for (int p = 0; p < 3; p++) { sd[i].plane[p] = srcs[i].planes[p]; sd[i].pitch[p] = srcs[i].pitch[p]; }
-            sd[i].width = srcs[i].width; sd[i].height = srcs[i].height; sd[i].pad_ = 0;
-        }
         // Launch order: largest estimated work first (counting sort on 64 buckets of the staged
         // bytes, crop width x touched rows). Workgroups are dispatched in order as slots free, so
         // the long ROIs start first and the short ones fill the tail.
@@ -2575,7 +2561,7 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
         std::vector<int>& bucket = h->sc_bucket;
         bucket.resize(n_items);
         for (int f = 0; f < 4; f++) {
-            if (!rec_off[f]) continue;
+            if (path[f] != kPathRoi) continue;
             RoiRec* rr = reinterpret_cast<RoiRec*>(dyn + rec_off[f]);
             int64_t maxw = 1;
             if (sort)
@@ -2595,8 +2581,12 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
             for (int i = 0; i < n_items; i++) {
                 if (fmt[i] != f) continue;
                 RoiRec& r = rr[start[bucket[i]]++];
-                if (items) { r.src_index = items[i].src_index; r.x = items[i].x; r.y = items[i].y; r.w = items[i].w; r.h = items[i].h; }
-                else { r.src_index = i; r.x = r.y = r.w = r.h = 0; }  // w <= 0: the full frame
+                const evam_image& sim = srcs[items ? items[i].src_index : i];
+                r.plane[0] = sim.planes[0]; r.plane[1] = sim.planes[1]; r.plane[2] = sim.planes[2];
+                r.pitch[0] = sim.pitch[0]; r.pitch[1] = sim.pitch[1]; r.pitch[2] = sim.pitch[2];
+                r.width = sim.width; r.height = sim.height;
+                if (items) { r.x = items[i].x; r.y = items[i].y; r.w = items[i].w; r.h = items[i].h; }
+                else { r.x = r.y = r.w = r.h = 0; }  // w <= 0: the full frame
                 r.item = i;
             }
         }
@@ -2615,7 +2605,6 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
         const float* lut_d = reinterpret_cast<const float*>(d_block);
         if (path[f] == kPathRoi) {
             QParams q = qp[f];
-            q.srcs = reinterpret_cast<const SrcDesc*>(d_dyn + src_off);
             q.recs = reinterpret_cast<const RoiRec*>(d_dyn + rec_off[f]);
             q.lut = lut_d;
             q.dst = dst->data;
