@@ -1405,7 +1405,8 @@ struct QParams {
     int buf_bytes;            // one staging buffer
     int color_rgb;
     uint32_t fill;
-    int ablate;               // diagnostics only (EVAM_PP_ABLATE bits): 2 no pixel math, 4 no stores, 16 no DMA
+    int ablate;               // diagnostics only (EVAM_PP_ABLATE bits): 2 no pixel math, 4 no stores, 16 no DMA,
+                              // 32 stop after setup, 64 stop after geometry, 128 return at entry
 };
 
 template <int N>
@@ -1446,6 +1447,7 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_roi(const QParams P) {
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    if (P.ablate & 128) return;  // diagnostics: launch cost only
     const int t = blockIdx.x;
     const int li = t / P.tiles_per_item;
     const int ty = t - li * P.tiles_per_item;
@@ -1459,6 +1461,8 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_roi(const QParams P) {
     const int cw = __builtin_amdgcn_readfirstlane(g.cw), ch = __builtin_amdgcn_readfirstlane(g.ch);
     const int rw = __builtin_amdgcn_readfirstlane(g.rw), rh = __builtin_amdgcn_readfirstlane(g.rh);
     const int ox = __builtin_amdgcn_readfirstlane(g.ox), oy = __builtin_amdgcn_readfirstlane(g.oy);
+    // diagnostics: stop after the geometry (64) / after the per-lane setup (32)
+    if ((P.ablate & 64) && rw != -7) return;
     const double scx = 1. / ((double)rw / cw), scy = 1. / ((double)rh / ch);
     const uint8_t* p0 = src->plane[0];
     const uint8_t* p1 = src->plane[1];
@@ -1572,6 +1576,10 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_roi(const QParams P) {
         }
     }
     const int ngroups = (rows + R - 1) / R;
+    if ((P.ablate & 32) && ngroups != -7) {
+        asm volatile("" :: "v"(lY[0][0]), "v"(lC[0][0]), "v"(wa[0][0]), "v"(rr[0]), "s"(mY), "s"(mC));
+        return;
+    }
 
     // One plane region of group grp: chunk q -> (segment, chunk) -> (row, tap) -> source offset.
     auto issue_plane = [&](int grp, uint8_t* base, int nr, int n, uint32_t m, int pl) {
