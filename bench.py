@@ -248,6 +248,17 @@ def main():
         dist.barrier()
     wall = time.perf_counter() - t0
     kern_ms = e0.elapsed_time(e1) / args.steps  # one launch per step
+    # Per-launch spread (median, p10 / p90), measured after the timed region: one event
+    # pair around each of up to 200 extra steps, so the timed loop above carries no per-step events.
+    n_dist = min(args.steps, 200)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n_dist)]
+    for t, (a, b) in enumerate(evs):
+        a.record(stream)
+        step(t)
+        b.record(stream)
+    torch.cuda.synchronize()
+    per = np.sort(np.array([a.elapsed_time(b) for a, b in evs])) if n_dist else np.zeros(1)
+    pct = {q: round(float(np.percentile(per, q)), 5) for q in (10, 50, 90)}
     tot = evam.streams.reduce_run(wall, n * args.steps, alg_bytes * args.steps,
                                   device=device if world > 1 and backend == "nccl" else None)
     wall_max = tot.elapsed_max_s
@@ -275,7 +286,8 @@ def main():
                        "parallelism": f"streams s mod {world}, one process per GPU, no hot-loop collective"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "algorithmic_bytes_per_launch": alg_bytes, "mean_launch_ms": round(kern_ms, 5)},
+                         "algorithmic_bytes_per_launch": alg_bytes, "mean_launch_ms": round(kern_ms, 5),
+                         "launch_ms_p10_p50_p90": [pct[10], pct[50], pct[90]]},
         }
         if feed is not None:
             res["h2d"] = {"bytes_per_step": feed.bytes_per_batch,
