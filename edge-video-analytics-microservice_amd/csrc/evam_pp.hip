@@ -441,6 +441,36 @@ __device__ __forceinline__ void y_plus_uv(int Y, const UV3& t, int& b, int& g, i
     r = clamp255((y + t.r) >> 20);
 }
 
+// Saturating form of the same integers, two taps per register. The chroma terms carry the bias
+// 2^32 - 2^28 on top of kK*, so for S = y + term (the BT.601 sum before >> 20) the unsigned
+// saturating add y + term' is S + 2^32 - 2^28 when S < 2^28 and 0xFFFFFFFF otherwise; every term'
+// lies in [0, 2^32) (no wrap). Its high half is then floor(S / 2^16) + 61440, and one u16
+// saturating subtract of 61440 clamps it to [0, 4095], i.e. to 16 * clamp255(S >> 20) plus four
+// low bits that a mask drops. Two taps' high halves share one register (v_perm), so the clamp costs
+// a packed subtract and a mask per tap pair, and the horizontal pass D = c0*a0 + c1*a1 is one
+// v_dot2_u32_u16 that yields 16 * D, the D' vresize takes. tools/check_sat_clamp.py checks the
+// clamp against clamp255((y + term) >> 20) over all 2^24 (Y, U, V).
+typedef unsigned short evam_u16x2 __attribute__((ext_vector_type(2)));
+constexpr uint32_t kSatBias = 0xF0000000u;  // 2^32 - 2^28
+constexpr uint32_t kKBs = (uint32_t)kKB + kSatBias, kKGs = (uint32_t)kKG + kSatBias, kKRs = (uint32_t)kKR + kSatBias;
+struct UVs { uint32_t b, g, r; };
+__device__ __forceinline__ UVs uv_terms_sat(uint32_t U, uint32_t V) {
+    return UVs{__umul24(U, (uint32_t)kCUB) + kKBs,
+               (uint32_t)(__mul24((int)V, kCVG) + __mul24((int)U, kCUG)) + kKGs,
+               __umul24(V, (uint32_t)kCVR) + kKRs};
+}
+__device__ __forceinline__ uint32_t luma_term(uint32_t Y) { return __umul24(max(Y, 16u), (uint32_t)kCY); }
+// One source row, one channel: taps' sums s0 (column x0) and s1 (column x1), packed weights w = a0 | a1 << 16
+// (plain 11-bit) -> 16 * (c0 * a0 + c1 * a1).
+__device__ __forceinline__ uint32_t hpass_sat(uint32_t y0, uint32_t t0, uint32_t y1, uint32_t t1, uint32_t w) {
+    const uint32_t s0 = __builtin_elementwise_add_sat(y0, t0);
+    const uint32_t s1 = __builtin_elementwise_add_sat(y1, t1);
+    const evam_u16x2 h = __builtin_bit_cast(evam_u16x2, __builtin_amdgcn_perm(s1, s0, 0x07060302u));
+    const evam_u16x2 c = __builtin_elementwise_sub_sat(h, (evam_u16x2){61440, 61440});
+    const uint32_t c16 = __builtin_bit_cast(uint32_t, c) & 0xFFF0FFF0u;
+    return __builtin_amdgcn_udot2(__builtin_bit_cast(evam_u16x2, c16), __builtin_bit_cast(evam_u16x2, w), 0u, false);
+}
+
 template <int FMT>
 struct Chroma {  // raw chroma of one tap: NV12 packed UV (u16), I420 U and V bytes
     uint32_t u, v;
@@ -754,7 +784,8 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_staged(const SParams P) {
     // inside a slot, weights
     const int X = X0 + seg * 64 + lane;
     const bool xin = X < P.DW;
-    uint32_t lY0 = 0, lY1 = 0, lC0 = 0, lC1 = 0, wa = 0;
+    uint32_t lY0 = 0, lY1 = 0, lC0 = 0, lC1 = 0, wa = 0, wp = 0;  // wp: plain 11-bit weights a0 | a1 << 16
+    (void)wp;
     const uint32_t xo = (uint32_t)(xin ? X : 0) * (uint32_t)esz;
     const bool wave_stores = X0 + seg * 64 < P.DW;  // some lane of this wave stores (wave-uniform)
     const int rows = Y1 - Y0;
@@ -837,6 +868,27 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_staged(const SParams P) {
                 const uint8_t* sy1 = sy0 + kSlot;
                 const uint8_t* sc0 = buf + (2 * R + 2 * r) * kSlot;
                 int c[4][3];
+#ifndef EVAM_PP_NO_SAT
+                if constexpr (kYUV) {
+                    const int ya = y0 + ytab[Y].r0, yb = y0 + ytab[Y].r1;
+                    const bool share = (ya >> 1) == (yb >> 1);
+                    const uint8_t* sc1 = share ? sc0 : sc0 + kSlot;
+                    // NV12: U and V of a tap are adjacent bytes of the staged UV row; I420: same offset in
+                    // the U and V slots.
+                    const uint8_t* sv0 = FMT == kNV12 ? sc0 + 1 : sc0 + 2 * R * kSlot;
+                    const uint8_t* sv1 = FMT == kNV12 ? sc1 + 1 : sc1 + 2 * R * kSlot;
+                    const UVs tA = uv_terms_sat(sc0[lC0], sv0[lC0]);
+                    const UVs tB = uv_terms_sat(sc0[lC1], sv0[lC1]);
+                    const UVs tC = uv_terms_sat(sc1[lC0], sv1[lC0]);
+                    const UVs tD = uv_terms_sat(sc1[lC1], sv1[lC1]);
+                    const uint32_t yA = luma_term(sy0[lY0]), yB = luma_term(sy0[lY1]);
+                    const uint32_t yC = luma_term(sy1[lY0]), yD = luma_term(sy1[lY1]);
+                    v[0] = vresize(hpass_sat(yA, tA.b, yB, tB.b, wp), hpass_sat(yC, tC.b, yD, tD.b, wp), wb0, wb1);
+                    v[1] = vresize(hpass_sat(yA, tA.g, yB, tB.g, wp), hpass_sat(yC, tC.g, yD, tD.g, wp), wb0, wb1);
+                    v[2] = vresize(hpass_sat(yA, tA.r, yB, tB.r, wp), hpass_sat(yC, tC.r, yD, tD.r, wp), wb0, wb1);
+                } else
+#endif
+                {
                 if constexpr (kYUV) {
                     const int ya = y0 + ytab[Y].r0, yb = y0 + ytab[Y].r1;
                     const bool share = (ya >> 1) == (yb >> 1);
@@ -882,6 +934,7 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_staged(const SParams P) {
                     const uint32_t D1 = __umul24(c[2][ch3], a0) + __umul24(c[3][ch3], a1);
                     v[ch3] = vresize(D0, D1, wb0, wb1);
                 }
+                }
                 if (P.color_rgb) { const int tmp = v[0]; v[0] = v[2]; v[2] = tmp; }
             }
             if (!xin) continue;
@@ -913,6 +966,7 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_staged(const SParams P) {
     {
         const XTab xt = P.xtab[xin ? X : 0];
         wa = (uint32_t)xt.a0 | ((uint32_t)xt.a1 << 16);
+        wp = (wa >> 4) & 0x0FFF0FFFu;
         if (xin && wa != 0) {
             const int ca = x0 + xt.s0, cb = x0 + xt.s1;
             lY0 = (uint32_t)(ca * T::bpp - fsY);
