@@ -471,6 +471,15 @@ __device__ __forceinline__ uint32_t hpass_sat(uint32_t y0, uint32_t t0, uint32_t
     return __builtin_amdgcn_udot2(__builtin_bit_cast(evam_u16x2, c16), __builtin_bit_cast(evam_u16x2, w), 0u, false);
 }
 
+// Horizontal pass of one source row, three channels, from the two taps' luma bytes and chroma terms.
+__device__ __forceinline__ void hrow_sat(uint32_t Y0, uint32_t Y1, const UVs& tA, const UVs& tB, uint32_t w,
+                                         uint32_t (&H)[3]) {
+    const uint32_t yA = luma_term(Y0), yB = luma_term(Y1);
+    H[0] = hpass_sat(yA, tA.b, yB, tB.b, w);
+    H[1] = hpass_sat(yA, tA.g, yB, tB.g, w);
+    H[2] = hpass_sat(yA, tA.r, yB, tB.r, w);
+}
+
 template <int FMT>
 struct Chroma {  // raw chroma of one tap: NV12 packed UV (u16), I420 U and V bytes
     uint32_t u, v;
@@ -1200,6 +1209,15 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_wave(const WParams P) {
         for (int j = 0; j < PX; j++) {
             const uint32_t tY0 = lY[j] & 0xFFFF, tY1 = lY[j] >> 16;
             int c0[3], c1[3];
+#ifndef EVAM_PP_NO_SAT
+            if constexpr (kYUV) {
+                const uint32_t tC0 = lC[j] & 0xFFFF, tC1 = lC[j] >> 16;
+                const uint8_t* svv = FMT == kNV12 ? sc + 1 : sv;
+                hrow_sat(sy[tY0], sy[tY1], uv_terms_sat(sc[tC0], svv[tC0]), uv_terms_sat(sc[tC1], svv[tC1]),
+                         (wa[j] >> 4) & 0x0FFF0FFFu, H[j]);
+                continue;
+            }
+#endif
             if constexpr (kYUV) {
                 const uint32_t tC0 = lC[j] & 0xFFFF, tC1 = lC[j] >> 16;
                 Chroma<FMT> cA, cB;
@@ -1232,6 +1250,16 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_wave(const WParams P) {
         for (int j = 0; j < PX; j++) {
             const uint32_t tY0 = lY[j] & 0xFFFF, tY1 = lY[j] >> 16;
             const uint32_t tC0 = lC[j] & 0xFFFF, tC1 = lC[j] >> 16;
+#ifndef EVAM_PP_NO_SAT
+            {
+                const uint8_t* svv = FMT == kNV12 ? sc + 1 : sv;
+                const UVs sA = uv_terms_sat(sc[tC0], svv[tC0]), sB = uv_terms_sat(sc[tC1], svv[tC1]);
+                const uint32_t wp = (wa[j] >> 4) & 0x0FFF0FFFu;
+                hrow_sat(sya[tY0], sya[tY1], sA, sB, wp, HA[j]);
+                hrow_sat(syb[tY0], syb[tY1], sA, sB, wp, HB[j]);
+                continue;
+            }
+#endif
             Chroma<FMT> cA, cB;
             if constexpr (FMT == kNV12) {
                 cA.u = *reinterpret_cast<const uint16_t*>(sc + tC0);
@@ -1695,6 +1723,21 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_roi(const QParams P) {
                 const uint32_t a0 = wa[k][j] & 0xFFFF, a1 = wa[k][j] >> 16;
                 const uint32_t tY0 = lY[k][j] & 0xFFFF, tY1 = lY[k][j] >> 16;
                 int c[4][3];
+#ifndef EVAM_PP_NO_SAT
+                if constexpr (kYUV) {
+                    const uint32_t tC0 = lC[k][j] & 0xFFFF, tC1 = lC[k][j] >> 16;
+                    const uint8_t* sv0 = FMT == kNV12 ? sc0 + 1 : sc0 + 2 * R * segC;
+                    const uint8_t* sv1 = FMT == kNV12 ? sc1 + 1 : sc1 + 2 * R * segC;
+                    const uint32_t wp = (wa[k][j] >> 4) & 0x0FFF0FFFu;
+                    uint32_t H0[3], H1[3];
+                    hrow_sat(sy0[tY0], sy0[tY1], uv_terms_sat(sc0[tC0], sv0[tC0]), uv_terms_sat(sc0[tC1], sv0[tC1]), wp, H0);
+                    hrow_sat(sy1[tY0], sy1[tY1], uv_terms_sat(sc1[tC0], sv1[tC0]), uv_terms_sat(sc1[tC1], sv1[tC1]), wp, H1);
+#pragma unroll
+                    for (int ch3 = 0; ch3 < 3; ch3++) v[ch3][j] = vresize(H0[ch3], H1[ch3], wb0, wb1);
+                    if (P.color_rgb) { const int tmp = v[0][j]; v[0][j] = v[2][j]; v[2][j] = tmp; }
+                    continue;
+                }
+#endif
                 if constexpr (kYUV) {
                     const uint32_t tC0 = lC[k][j] & 0xFFFF, tC1 = lC[k][j] >> 16;
                     Chroma<FMT> cA, cB, cC, cD;

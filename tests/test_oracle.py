@@ -173,3 +173,14 @@ def test_nv12_equals_i420_same_samples(O, coracle):
     nv.planes[0][:] = 100
     b = O.np_to_bgr(nv, 0, 0, 64, 48)
     assert (b[0::2, 0::2] == b[1::2, 1::2]).all() and (b[0::2, 0::2] == b[0::2, 1::2]).all()
+
+
+def test_saturating_clamp_identity():
+    """The kernels' packed saturating clamp (evam_pp.hip hpass_sat) equals clamp255(S >> 20) on all (Y, U, V)."""
+    import importlib.util
+    import os
+    spec = importlib.util.spec_from_file_location(
+        "check_sat_clamp", os.path.join(os.path.dirname(__file__), "..", "tools", "check_sat_clamp.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    assert mod.check() == 0
