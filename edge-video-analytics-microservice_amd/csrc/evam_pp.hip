@@ -204,6 +204,12 @@ __device__ __forceinline__ uint32_t mulhi_u24(uint32_t a, uint32_t b) {
 __device__ __forceinline__ int vresize(uint32_t D0s, uint32_t D1s, uint32_t b0s, uint32_t b1s) {
     return (int)((mulhi_u24(b0s, D0s & 0xFFFF00u) + mulhi_u24(b1s, D1s & 0xFFFF00u) + 2u) >> 2);
 }
+// Same, for OUT == 1 returned as 4 * result (the byte offset into a float LUT section).
+template <int OUT>
+__device__ __forceinline__ uint32_t vfinal(uint32_t D0s, uint32_t D1s, uint32_t b0s, uint32_t b1s) {
+    const uint32_t x = mulhi_u24(b0s, D0s & 0xFFFF00u) + mulhi_u24(b1s, D1s & 0xFFFF00u) + 2u;
+    return OUT == 1 ? (x & ~3u) : (x >> 2);
+}
 
 template <int FMT>
 struct FmtTraits {
@@ -764,12 +770,16 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_staged(const SParams P) {
     const __amdgpu_buffer_rsrc_t rsY = __builtin_amdgcn_make_buffer_rsrc((void*)p0, (short)0, 0x7FFFFFFF, 0x00020000);
     const __amdgpu_buffer_rsrc_t rsC = __builtin_amdgcn_make_buffer_rsrc((void*)(p1 ? p1 : p0), (short)0, 0x7FFFFFFF, 0x00020000);
     const __amdgpu_buffer_rsrc_t rsV = __builtin_amdgcn_make_buffer_rsrc((void*)(p2 ? p2 : p0), (short)0, 0x7FFFFFFF, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rsD0 = __builtin_amdgcn_make_buffer_rsrc((void*)d0, (short)0, 0x7FFFFFFF, 0x00020000);
+    // plane of source channel 0 / 2 (B / R): swapped for RGB order
+    const __amdgpu_buffer_rsrc_t rsD0 = __builtin_amdgcn_make_buffer_rsrc((void*)(P.color_rgb ? d2 : d0), (short)0, 0x7FFFFFFF, 0x00020000);
     const __amdgpu_buffer_rsrc_t rsD1 = __builtin_amdgcn_make_buffer_rsrc((void*)d1, (short)0, 0x7FFFFFFF, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rsD2 = __builtin_amdgcn_make_buffer_rsrc((void*)d2, (short)0, 0x7FFFFFFF, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsD2 = __builtin_amdgcn_make_buffer_rsrc((void*)(P.color_rgb ? d0 : d2), (short)0, 0x7FFFFFFF, 0x00020000);
 
     float* lut_s = reinterpret_cast<float*>(smem);
-    const int f0 = P.fill & 0xFF, f1 = (P.fill >> 8) & 0xFF, f2 = (P.fill >> 16) & 0xFF;
+    // fill in source channel order (P.fill is in output plane order); fp32: LUT byte offsets
+    const uint32_t fq0 = P.fill & 0xFF, fq1 = (P.fill >> 8) & 0xFF, fq2 = (P.fill >> 16) & 0xFF;
+    const uint32_t fsh = OUT == 1 ? 2 : 0;
+    const uint32_t fillv[3] = {(P.color_rgb ? fq2 : fq0) << fsh, fq1 << fsh, (P.color_rgb ? fq0 : fq2) << fsh};
 
     const int X0 = tx * TW, Y0 = ty * P.TH, Y1 = min(Y0 + P.TH, P.DH);
     const int seg = wave % NSEGX, rph = wave / NSEGX;
@@ -859,6 +869,10 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_staged(const SParams P) {
     };
 
     // ---- convert + resize + normalise + store the rows of group g owned by this wave ----
+    // Channel routing: v[c] holds source channel c (B, G, R). It is stored to output plane c, or 2 - c for
+    // RGB order, through swapped plane resources; the LDS LUT is loaded with its sections in source
+    // channel order (prologue), so the per-pixel path carries no swap. For fp32 output the vertical
+    // pass yields 4 * v, the LUT byte offset, directly ((x + 2) & ~3 instead of (x + 2) >> 2).
     auto compute = [&](int g, const uint8_t* buf) {
 #pragma unroll
         for (int k = 0; k < RPW; k++) {
@@ -867,99 +881,98 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_staged(const SParams P) {
             if (Y >= Y1) continue;
             const int b0 = ytab[Y].b0, b1 = ytab[Y].b1;
             const int sO = (int)((uint32_t)(Y * P.DW) * (uint32_t)esz);
-            int v[3];
-            if ((b0 | b1) == 0 || wa == 0 || (P.ablate & 2)) {  // padding row / column
-                v[0] = f0; v[1] = f1; v[2] = f2;
-            } else {
-                const uint32_t a0 = wa & 0xFFFF, a1 = wa >> 16;  // 15-bit
-                const uint32_t wb0 = (uint32_t)b0, wb1 = (uint32_t)b1;
-                const uint8_t* sy0 = buf + (2 * r) * kSlot;
-                const uint8_t* sy1 = sy0 + kSlot;
-                const uint8_t* sc0 = buf + (2 * R + 2 * r) * kSlot;
-                int c[4][3];
-#ifndef EVAM_PP_NO_SAT
-                if constexpr (kYUV) {
-                    const int ya = y0 + ytab[Y].r0, yb = y0 + ytab[Y].r1;
-                    const bool share = (ya >> 1) == (yb >> 1);
-                    const uint8_t* sc1 = share ? sc0 : sc0 + kSlot;
-                    // NV12: U and V of a tap are adjacent bytes of the staged UV row; I420: same offset in
-                    // the U and V slots.
-                    const uint8_t* sv0 = FMT == kNV12 ? sc0 + 1 : sc0 + 2 * R * kSlot;
-                    const uint8_t* sv1 = FMT == kNV12 ? sc1 + 1 : sc1 + 2 * R * kSlot;
-                    const UVs tA = uv_terms_sat(sc0[lC0], sv0[lC0]);
-                    const UVs tB = uv_terms_sat(sc0[lC1], sv0[lC1]);
-                    const UVs tC = uv_terms_sat(sc1[lC0], sv1[lC0]);
-                    const UVs tD = uv_terms_sat(sc1[lC1], sv1[lC1]);
-                    const uint32_t yA = luma_term(sy0[lY0]), yB = luma_term(sy0[lY1]);
-                    const uint32_t yC = luma_term(sy1[lY0]), yD = luma_term(sy1[lY1]);
-                    v[0] = vresize(hpass_sat(yA, tA.b, yB, tB.b, wp), hpass_sat(yC, tC.b, yD, tD.b, wp), wb0, wb1);
-                    v[1] = vresize(hpass_sat(yA, tA.g, yB, tB.g, wp), hpass_sat(yC, tC.g, yD, tD.g, wp), wb0, wb1);
-                    v[2] = vresize(hpass_sat(yA, tA.r, yB, tB.r, wp), hpass_sat(yC, tC.r, yD, tD.r, wp), wb0, wb1);
-                } else
-#endif
-                {
-                if constexpr (kYUV) {
-                    const int ya = y0 + ytab[Y].r0, yb = y0 + ytab[Y].r1;
-                    const bool share = (ya >> 1) == (yb >> 1);
-                    const uint8_t* sc1 = share ? sc0 : sc0 + kSlot;
-                    Chroma<FMT> cA, cB, cC, cD;
-                    if constexpr (FMT == kNV12) {
-                        cA.u = *reinterpret_cast<const uint16_t*>(sc0 + lC0);
-                        cB.u = *reinterpret_cast<const uint16_t*>(sc0 + lC1);
-                        cC.u = *reinterpret_cast<const uint16_t*>(sc1 + lC0);
-                        cD.u = *reinterpret_cast<const uint16_t*>(sc1 + lC1);
-                    } else {
-                        const uint8_t* sv0 = sc0 + 2 * R * kSlot;
-                        const uint8_t* sv1 = sc1 + 2 * R * kSlot;
-                        cA.u = sc0[lC0]; cA.v = sv0[lC0];
-                        cB.u = sc0[lC1]; cB.v = sv0[lC1];
-                        cC.u = sc1[lC0]; cC.v = sv1[lC0];
-                        cD.u = sc1[lC1]; cD.v = sv1[lC1];
-                    }
-                    const UV3 tA = chroma_terms<FMT>(cA);
-                    const UV3 tB = chroma_terms<FMT>(cB);
-                    const UV3 tC = chroma_terms<FMT>(cC);
-                    const UV3 tD = chroma_terms<FMT>(cD);
-                    y_plus_uv((int)sy0[lY0], tA, c[0][0], c[0][1], c[0][2]);
-                    y_plus_uv((int)sy0[lY1], tB, c[1][0], c[1][1], c[1][2]);
-                    y_plus_uv((int)sy1[lY0], tC, c[2][0], c[2][1], c[2][2]);
-                    y_plus_uv((int)sy1[lY1], tD, c[3][0], c[3][1], c[3][2]);
-                } else {
-                    const uint8_t* rowp[2] = {sy0, sy1};
-#pragma unroll
-                    for (int q = 0; q < 4; q++) {
-                        const uint8_t* sp = rowp[q >> 1] + ((q & 1) ? lY1 : lY0);
-                        if constexpr (FMT == kBGRX) {
-                            const uint32_t px = *reinterpret_cast<const uint32_t*>(sp);
-                            c[q][0] = px & 0xFF; c[q][1] = (px >> 8) & 0xFF; c[q][2] = (px >> 16) & 0xFF;
-                        } else {
-                            c[q][0] = sp[0]; c[q][1] = sp[1]; c[q][2] = sp[2];
-                        }
-                    }
-                }
-#pragma unroll
-                for (int ch3 = 0; ch3 < 3; ch3++) {
-                    const uint32_t D0 = __umul24(c[0][ch3], a0) + __umul24(c[1][ch3], a1);
-                    const uint32_t D1 = __umul24(c[2][ch3], a0) + __umul24(c[3][ch3], a1);
-                    v[ch3] = vresize(D0, D1, wb0, wb1);
-                }
-                }
-                if (P.color_rgb) { const int tmp = v[0]; v[0] = v[2]; v[2] = tmp; }
-            }
             if (!xin) continue;
-            if (P.ablate & 4) {
-                asm volatile("" :: "v"(v[0]), "v"(v[1]), "v"(v[2]));
+            auto put = [&](const uint32_t (&v)[3]) {
+                if (P.ablate & 4) {
+                    asm volatile("" :: "v"(v[0]), "v"(v[1]), "v"(v[2]));
+                    return;
+                }
+                if constexpr (OUT == 1) {
+                    const uint8_t* lb = reinterpret_cast<const uint8_t*>(lut_s);
+                    __builtin_amdgcn_raw_buffer_store_b32(*reinterpret_cast<const uint32_t*>(lb + v[0]), rsD0, xo, sO, 0);
+                    __builtin_amdgcn_raw_buffer_store_b32(*reinterpret_cast<const uint32_t*>(lb + 1024 + v[1]), rsD1, xo, sO, 0);
+                    __builtin_amdgcn_raw_buffer_store_b32(*reinterpret_cast<const uint32_t*>(lb + 2048 + v[2]), rsD2, xo, sO, 0);
+                } else {
+                    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v[0], rsD0, xo, sO, 0);
+                    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v[1], rsD1, xo, sO, 0);
+                    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v[2], rsD2, xo, sO, 0);
+                }
+            };
+            if ((b0 | b1) == 0 || wa == 0 || (P.ablate & 2)) {  // padding row / column
+                put(fillv);
                 continue;
             }
-            if constexpr (OUT == 1) {
-                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lut_s[v[0]]), rsD0, xo, sO, 0);
-                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lut_s[256 + v[1]]), rsD1, xo, sO, 0);
-                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lut_s[512 + v[2]]), rsD2, xo, sO, 0);
-            } else {
-                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v[0], rsD0, xo, sO, 0);
-                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v[1], rsD1, xo, sO, 0);
-                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v[2], rsD2, xo, sO, 0);
+            const uint32_t wb0 = (uint32_t)b0, wb1 = (uint32_t)b1;
+            const uint8_t* sy0 = buf + (2 * r) * kSlot;
+            const uint8_t* sy1 = sy0 + kSlot;
+            const uint8_t* sc0 = buf + (2 * R + 2 * r) * kSlot;
+            uint32_t v[3];
+#ifndef EVAM_PP_NO_SAT
+            if constexpr (kYUV) {
+                const int ya = y0 + ytab[Y].r0, yb = y0 + ytab[Y].r1;
+                const bool share = (ya >> 1) == (yb >> 1);
+                const uint8_t* sc1 = share ? sc0 : sc0 + kSlot;
+                // NV12: U and V of a tap are adjacent bytes of the staged UV row; I420: same offset in the
+                // U and V slots.
+                const uint8_t* sv0 = FMT == kNV12 ? sc0 + 1 : sc0 + 2 * R * kSlot;
+                const uint8_t* sv1 = FMT == kNV12 ? sc1 + 1 : sc1 + 2 * R * kSlot;
+                const UVs tA = uv_terms_sat(sc0[lC0], sv0[lC0]);
+                const UVs tB = uv_terms_sat(sc0[lC1], sv0[lC1]);
+                const UVs tC = uv_terms_sat(sc1[lC0], sv1[lC0]);
+                const UVs tD = uv_terms_sat(sc1[lC1], sv1[lC1]);
+                const uint32_t yA = luma_term(sy0[lY0]), yB = luma_term(sy0[lY1]);
+                const uint32_t yC = luma_term(sy1[lY0]), yD = luma_term(sy1[lY1]);
+                v[0] = vfinal<OUT>(hpass_sat(yA, tA.b, yB, tB.b, wp), hpass_sat(yC, tC.b, yD, tD.b, wp), wb0, wb1);
+                v[1] = vfinal<OUT>(hpass_sat(yA, tA.g, yB, tB.g, wp), hpass_sat(yC, tC.g, yD, tD.g, wp), wb0, wb1);
+                v[2] = vfinal<OUT>(hpass_sat(yA, tA.r, yB, tB.r, wp), hpass_sat(yC, tC.r, yD, tD.r, wp), wb0, wb1);
+                put(v);
+                continue;
             }
+#endif
+            const uint32_t a0 = wa & 0xFFFF, a1 = wa >> 16;  // 15-bit
+            int c[4][3];
+            if constexpr (kYUV) {
+                const int ya = y0 + ytab[Y].r0, yb = y0 + ytab[Y].r1;
+                const bool share = (ya >> 1) == (yb >> 1);
+                const uint8_t* sc1 = share ? sc0 : sc0 + kSlot;
+                Chroma<FMT> cA, cB, cC, cD;
+                if constexpr (FMT == kNV12) {
+                    cA.u = *reinterpret_cast<const uint16_t*>(sc0 + lC0);
+                    cB.u = *reinterpret_cast<const uint16_t*>(sc0 + lC1);
+                    cC.u = *reinterpret_cast<const uint16_t*>(sc1 + lC0);
+                    cD.u = *reinterpret_cast<const uint16_t*>(sc1 + lC1);
+                } else {
+                    const uint8_t* sv0 = sc0 + 2 * R * kSlot;
+                    const uint8_t* sv1 = sc1 + 2 * R * kSlot;
+                    cA.u = sc0[lC0]; cA.v = sv0[lC0];
+                    cB.u = sc0[lC1]; cB.v = sv0[lC1];
+                    cC.u = sc1[lC0]; cC.v = sv1[lC0];
+                    cD.u = sc1[lC1]; cD.v = sv1[lC1];
+                }
+                y_plus_uv((int)sy0[lY0], chroma_terms<FMT>(cA), c[0][0], c[0][1], c[0][2]);
+                y_plus_uv((int)sy0[lY1], chroma_terms<FMT>(cB), c[1][0], c[1][1], c[1][2]);
+                y_plus_uv((int)sy1[lY0], chroma_terms<FMT>(cC), c[2][0], c[2][1], c[2][2]);
+                y_plus_uv((int)sy1[lY1], chroma_terms<FMT>(cD), c[3][0], c[3][1], c[3][2]);
+            } else {
+                const uint8_t* rowp[2] = {sy0, sy1};
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const uint8_t* sp = rowp[q >> 1] + ((q & 1) ? lY1 : lY0);
+                    if constexpr (FMT == kBGRX) {
+                        const uint32_t px = *reinterpret_cast<const uint32_t*>(sp);
+                        c[q][0] = px & 0xFF; c[q][1] = (px >> 8) & 0xFF; c[q][2] = (px >> 16) & 0xFF;
+                    } else {
+                        c[q][0] = sp[0]; c[q][1] = sp[1]; c[q][2] = sp[2];
+                    }
+                }
+            }
+#pragma unroll
+            for (int ch3 = 0; ch3 < 3; ch3++) {
+                const uint32_t D0 = __umul24(c[0][ch3], a0) + __umul24(c[1][ch3], a1);
+                const uint32_t D1 = __umul24(c[2][ch3], a0) + __umul24(c[3][ch3], a1);
+                v[ch3] = vfinal<OUT>(D0, D1, wb0, wb1);
+            }
+            put(v);
         }
     };
 
@@ -969,8 +982,8 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_staged(const SParams P) {
     // latencies overlap instead of adding up.
     issue(0, buf0);
     asm volatile("" ::: "memory");
-    if constexpr (OUT == 1) {
-        for (int i = tid; i < 768; i += kThreads) lut_s[i] = P.lut[i];
+    if constexpr (OUT == 1) {  // sections in source channel order (B, G, R): see compute
+        for (int i = tid; i < 768; i += kThreads) lut_s[i] = P.lut[P.color_rgb ? 512 - (i & ~255) + (i & 255) : i];
     }
     {
         const XTab xt = P.xtab[xin ? X : 0];
