@@ -1576,28 +1576,19 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_roi(const QParams P) {
     const __amdgpu_buffer_rsrc_t rsD1 = __builtin_amdgcn_make_buffer_rsrc((void*)d1, (short)0, 0x7FFFFFFF, 0x00020000);
     const __amdgpu_buffer_rsrc_t rsD2 = __builtin_amdgcn_make_buffer_rsrc((void*)d2, (short)0, 0x7FFFFFFF, 0x00020000);
 
+    // Prologue order: the LUT loads go out first; the row table is built while they are in flight;
+    // group 0's DMA (it needs only the row table and the analytic footprint) goes out before the column
+    // table and the per-lane setup are built, so its latency overlaps them.
     float* lut_s = reinterpret_cast<float*>(smem);
+    float lutv[3] = {0.f, 0.f, 0.f};
     if constexpr (OUT == 1) {
-        for (int i = tid; i < 768; i += kThreads) lut_s[i] = P.lut[i];
+#pragma unroll
+        for (int k = 0; k < 3; k++) lutv[k] = P.lut[tid + k * kThreads];  // 768 = 3 x kThreads
     }
     XTab* xt = reinterpret_cast<XTab*>(smem + P.offXT);
     YTab* yt = reinterpret_cast<YTab*>(smem + P.offYT);
     const int DW = P.DW;
     const int Y0 = ty * P.TH, Y1 = min(Y0 + P.TH, P.DH), rows = Y1 - Y0;
-    for (int X = tid; X < DW; X += kThreads) {
-        XTab e;
-        e.s0 = 0; e.s1 = 0; e.a0 = 0; e.a1 = 0; e.pad = 0;
-        const int dx = X - ox;
-        if (dx >= 0 && dx < rw) {
-            int sx, a0, a1;
-            linear_coef(dx, scx, cw, true, sx, a0, a1);
-            e.s0 = sx;
-            e.s1 = min(sx + 1, cw - 1);
-            e.a0 = (uint16_t)(a0 << 4);
-            e.a1 = (uint16_t)(a1 << 4);
-        }
-        xt[X] = e;
-    }
     for (int ly = tid; ly < rows; ly += kThreads) {
         YTab e;
         e.r0 = 0; e.r1 = 0; e.b0 = 0; e.b1 = 0;
@@ -1641,41 +1632,11 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_roi(const QParams P) {
     // q / n for q < 2^16 by one mul_hi: m = ceil(2^32 / n) is exact there (n = 1: the identity).
     const uint32_t mY = nY > 1 ? (uint32_t)((0x100000000ull + nY - 1) / nY) : 0u;
     const uint32_t mC = nC > 1 ? (uint32_t)((0x100000000ull + nC - 1) / nC) : 0u;
-    __syncthreads();
-
-    const int f0 = P.fill & 0xFF, f1 = (P.fill >> 8) & 0xFF, f2 = (P.fill >> 16) & 0xFF;
-    // Per-lane state for quad steps k < K, identical for every group: row of the quad inside the
-    // group; per pixel packed LDS tap offsets (tap 0 low, tap 1 high half) and horizontal weights.
-    uint32_t lY[KQ][PX], lC[KQ][PX], wa[KQ][PX];
-    int rr[KQ];
+    if constexpr (OUT == 1) {
 #pragma unroll
-    for (int k = 0; k < KQ; k++) {
-        const int q = tid + k * kThreads;
-        const bool v = k < K && q < nq;
-        const int r = v ? q / QW : 0;
-        const int c0 = v ? (q - r * QW) * PX : 0;
-        rr[k] = v ? r : -1;
-#pragma unroll
-        for (int j = 0; j < PX; j++) {
-            const XTab e = xt[c0 + j];
-            wa[k][j] = (uint32_t)e.a0 | ((uint32_t)e.a1 << 16);
-            lY[k][j] = lC[k][j] = 0;
-            if (v && wa[k][j] != 0) {
-                const int ca = x0 + e.s0, cb = x0 + e.s1;
-                lY[k][j] = (uint32_t)(ca * T::bpp - fsY) | ((uint32_t)(cb * T::bpp - fsY) << 16);
-                if constexpr (FMT == kNV12)
-                    lC[k][j] = (uint32_t)(2 * (ca >> 1) - fsC) | ((uint32_t)(2 * (cb >> 1) - fsC) << 16);
-                else if constexpr (FMT == kI420)
-                    lC[k][j] = (uint32_t)((ca >> 1) - fsC) | ((uint32_t)((cb >> 1) - fsC) << 16);
-            }
-        }
+        for (int k = 0; k < 3; k++) lut_s[tid + k * kThreads] = lutv[k];
     }
-    const int ngroups = (rows + R - 1) / R;
-    if ((P.ablate & 32) && ngroups != -7) {
-        asm volatile("" :: "v"(lY[0][0]), "v"(lC[0][0]), "v"(wa[0][0]), "v"(rr[0]), "s"(mY), "s"(mC));
-        return;
-    }
-
+    __syncthreads();  // row table visible to the DMA issue
     // One plane region of group grp: chunk q -> (segment, chunk) -> (row, tap) -> source offset.
     auto issue_plane = [&](int grp, uint8_t* base, int nr, int n, uint32_t m, int pl) {
         const int nq = 2 * nr * n;
@@ -1707,6 +1668,57 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_roi(const QParams P) {
         if constexpr (NP >= 2) issue_plane(grp, buf + offC, nr, nC, mC, 1);
         if constexpr (NP >= 3) issue_plane(grp, buf + offC + 2 * R * segC, nr, nC, mC, 2);
     };
+    uint8_t* const buf0 = smem + P.offBuf;
+    uint8_t* const buf1 = buf0 + P.buf_bytes;
+    issue(0, buf0);
+    for (int X = tid; X < DW; X += kThreads) {
+        XTab e;
+        e.s0 = 0; e.s1 = 0; e.a0 = 0; e.a1 = 0; e.pad = 0;
+        const int dx = X - ox;
+        if (dx >= 0 && dx < rw) {
+            int sx, a0, a1;
+            linear_coef(dx, scx, cw, true, sx, a0, a1);
+            e.s0 = sx;
+            e.s1 = min(sx + 1, cw - 1);
+            e.a0 = (uint16_t)(a0 << 4);
+            e.a1 = (uint16_t)(a1 << 4);
+        }
+        xt[X] = e;
+    }
+    __syncthreads();  // column table visible to the per-lane setup
+    const int f0 = P.fill & 0xFF, f1 = (P.fill >> 8) & 0xFF, f2 = (P.fill >> 16) & 0xFF;
+    // Per-lane state for quad steps k < K, identical for every group: row of the quad inside the
+    // group; per pixel packed LDS tap offsets (tap 0 low, tap 1 high half) and horizontal weights.
+    uint32_t lY[KQ][PX], lC[KQ][PX], wa[KQ][PX];
+    int rr[KQ];
+#pragma unroll
+    for (int k = 0; k < KQ; k++) {
+        const int q = tid + k * kThreads;
+        const bool v = k < K && q < nq;
+        const int r = v ? q / QW : 0;
+        const int c0 = v ? (q - r * QW) * PX : 0;
+        rr[k] = v ? r : -1;
+#pragma unroll
+        for (int j = 0; j < PX; j++) {
+            const XTab e = xt[c0 + j];
+            wa[k][j] = (uint32_t)e.a0 | ((uint32_t)e.a1 << 16);
+            lY[k][j] = lC[k][j] = 0;
+            if (v && wa[k][j] != 0) {
+                const int ca = x0 + e.s0, cb = x0 + e.s1;
+                lY[k][j] = (uint32_t)(ca * T::bpp - fsY) | ((uint32_t)(cb * T::bpp - fsY) << 16);
+                if constexpr (FMT == kNV12)
+                    lC[k][j] = (uint32_t)(2 * (ca >> 1) - fsC) | ((uint32_t)(2 * (cb >> 1) - fsC) << 16);
+                else if constexpr (FMT == kI420)
+                    lC[k][j] = (uint32_t)((ca >> 1) - fsC) | ((uint32_t)((cb >> 1) - fsC) << 16);
+            }
+        }
+    }
+    const int ngroups = (rows + R - 1) / R;
+    if ((P.ablate & 32) && ngroups != -7) {
+        asm volatile("" :: "v"(lY[0][0]), "v"(lC[0][0]), "v"(wa[0][0]), "v"(rr[0]), "s"(mY), "s"(mC));
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // group 0's DMA lands before the LDS is released
+        return;
+    }
 
     auto compute = [&](int grp, const uint8_t* buf) {
         const uint32_t gbase = (uint32_t)((Y0 + grp * R) * DW);
@@ -1804,9 +1816,7 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_roi(const QParams P) {
         }
     };
 
-    uint8_t* const buf0 = smem + P.offBuf;
-    uint8_t* const buf1 = buf0 + P.buf_bytes;
-    issue(0, buf0);
+
     for (int grp = 0; grp < ngroups; grp++) {
         // Wait for this wave's share of group grp's DMA. Group grp-1 was full (only the last group can
         // be partial), so this wave issued at least 3 stores for each of its nk_w store steps after
