@@ -2793,7 +2793,8 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
                 sp.tiles_x = (DW + tw - 1) / tw;
                 // ~4096 pixels per workgroup, but short enough tiles that small batches still put
                 // 8 workgroups on every CU (a whole clip-ring step is only 32 x 224 x 224 pixels).
-                int th = std::max(kStageRows, 4096 / tw);
+                // At most 16 rows: C4 (tw 128) runs 3-7 % faster at 16 than at 32 (profiles/r01ad_sweep_th*.txt).
+                int th = std::max(kStageRows, std::min(16, 4096 / tw));
                 const int64_t cols = (int64_t)count[f] * sp.tiles_x;
                 const int64_t want = 8 * (int64_t)h->n_cu;
                 if (cols * ((DH + th - 1) / th) < want) th = (int)std::max<int64_t>(kStageRows, cols * DH / want);
