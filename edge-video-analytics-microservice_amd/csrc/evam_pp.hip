@@ -150,7 +150,16 @@ struct SParams {
     int color_rgb;
     uint32_t fill;
     int ablate;
+    int xcd_remap;       // 1: consecutive tiles land on one XCD (shared halo rows stay in one L2)
 };
+
+// Workgroups are dispatched round-robin over the 8 XCDs (block b runs on XCD b % 8). Remap so each
+// XCD walks a contiguous run of tiles: neighbouring tiles of one frame share source rows at their
+// edges, and those rows then hit the same L2. Bijective for any grid size.
+__device__ inline int xcd_tile(int b, int grid) {
+    const int q = grid >> 3, r = grid & 7, x = b & 7, i = b >> 3;
+    return x < r ? x * (q + 1) + i : r * (q + 1) + (x - r) * q + i;
+}
 
 // ------------------------------------------------------------------------------------------------
 // exact OpenCV arithmetic (shared host/device)
@@ -748,7 +757,7 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_staged(const SParams P) {
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int t = blockIdx.x;
+    const int t = P.xcd_remap ? xcd_tile(blockIdx.x, gridDim.x) : (int)blockIdx.x;
     const int item = t / P.tiles_per_item;
     const int tile = t - item * P.tiles_per_item;
     const int ty = tile / P.tiles_x;
@@ -2807,6 +2816,9 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
                 sp.color_rgb = color_rgb;
                 sp.fill = fill;
                 sp.ablate = env_int("EVAM_PP_ABLATE", 0);
+                // XCD-contiguous tiles: C2 -1.4 %, C4 -3 % kernel time; a grid of one workgroup round or
+                // less (C5) gains nothing (profiles/r01ae_sweep_xcd.txt). EVAM_PP_XCD=0/1 forces it.
+                sp.xcd_remap = env_int("EVAM_PP_XCD", (int)(count[f] * (int64_t)sp.tiles_per_item >= 8 * (int64_t)h->n_cu));
                 const int64_t grid = (int64_t)count[f] * sp.tiles_per_item;
                 if (grid > 0x7FFFFFFF) return fail(EVAM_PP_ERR_INVALID_ARG, "evam_pp_run: too many tiles");
                 const int lds = sp.offBuf + 2 * sp.buf_bytes;
