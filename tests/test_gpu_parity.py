@@ -361,16 +361,17 @@ def test_stats_and_timing(evam, O, gpu):
     ((300, 180), (131, 97), "aspect-ratio"),        # odd DW -> PX 1, letterbox
     ((480, 270), (224, 224), "aspect-crop"),        # C5 shape: central crop
 ])
-@pytest.mark.parametrize("variant", ["auto", "wave", "px1", "px2", "noreuse", "staged"])
+@pytest.mark.parametrize("variant", ["auto", "wave", "px1", "px2", "noreuse", "staged", "staged_xcd"])
 def test_wave_kernel_variants(evam, O, coracle, gpu, fmt, src, dst, resize, variant, monkeypatch):
     """Uniform-geometry batches through the default kernel choice, the wave-row kernel forced
-    (EVAM_PP_WAVE=2; every PX / REUSE choice) and the staged kernel (EVAM_PP_WAVE=0), RGB order, fp32
+    (EVAM_PP_WAVE=2; every PX / REUSE choice) and the staged kernel (EVAM_PP_WAVE=0; with the
+    XCD-contiguous tile order forced on small, non-multiple-of-8 grids: EVAM_PP_XCD=1), RGB order, fp32
     with normalisation and u8."""
     import torch
 
     env = {"wave": {"EVAM_PP_WAVE": "2"}, "px1": {"EVAM_PP_WAVE": "2", "EVAM_PP_PX": "1"},
            "px2": {"EVAM_PP_WAVE": "2", "EVAM_PP_PX": "2"}, "noreuse": {"EVAM_PP_WAVE": "2", "EVAM_PP_REUSE": "0"},
-           "staged": {"EVAM_PP_WAVE": "0"}}.get(variant, {})
+           "staged": {"EVAM_PP_WAVE": "0"}, "staged_xcd": {"EVAM_PP_WAVE": "0", "EVAM_PP_XCD": "1"}}.get(variant, {})
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     if variant == "px2" and dst[0] % 2:
