@@ -2293,6 +2293,7 @@ struct evam_pp {
     float lut[768];
     std::vector<int> sc_fmt;       // per-call scratch, kept to avoid reallocation
     std::vector<int> sc_bucket;
+    std::vector<int> sc_order;
     std::vector<Geom> sc_geo;
 };
 
@@ -2695,6 +2696,7 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
         // bytes, crop width x touched rows). Workgroups are dispatched in order as slots free, so
         // the long ROIs start first and the short ones fill the tail.
         const bool sort = env_int("EVAM_PP_ROI_SORT", 1) != 0;
+        const bool xcd_group = env_int("EVAM_PP_ROI_XCD", 0) != 0;
         std::vector<int>& bucket = h->sc_bucket;
         bucket.resize(n_items);
         for (int f = 0; f < 4; f++) {
@@ -2715,9 +2717,28 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
                 start[bucket[i] + 1]++;
             }
             for (int b = 0; b < 64; b++) start[b + 1] += start[b];
-            for (int i = 0; i < n_items; i++) {
-                if (fmt[i] != f) continue;
-                RoiRec& r = rr[start[bucket[i]]++];
+            std::vector<int>& ord = h->sc_order;
+            ord.assign(start[64], 0);
+            for (int i = 0; i < n_items; i++)
+                if (fmt[i] == f) ord[start[bucket[i]]++] = i;
+            if (xcd_group) {
+                // Record p runs on XCD p % 8: deal each frame's ROIs (frame s -> XCD s % 8, largest
+                // first within the XCD) so overlapping crops of one frame share one L2.
+                std::vector<int> q[8];
+                for (int i : ord) q[(items ? items[i].src_index : i) & 7].push_back(i);
+                size_t head[8] = {0};
+                for (size_t p = 0; p < ord.size(); p++) {
+                    int x = (int)(p & 7);
+                    if (head[x] == q[x].size())  // this XCD's frames are done: take the largest head left
+                        for (int y = 0, best = -1; y < 8; y++)
+                            if (head[y] < q[y].size() &&
+                                (best < 0 || bucket[q[y][head[y]]] < bucket[q[best][head[best]]])) x = best = y;
+                    ord[p] = q[x][head[x]++];
+                }
+            }
+            for (size_t p = 0; p < ord.size(); p++) {
+                const int i = ord[p];
+                RoiRec& r = rr[p];
                 const evam_image& sim = srcs[items ? items[i].src_index : i];
                 r.plane[0] = sim.planes[0]; r.plane[1] = sim.planes[1]; r.plane[2] = sim.planes[2];
                 r.pitch[0] = sim.pitch[0]; r.pitch[1] = sim.pitch[1]; r.pitch[2] = sim.pitch[2];

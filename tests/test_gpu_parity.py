@@ -446,3 +446,23 @@ def test_roi_kernel_px4(evam, O, coracle, gpu, fmt, dst, dtype, monkeypatch):
                      torch.float32 if dtype == "f32" else torch.uint8, info, rois=[evam.Roi(*r) for r in rois])
     ref, _ = run_oracle(O, coracle, frames, shape, dtype, info, rois=rois)
     assert_same(got, ref, f"roi px4 {fmt} {dst} {dtype}")
+
+
+@pytest.mark.parametrize("fmt", FORMATS)
+def test_roi_kernel_xcd_order(evam, O, coracle, gpu, fmt, monkeypatch):
+    """ROI records dealt to XCDs by source frame (EVAM_PP_ROI_XCD=1), more frames than XCDs."""
+    import torch
+
+    monkeypatch.setenv("EVAM_PP_ROI_XCD", "1")
+    rng = np.random.default_rng(zlib.crc32(f"xcd{fmt}".encode()))
+    W, H = 192, 108
+    frames = [O.random_frame(rng, fc(O, fmt), W, H, pattern="gradient" if i % 2 else "uniform") for i in range(11)]
+    rois = [(int(rng.integers(0, 11)), int(rng.integers(0, W - 8)), int(rng.integers(0, H - 8)),
+             int(rng.integers(4, 120)), int(rng.integers(4, 90))) for _ in range(53)]
+    info = evam.PreProcInfo(resize="aspect-ratio", placement="center", fill=(1, 2, 3),
+                            range=(0.0, 1.0), mean=(0.1, 0.2, 0.3), std=(0.3, 0.2, 0.1))
+    shape = (len(rois), 3, 40, 40)
+    got, _ = run_hip(evam, torch, upload(evam, frames, gpu), shape, torch.float32, info,
+                     rois=[evam.Roi(*r) for r in rois])
+    ref, _ = run_oracle(O, coracle, frames, shape, "f32", info, rois=rois)
+    assert_same(got, ref, f"roi xcd order {fmt}")
