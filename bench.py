@@ -12,6 +12,12 @@ Multi-GPU: one process per GPU (torchrun); camera streams are partitioned s mod 
 own batch (weak scaling), no collective touches the hot loop; after the timed region one all_reduce(MAX)
 of the elapsed time and one all_gather of per-rank stats run over RCCL.
 
+HBM-honest by default: every step reads a different set of frames and writes a different output
+tensor, from a pool whose footprint is >= 3x the 256 MiB Infinity Cache (MI355X_MICROARCH.md: a buffer
+stays on-die only while everything touched between two of its uses fits in ~256 MiB), so the timed
+launches stream from HBM, not from the die-level cache. `--pool 1` re-reads one resident set (the
+round-1 mode); its numbers are reported as the secondary `roofline.resident` field either way.
+
 Output: ONE JSON line from rank 0 with value = frames/s over all ranks, plus `roofline` (algorithmic
 bytes per launch / mean launch time from HIP events on the launch stream) and `cpu_baseline` (the C
 oracle, OpenMP on the host cores, on a bounded sample — rank 0 at N=1 only).
@@ -34,6 +40,7 @@ METRIC = "pre-processed frames/sec (1080p NV12→512² NCHW fp32) 1–8 GPU; % H
 BGR_MEAN = (0.406, 0.456, 0.485)
 BGR_STD = (0.225, 0.224, 0.229)
 ROI_SETS = 4  # C3: distinct seeded ROI sets cycled step by step
+MALL_BYTES = 256 * 2**20  # MI355X Infinity Cache (die-level L3)
 
 WORKLOADS = {
     "c1": dict(desc="C1: 768x432 NV12 -> 512x512 u8 BGR NCHW (no normalisation)", fourcc="NV12", src=(768, 432),
@@ -89,6 +96,13 @@ def device_frames(evam, torch, wl, n, device, seed):
     return imgs
 
 
+def pool_sets(step_bytes: int, want: int) -> int:
+    """Frame / output sets cycled by the timed loop: enough that the pool is >= 3x the Infinity Cache."""
+    if want > 0:
+        return want
+    return max(1, min(64, -(-3 * MALL_BYTES // max(step_bytes, 1))))
+
+
 def cpu_baseline(wl, budget_s: float):
     """Time the C oracle (the CPU restatement, OpenMP over output rows) on the host cores."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -124,15 +138,16 @@ def cpu_baseline(wl, budget_s: float):
                       f"(oracle/evam_oracle.c, OpenMP {cores} threads) in {el:.1f} s"}
 
 
-def load_pmc_traffic(config_name: str, n_frames_per_launch: int):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary for this workload, if any."""
+def load_pmc_traffic(config_name: str, n_frames_per_launch: int, pool: int):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary of this exact workload (same frames
+    per launch and the same pool of cycled sets: a resident set's FETCH_SIZE counts Infinity-Cache hits)."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(path):
         return None
     try:
         d = json.load(open(path))
         e = d.get(config_name)
-        if e and e.get("frames_per_launch") == n_frames_per_launch:
+        if e and e.get("frames_per_launch") == n_frames_per_launch and e.get("pool_sets", 1) == pool:
             return e.get("hbm_bytes_per_launch")
     except Exception:
         return None
@@ -151,6 +166,11 @@ def main():
                     help="host: frames start in pinned host memory and cross PCIe every step (SURVEY §8 f3); "
                          "reported as a separate PCIe-inclusive line, never the headline value")
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU-baseline work")
+    ap.add_argument("--pool", type=int, default=0,
+                    help="frame/output sets cycled step by step (0: auto, >= 3x the 256 MiB Infinity Cache; "
+                         "1: one resident set)")
+    ap.add_argument("--resident-steps", type=int, default=200,
+                    help="extra steps on one resident set, reported as roofline.resident (0: skip)")
     args = ap.parse_args()
 
     import torch
@@ -180,8 +200,6 @@ def main():
     strong = args.config == "c4" and world > 1 and not args.frames
     if strong:  # C4 is a fixed set of 64 streams, partitioned s mod G (strong split)
         n = len(evam.streams.streams_for_rank(wl["frames"], world, rank))
-    imgs = device_frames(evam, torch, wl, n, device, seed=1234 + rank)
-    batch = evam.ImageBatch(imgs)
     info = make_info(evam, wl)
     DW, DH = wl["dst"]
     roi_sets = None
@@ -194,7 +212,19 @@ def main():
     ring = wl.get("ring")
     out_n = n * ring if ring else n_items
     dtype = torch.float32 if wl["dtype"] == "f32" else torch.uint8
-    out = torch.empty((out_n, 3, DH, DW), dtype=dtype, device=device)
+    esz = 4 if wl["dtype"] == "f32" else 1
+    fc = evam.preproc.FOURCC_BY_NAME[wl["fourcc"]]
+    in_bytes = n * sum(r * p for r, p in evam.plane_layout(fc, *wl["src"], pitch_align=16))
+    out_step = n_items * 3 * DH * DW * esz  # output bytes one step writes
+    # Pool: P frame sets and (full-tensor outputs) P output tensors, one of each per step, so a buffer is
+    # touched again only after the whole pool went by. The clip ring already spreads its writes over
+    # 16 slots, so it keeps one tensor.
+    P = 1 if args.feed == "host" else pool_sets(in_bytes + out_step, args.pool)
+    batches = [evam.ImageBatch(device_frames(evam, torch, wl, n, device, seed=1234 + rank + 7919 * k))
+               for k in range(P)]
+    n_out = 1 if ring else P
+    outs = [torch.empty((out_n, 3, DH, DW), dtype=dtype, device=device) for _ in range(n_out)]
+    pool_bytes = P * in_bytes + n_out * out_n * 3 * DH * DW * esz
     pp = evam.HipPreProcessor(device=local)
 
     feed = None
@@ -207,17 +237,20 @@ def main():
         for hb in feed.host:   # stands in for a decoder writing into the pinned ring
             hb.numpy()[:] = frng.integers(0, 256, hb.numel(), dtype=np.uint8)
 
-    def step(t):
+    def step(t, k=None):
+        """One launch; k = pool set (default: set t mod P, so consecutive steps touch different sets)."""
+        k = t % P if k is None else k
+        out = outs[k % n_out]
         if feed is not None:
-            k = feed.acquire()
-            feed.submit(k)
-            pp.convert(feed.batch(k), out, info)
-            feed.release(k)
+            j = feed.acquire()
+            feed.submit(j)
+            pp.convert(feed.batch(j), out, info)
+            feed.release(j)
             return
         if ring:
-            pp.convert(batch, out, info, slot_offset=t % ring, slot_stride=ring)
+            pp.convert(batches[k], out, info, slot_offset=t % ring, slot_stride=ring)
         else:
-            pp.convert(batch, out, info, rois=roi_sets[t % ROI_SETS] if roi_sets else None)
+            pp.convert(batches[k], out, info, rois=roi_sets[t % ROI_SETS] if roi_sets else None)
 
     # algorithmic bytes per launch (SURVEY.md §8d), from the library's own accounting
     pp.set_option(evam.native.OPT_STATS, 1)
@@ -259,12 +292,31 @@ def main():
     torch.cuda.synchronize()
     per = np.sort(np.array([a.elapsed_time(b) for a, b in evs])) if n_dist else np.zeros(1)
     pct = {q: round(float(np.percentile(per, q)), 5) for q in (10, 50, 90)}
+    # Secondary: the same launches re-reading ONE set (frames and output resident in the Infinity Cache
+    # when they fit), for comparison with the pooled headline.
+    resident = None
+    if args.resident_steps > 0 and feed is None:
+        for t in range(20):
+            step(t, k=0)
+        r0 = torch.cuda.Event(enable_timing=True)
+        r1 = torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        r0.record(stream)
+        for t in range(args.resident_steps):
+            step(t, k=0)
+        r1.record(stream)
+        torch.cuda.synchronize()
+        res_ms = r0.elapsed_time(r1) / args.resident_steps
+        res_gbs = alg_bytes / (res_ms * 1e-3) / 1e9
+        resident = {"achieved": round(res_gbs, 1), "frac": round(res_gbs / HBM_PEAK_GBS, 4),
+                    "mean_launch_ms": round(res_ms, 5), "steps": args.resident_steps,
+                    "set_bytes": in_bytes + out_n * 3 * DH * DW * esz}
     tot = evam.streams.reduce_run(wall, n * args.steps, alg_bytes * args.steps,
                                   device=device if world > 1 and backend == "nccl" else None)
     wall_max = tot.elapsed_max_s
     value = tot.frames / wall_max
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
-    traffic = load_pmc_traffic(args.config, n)
+    traffic = load_pmc_traffic(args.config, n, P)
 
     if rank == 0:
         res = {
@@ -283,11 +335,14 @@ def main():
             "data": "synthetic (seeded uniform u8 planes generated on device; no video decode)",
             "config": {"workload": wl["desc"], "frames_per_gpu_per_step": n, "items_per_launch": n_items,
                        "src": f"{wl['src'][0]}x{wl['src'][1]} {wl['fourcc']}", "dst": f"{DW}x{DH}",
+                       "pool_sets": P, "pool_bytes": pool_bytes,
+                       "pool": "each step reads a different frame set and writes a different output tensor; "
+                               "pool >= 3x the 256 MiB Infinity Cache" if P > 1 else "one resident set",
                        "parallelism": f"streams s mod {world}, one process per GPU, no hot-loop collective"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "algorithmic_bytes_per_launch": alg_bytes, "mean_launch_ms": round(kern_ms, 5),
-                         "launch_ms_p10_p50_p90": [pct[10], pct[50], pct[90]]},
+                         "launch_ms_p10_p50_p90": [pct[10], pct[50], pct[90]], "resident": resident},
         }
         if feed is not None:
             res["h2d"] = {"bytes_per_step": feed.bytes_per_batch,

@@ -1,0 +1,275 @@
+// evam_geom.h — the integer / IEEE arithmetic shared by the HIP kernels and the host planner of
+// libevam_pp.so: OpenCV INTER_LINEAR coefficient entries, ROI clipping and aspect-ratio geometry,
+// staged source footprints, LDS staging bounds and the algorithmic byte count (SURVEY.md §8 a2, a5,
+// a6, d). Everything here is plain C++ on integers and IEEE doubles/floats, so the device and the
+// host compute bit-identical values; tests/native/planner_check.cpp compiles this header for the host
+// alone under AddressSanitizer / UBSan (tests/test_native_asan.py).
+//
+// EVAM_HD marks functions the kernels call too: evam_pp.hip defines it as __host__ __device__ before
+// including this header; a host-only build leaves it empty. Translation units that include this
+// header must be compiled with -ffp-contract=off (linear_coef is OpenCV's exact float sequence).
+#ifndef EVAM_GEOM_H
+#define EVAM_GEOM_H
+
+#include <stdint.h>
+
+#include <algorithm>
+#include <cmath>
+#include <vector>
+
+#include "../../include/evam_pp.h"
+
+#ifndef EVAM_HD
+#define EVAM_HD
+#endif
+
+namespace evam {
+
+enum FmtId { kNV12 = 0, kI420 = 1, kBGRX = 2, kBGR = 3 };
+
+inline int fmt_bpp(int f) { return f == kBGRX ? 4 : (f == kBGR ? 3 : 1); }
+inline int fmt_nplanes(int f) { return f == kNV12 ? 2 : (f == kI420 ? 3 : 1); }
+
+// Row-kernel (uniform geometry) tables, built on the host once per geometry and cached in the
+// descriptor block. Indexed by output column X / output row Y of the DW x DH plane.
+struct alignas(16) XTab {  // 16 B
+    int32_t s0, s1;      // source columns of the two taps, relative to the crop (s1 = min(s0+1, cw-1))
+    uint16_t a0, a1;     // 11-bit weights << 4; both 0: column shows padding
+    int32_t pad;
+};
+struct alignas(16) YTab {  // 16 B
+    int32_t r0, r1;      // source rows of the two taps, relative to the crop (clamped)
+    int32_t b0, b1;      // 11-bit weights << 8; both 0: row shows padding
+};
+
+// hal::resize INTER_LINEAR table entry (OpenCV resize.cpp). Every operation is a single IEEE
+// rounding; the translation unit is compiled with -ffp-contract=off so (d+0.5)*scale-0.5 never
+// becomes an FMA.
+EVAM_HD inline void linear_coef(int d, double scale, int ssize, bool is_x, int& s, int& c0, int& c1) {
+    double t = ((double)d + 0.5) * scale;
+    t = t - 0.5;
+    float f = (float)t;
+    float fl = floorf(f);
+    int si = (int)fl;
+    f = f - fl;
+    if (is_x) {
+        if (si < 0) { f = 0.f; si = 0; }
+        if (si >= ssize - 1) { f = 0.f; si = ssize - 1; }
+    }
+    s = si;
+    float w0 = (1.f - f) * 2048.f;
+    float w1 = f * 2048.f;
+    c0 = (int)rintf(w0);
+    c1 = (int)rintf(w1);
+}
+
+struct Geom {
+    int x0, y0, cw, ch, rw, rh, ox, oy;
+};
+
+// ROI clipping / 4:2:0 even alignment (rules documented in include/evam_pp.h). Shared by the host
+// planner and the ROI kernel, which derives every item's geometry from the raw evam_roi on the device.
+// Returns 0 or EVAM_PP_ERR_EMPTY_ROI.
+EVAM_HD inline int roi_clip(int f, int W, int H, bool has_roi, int rx, int ry, int rwid, int rhei, Geom& g) {
+    int x0 = 0, y0 = 0, x1 = W, y1 = H;
+    if (has_roi && rwid > 0 && rhei > 0) {
+        // 64-bit: x + w of caller-supplied int32 rects may exceed INT32_MAX
+        auto cl = [](long long v, int hi) { return v < 0 ? 0 : (v > hi ? hi : (int)v); };
+        x0 = cl(rx, W); y0 = cl(ry, H);
+        x1 = cl((long long)rx + rwid, W); y1 = cl((long long)ry + rhei, H);
+        if (f == kNV12 || f == kI420) {
+            x0 &= ~1; y0 &= ~1;
+            x1 = (x1 + 1) & ~1; x1 = x1 < W ? x1 : W;
+            y1 = (y1 + 1) & ~1; y1 = y1 < H ? y1 : H;
+        }
+    }
+    if (x1 - x0 <= 0 || y1 - y0 <= 0) return EVAM_PP_ERR_EMPTY_ROI;
+    g.x0 = x0; g.y0 = y0; g.cw = x1 - x0; g.ch = y1 - y0;
+    return 0;
+}
+
+// Crop + resize + placement of one item (DL Streamer model-proc resize / crop).
+EVAM_HD inline int roi_geometry(int f, int W, int H, bool has_roi, int rx, int ry, int rwid, int rhei, int mode,
+                                int placement, int DW, int DH, Geom& g) {
+    if (roi_clip(f, W, H, has_roi, rx, ry, rwid, rhei, g)) return EVAM_PP_ERR_EMPTY_ROI;
+    g.ox = 0; g.oy = 0;
+    if (mode == EVAM_RESIZE_NO_ASPECT) {
+        g.rw = DW; g.rh = DH;
+        return 0;
+    }
+    const double sx = (double)DW / g.cw, sy = (double)DH / g.ch;
+    const bool x_dom = mode == EVAM_RESIZE_ASPECT ? (sx <= sy) : (sx >= sy);
+    if (x_dom) { g.rw = DW; g.rh = (int)(g.ch * sx); }
+    else { g.rh = DH; g.rw = (int)(g.cw * sy); }
+    g.rw = g.rw > 1 ? g.rw : 1;
+    g.rh = g.rh > 1 ? g.rh : 1;
+    if (mode == EVAM_RESIZE_ASPECT) {
+        g.rw = g.rw < DW ? g.rw : DW;
+        g.rh = g.rh < DH ? g.rh : DH;
+        if (placement == EVAM_PLACE_CENTER) { g.ox = (DW - g.rw) / 2; g.oy = (DH - g.rh) / 2; }
+    } else {
+        g.rw = g.rw > DW ? g.rw : DW;
+        g.rh = g.rh > DH ? g.rh : DH;
+        g.ox = -((g.rw - DW) / 2);
+        g.oy = -((g.rh - DH) / 2);
+    }
+    return 0;
+}
+
+// 16-byte-aligned byte windows [fs, fs + 16 n) of a luma / packed row (Y) and of a chroma row (C) that
+// the taps of source columns [xa, xb] (absolute) read.
+EVAM_HD inline void footprint_chunks(int FMT, int bpp, int xa, int xb, int& fsY, int& nY, int& fsC, int& nC) {
+    fsY = (xa * bpp) & ~15;
+    nY = (((xb * bpp + bpp + 15) & ~15) - fsY) >> 4;
+    fsC = nC = 0;
+    if (FMT == kNV12) {
+        fsC = (2 * (xa >> 1)) & ~15;
+        nC = (((2 * (xb >> 1) + 2 + 15) & ~15) - fsC) >> 4;
+    } else if (FMT == kI420) {
+        fsC = (xa >> 1) & ~15;
+        nC = ((((xb >> 1) + 1 + 15) & ~15) - fsC) >> 4;
+    }
+}
+
+// Source footprint of one item's visible output columns (ROI kernel).
+EVAM_HD inline void item_footprint(int FMT, int bpp, int x0, int cw, int rw, int ox, double scx, int DW, int& fsY,
+                                   int& nY, int& fsC, int& nC) {
+    fsY = nY = fsC = nC = 0;
+    const int Xv0 = ox > 0 ? ox : 0;
+    const int Xv1 = (ox + rw < DW ? ox + rw : DW) - 1;
+    if (Xv0 > Xv1) return;
+    int sa, sb, c0, c1;
+    linear_coef(Xv0 - ox, scx, cw, true, sa, c0, c1);
+    linear_coef(Xv1 - ox, scx, cw, true, sb, c0, c1);
+    const int xa = x0 + sa, xb = x0 + (sb + 1 < cw - 1 ? sb + 1 : cw - 1);
+    footprint_chunks(FMT, bpp, xa, xb, fsY, nY, fsC, nC);
+}
+
+// Upper bound of the staged bytes of one output row of an item whose crop is cw pixels wide (both
+// luma / packed taps plus both chroma taps of every chroma plane), for the host's buffer sizing.
+inline int row_bytes_bound(int f, int cw) {
+    const int bpp = fmt_bpp(f);
+    const int segY = ((cw * bpp + 15) / 16 + 1) * 16;
+    const int segC = f == kNV12 ? ((cw + 1 + 15) / 16 + 1) * 16 : (f == kI420 ? ((cw / 2 + 1 + 15) / 16 + 1) * 16 : 0);
+    const int npc = f == kI420 ? 2 : (f == kNV12 ? 1 : 0);
+    return 2 * segY + 2 * npc * segC;
+}
+
+// Widest 16-byte chunk counts (mY luma/packed, mC chroma) of the per-tile footprints of a uniform
+// group, over every tile of tw output columns and every crop-origin residue x0 mod 32 present
+// (x0_mask bit r). The chunk count of a footprint depends on x0 only through x0 mod 32 (the 16-byte
+// phase of every plane: luma / packed at bpp 1, 3, 4; NV12 chroma 2 (x >> 1); I420 chroma x >> 1).
+// xt: the group's column table; ox / rw: its placement and resized width.
+inline void wave_segments(int f, int ox, int rw, int DW, const XTab* xt, uint32_t x0_mask, int tw, int& mY,
+                          int& mC) {
+    const int bpp = fmt_bpp(f);
+    mY = mC = 0;
+    for (int r = 0; r < 32; r++) {
+        if (!((x0_mask >> r) & 1u)) continue;
+        for (int X0 = 0; X0 < DW; X0 += tw) {
+            const int Xv0 = std::max(X0, ox), Xv1 = std::min(std::min(X0 + tw, DW), ox + rw) - 1;
+            if (Xv0 > Xv1) continue;
+            int fsY, nY, fsC, nC;
+            footprint_chunks(f, bpp, r + xt[Xv0].s0, r + xt[Xv1].s1, fsY, nY, fsC, nC);
+            mY = std::max(mY, nY);
+            mC = std::max(mC, nC);
+        }
+    }
+}
+
+// Staged kernel geometry: the widest column segment count (of 4 / 2 / 1 x 64 output columns) whose
+// worst-case source footprint fits a slot-byte LDS row slot. Returns 0 when none does.
+inline int staged_nsegx(int f, double ratio, int stage_rows, int slot) {
+    const int bpp = fmt_bpp(f);
+    for (int n : {4, 2, 1}) {
+        if (stage_rows % (4 / n) != 0) continue;
+        const int tw = 64 * n;
+        const int span = (int)std::ceil((tw - 1) * ratio) + 3;  // source columns touched by one tile row
+        if (span * bpp + 32 <= slot) return n;
+    }
+    return 0;
+}
+
+// Algorithmic bytes of one item: distinct touched source rows x the byte width of
+// the source window feeding the visible output, per plane; plus output bytes.
+inline int64_t item_src_bytes(int f, const Geom& g, int DW, int DH) {
+    const int dx_lo = std::max(-g.ox, 0), dx_hi = std::min(DW - g.ox, g.rw) - 1;
+    const int dy_lo = std::max(-g.oy, 0), dy_hi = std::min(DH - g.oy, g.rh) - 1;
+    if (dx_lo > dx_hi || dy_lo > dy_hi) return 0;
+    const double scx = 1. / ((double)g.rw / g.cw), scy = 1. / ((double)g.rh / g.ch);
+    int s, c0, c1, sxa, sxb;
+    linear_coef(dx_lo, scx, g.cw, true, sxa, c0, c1);
+    linear_coef(dx_hi, scx, g.cw, true, sxb, c0, c1);
+    int xa = g.x0 + sxa, xb = g.x0 + std::min(sxb + 1, g.cw - 1);
+    if (dx_lo == 0 && dx_hi == g.rw - 1) { xa = g.x0; xb = g.x0 + g.cw - 1; }  // whole crop window
+    int64_t rows = 0, crow = 0;
+    int last = -1, lastc = -1;
+    for (int dy = dy_lo; dy <= dy_hi; dy++) {
+        linear_coef(dy, scy, g.ch, false, s, c0, c1);
+        const int r0 = g.y0 + std::min(std::max(s, 0), g.ch - 1);
+        const int r1 = g.y0 + std::min(std::max(s + 1, 0), g.ch - 1);
+        for (int r : {r0, r1}) {  // rows are non-decreasing in dy
+            if (r > last) { rows++; last = r; }
+            if ((r >> 1) > lastc) { crow++; lastc = r >> 1; }
+        }
+    }
+    const int bpp = fmt_bpp(f);
+    int64_t bytes = rows * (int64_t)(xb - xa + 1) * bpp;
+    if (f == kNV12) bytes += crow * (int64_t)(2 * (xb >> 1) + 2 - 2 * (xa >> 1));
+    if (f == kI420) bytes += 2 * crow * (int64_t)((xb >> 1) - (xa >> 1) + 1);
+    return bytes;
+}
+
+// OpenCV coefficient tables of one uniform geometry, indexed by output column / row of the DW x DH plane
+// (padding columns / rows get zero weights).
+inline void build_tables_into(const Geom& g, int DW, int DH, XTab* x, YTab* y) {
+    const double scx = 1. / ((double)g.rw / g.cw), scy = 1. / ((double)g.rh / g.ch);
+    for (int X = 0; X < DW; X++) {
+        x[X] = XTab{};
+        const int dx = X - g.ox;
+        if (dx < 0 || dx >= g.rw) continue;  // padding: s0 = s1 = 0, weights 0
+        int sx, a0, a1;
+        linear_coef(dx, scx, g.cw, true, sx, a0, a1);
+        x[X].s0 = sx;
+        x[X].s1 = std::min(sx + 1, g.cw - 1);
+        x[X].a0 = (uint16_t)(a0 << 4);
+        x[X].a1 = (uint16_t)(a1 << 4);
+    }
+    for (int Y = 0; Y < DH; Y++) {
+        y[Y] = YTab{};
+        const int dy = Y - g.oy;
+        if (dy < 0 || dy >= g.rh) continue;
+        int sy, b0, b1;
+        linear_coef(dy, scy, g.ch, false, sy, b0, b1);
+        y[Y].r0 = std::min(std::max(sy, 0), g.ch - 1);
+        y[Y].r1 = std::min(std::max(sy + 1, 0), g.ch - 1);
+        y[Y].b0 = b0 << 8;
+        y[Y].b1 = b1 << 8;
+    }
+}
+
+// ROI launch order: largest estimated work first (counting sort on 64 buckets of crop width x touched
+// rows, stable within a bucket). idx: the group's item indices; bucket: scratch indexed by item index.
+inline void roi_largest_first(const int* idx, int n, const Geom* geo, int DH, bool sort, int* bucket,
+                              std::vector<int>& ord) {
+    int64_t maxw = 1;
+    if (sort)
+        for (int m = 0; m < n; m++) {
+            const int i = idx[m];
+            maxw = std::max(maxw, (int64_t)geo[i].cw * std::min(geo[i].ch, 2 * DH));
+        }
+    int start[65] = {0};
+    for (int m = 0; m < n; m++) {
+        const int i = idx[m];
+        const int64_t w = (int64_t)geo[i].cw * std::min(geo[i].ch, 2 * DH);
+        bucket[i] = sort ? 63 - (int)(w * 63 / maxw) : 0;  // 0 = largest
+        start[bucket[i] + 1]++;
+    }
+    for (int b = 0; b < 64; b++) start[b + 1] += start[b];
+    ord.assign(start[64], 0);
+    for (int m = 0; m < n; m++) ord[start[bucket[idx[m]]]++] = idx[m];
+}
+
+}  // namespace evam
+
+#endif  // EVAM_GEOM_H

@@ -34,7 +34,12 @@
 
 #include "../../include/evam_pp.h"
 
+#define EVAM_HD __host__ __device__
+#include "evam_geom.h"
+
 namespace {
+
+using namespace evam;
 
 // ------------------------------------------------------------------------------------------------
 // constants
@@ -58,8 +63,6 @@ constexpr int kHalf = 1 << 19;
 constexpr int kKR = kHalf - 128 * kCVR - 16 * kCY;  // the luma term is max(Y,16)*CY (see yuv_to_bgr)
 constexpr int kKG = kHalf - 128 * kCVG - 128 * kCUG - 16 * kCY;
 constexpr int kKB = kHalf - 128 * kCUB - 16 * kCY;
-
-enum FmtId { kNV12 = 0, kI420 = 1, kBGRX = 2, kBGR = 3 };
 
 // ------------------------------------------------------------------------------------------------
 // device-side descriptors
@@ -103,20 +106,24 @@ struct alignas(16) RowEntry {  // 32 B
     int32_t pad0, pad1;
 };
 
-// Row-kernel (uniform geometry) tables, built on the host once per geometry and cached in the
-// descriptor block. Indexed by output column X / output row Y of the DW x DH plane.
-struct alignas(16) XTab {  // 16 B
-    int32_t s0, s1;      // source columns of the two taps, relative to the crop (s1 = min(s0+1, cw-1))
-    uint16_t a0, a1;     // 11-bit weights << 4; both 0: column shows padding
-    int32_t pad;
+// Per-item arguments of the uniform-geometry kernels (staged / wave / rows), carried in the launch's
+// kernel arguments: every item of such a launch shares crop size, resized size and placement, so an
+// item differs only in its frame (planes, pitches), its crop origin and its output slot. Passing them
+// in the kernarg segment means a new set of frames (a decoder's next surfaces, a rotating frame pool)
+// costs no descriptor upload and no cross-stream wait; launches take up to kArgItems items each.
+struct ItemArg {  // 48 B
+    const uint8_t* plane[3];
+    int32_t pitch[3];
+    int32_t x0, y0;   // crop origin in source pixels
+    int32_t index;    // item index in the call: output slot = slot_offset + index * slot_stride
 };
-struct alignas(16) YTab {  // 16 B
-    int32_t r0, r1;      // source rows of the two taps, relative to the crop (clamped)
-    int32_t b0, b1;      // 11-bit weights << 8; both 0: row shows padding
-};
+static_assert(sizeof(ItemArg) == 48, "ItemArg layout");
+constexpr int kArgItems = 64;  // 3 KB of items per launch; the whole parameter block stays < 4 KB
+
 
 struct RParams {
-    const ItemDesc* items;
+    ItemArg items[kArgItems];
+    int ox, rw;          // uniform placement / resized width
     const float* lut;    // [3][256]
     const XTab* xtab;    // [DW]
     const YTab* ytab;    // [DH]
@@ -137,7 +144,8 @@ constexpr int kStageRows = EVAM_PP_STAGE_ROWS;  // output rows per staged group 
 constexpr int kSlot = 1024;  // bytes of one staged source-row segment = one wave-wide 16 B/lane LDS-DMA
 
 struct SParams {
-    const ItemDesc* items;
+    ItemArg items[kArgItems];
+    int ox, rw;          // uniform placement / resized width
     const float* lut;    // [3][256]
     const XTab* xtab;    // [DW]
     const YTab* ytab;    // [DH]
@@ -164,26 +172,6 @@ __device__ inline int xcd_tile(int b, int grid) {
 // ------------------------------------------------------------------------------------------------
 // exact OpenCV arithmetic (shared host/device)
 // ------------------------------------------------------------------------------------------------
-// hal::resize INTER_LINEAR table entry. Every operation is a single IEEE rounding; the translation
-// unit is compiled with -ffp-contract=off so (d+0.5)*scale-0.5 never becomes an FMA.
-__host__ __device__ inline void linear_coef(int d, double scale, int ssize, bool is_x, int& s, int& c0,
-                                            int& c1) {
-    double t = ((double)d + 0.5) * scale;
-    t = t - 0.5;
-    float f = (float)t;
-    float fl = floorf(f);
-    int si = (int)fl;
-    f = f - fl;
-    if (is_x) {
-        if (si < 0) { f = 0.f; si = 0; }
-        if (si >= ssize - 1) { f = 0.f; si = ssize - 1; }
-    }
-    s = si;
-    float w0 = (1.f - f) * 2048.f;
-    float w1 = f * 2048.f;
-    c0 = (int)rintf(w0);
-    c1 = (int)rintf(w1);
-}
 
 __device__ __forceinline__ uint32_t umulhi(uint32_t a, uint32_t b) { return __umulhi(a, b); }
 
@@ -525,17 +513,16 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_rows(const RParams P) {
     const int tile = t - item * P.tiles_per_item;
     const int ty = tile / P.tiles_x;
     const int tx = tile - ty * P.tiles_x;
-    const __attribute__((address_space(4))) ItemDesc* it =
-        (const __attribute__((address_space(4))) ItemDesc*)(P.items) + item;
+    const ItemArg& it = P.items[item];
     const __attribute__((address_space(4))) YTab* ytab = (const __attribute__((address_space(4))) YTab*)(P.ytab);
-    const uint8_t* __restrict__ p0 = it->plane[0];
-    const uint8_t* __restrict__ p1 = it->plane[1];
-    const uint8_t* __restrict__ p2 = it->plane[2];
-    const int pitch0 = it->pitch[0], pitch1 = it->pitch[1], pitch2 = it->pitch[2];
-    const int x0 = it->x0, y0 = it->y0;
+    const uint8_t* __restrict__ p0 = it.plane[0];
+    const uint8_t* __restrict__ p1 = it.plane[1];
+    const uint8_t* __restrict__ p2 = it.plane[2];
+    const int pitch0 = it.pitch[0], pitch1 = it.pitch[1], pitch2 = it.pitch[2];
+    const int x0 = it.x0, y0 = it.y0;
     const size_t plane = (size_t)P.DW * P.DH;
     const size_t esz = OUT == 1 ? 4 : 1;
-    uint8_t* const d0 = reinterpret_cast<uint8_t*>(P.dst) + (size_t)(P.slot_offset + it->index * P.slot_stride) * 3 * plane * esz;
+    uint8_t* const d0 = reinterpret_cast<uint8_t*>(P.dst) + (size_t)(P.slot_offset + it.index * P.slot_stride) * 3 * plane * esz;
     uint8_t* const d1 = d0 + plane * esz;
     uint8_t* const d2 = d1 + plane * esz;
     // Buffer resources (wave-uniform). Offsets are always in range by construction, so the range
@@ -762,18 +749,17 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_staged(const SParams P) {
     const int tile = t - item * P.tiles_per_item;
     const int ty = tile / P.tiles_x;
     const int tx = tile - ty * P.tiles_x;
-    const __attribute__((address_space(4))) ItemDesc* it =
-        (const __attribute__((address_space(4))) ItemDesc*)(P.items) + item;
+    const ItemArg& it = P.items[item];
     const __attribute__((address_space(4))) YTab* ytab = (const __attribute__((address_space(4))) YTab*)(P.ytab);
     const __attribute__((address_space(4))) XTab* xtab_s = (const __attribute__((address_space(4))) XTab*)(P.xtab);
-    const uint8_t* p0 = it->plane[0];
-    const uint8_t* p1 = it->plane[1];
-    const uint8_t* p2 = it->plane[2];
-    const int pitch0 = it->pitch[0], pitch1 = it->pitch[1], pitch2 = it->pitch[2];
-    const int x0 = it->x0, y0 = it->y0, ox = it->ox, rw = it->rw;
+    const uint8_t* p0 = it.plane[0];
+    const uint8_t* p1 = it.plane[1];
+    const uint8_t* p2 = it.plane[2];
+    const int pitch0 = it.pitch[0], pitch1 = it.pitch[1], pitch2 = it.pitch[2];
+    const int x0 = it.x0, y0 = it.y0, ox = P.ox, rw = P.rw;
     const size_t plane = (size_t)P.DW * P.DH;
     const size_t esz = OUT == 1 ? 4 : 1;
-    uint8_t* const d0 = reinterpret_cast<uint8_t*>(P.dst) + (size_t)(P.slot_offset + it->index * P.slot_stride) * 3 * plane * esz;
+    uint8_t* const d0 = reinterpret_cast<uint8_t*>(P.dst) + (size_t)(P.slot_offset + it.index * P.slot_stride) * 3 * plane * esz;
     uint8_t* const d1 = d0 + plane * esz;
     uint8_t* const d2 = d1 + plane * esz;
     const __amdgpu_buffer_rsrc_t rsY = __builtin_amdgcn_make_buffer_rsrc((void*)p0, (short)0, 0x7FFFFFFF, 0x00020000);
@@ -797,16 +783,7 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_staged(const SParams P) {
     const bool cols = Xv0 <= Xv1;
     int fsY = 0, nY = 0, fsC = 0, nC = 0;
     if (cols) {
-        const int xa = x0 + xtab_s[Xv0].s0, xb = x0 + xtab_s[Xv1].s1;
-        fsY = (xa * T::bpp) & ~15;
-        nY = (((xb * T::bpp + T::bpp + 15) & ~15) - fsY) >> 4;
-        if constexpr (FMT == kNV12) {
-            fsC = (2 * (xa >> 1)) & ~15;
-            nC = (((2 * (xb >> 1) + 2 + 15) & ~15) - fsC) >> 4;
-        } else if constexpr (FMT == kI420) {
-            fsC = (xa >> 1) & ~15;
-            nC = ((((xb >> 1) + 1 + 15) & ~15) - fsC) >> 4;
-        }
+        footprint_chunks(FMT, T::bpp, x0 + xtab_s[Xv0].s0, x0 + xtab_s[Xv1].s1, fsY, nY, fsC, nC);
     }
     // per-lane column state (filled once the first DMA is in flight): LDS byte offsets of the taps
     // inside a slot, weights
@@ -1029,7 +1006,8 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_staged(const SParams P) {
 // wave-row kernel (uniform geometry)
 // ------------------------------------------------------------------------------------------------
 struct WParams {
-    const ItemDesc* items;
+    ItemArg items[kArgItems];
+    int ox, rw;          // uniform placement / resized width
     const float* lut;    // [3][256]
     const XTab* xtab;    // [DW]
     const YTab* ytab;    // [DH]
@@ -1101,17 +1079,16 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_wave(const WParams P) {
     const int tile = t - item * P.tiles_per_item;
     const int ty = tile / P.tiles_x;
     const int tx = tile - ty * P.tiles_x;
-    const __attribute__((address_space(4))) ItemDesc* it =
-        (const __attribute__((address_space(4))) ItemDesc*)(P.items) + item;
+    const ItemArg& it = P.items[item];
     const __attribute__((address_space(4))) XTab* xtab_s = (const __attribute__((address_space(4))) XTab*)(P.xtab);
-    const uint8_t* p0 = it->plane[0];
-    const uint8_t* p1 = it->plane[1];
-    const uint8_t* p2 = it->plane[2];
-    const int pitch0 = it->pitch[0], pitch1 = it->pitch[1], pitch2 = it->pitch[2];
-    const int x0 = it->x0, y0 = it->y0, ox = it->ox, rw = it->rw;
+    const uint8_t* p0 = it.plane[0];
+    const uint8_t* p1 = it.plane[1];
+    const uint8_t* p2 = it.plane[2];
+    const int pitch0 = it.pitch[0], pitch1 = it.pitch[1], pitch2 = it.pitch[2];
+    const int x0 = it.x0, y0 = it.y0, ox = P.ox, rw = P.rw;
     const size_t plane = (size_t)P.DW * P.DH;
     const size_t esz = OUT == 1 ? 4 : 1;
-    uint8_t* const d0 = reinterpret_cast<uint8_t*>(P.dst) + (size_t)(P.slot_offset + it->index * P.slot_stride) * 3 * plane * esz;
+    uint8_t* const d0 = reinterpret_cast<uint8_t*>(P.dst) + (size_t)(P.slot_offset + it.index * P.slot_stride) * 3 * plane * esz;
     uint8_t* const d1 = d0 + plane * esz;
     uint8_t* const d2 = d1 + plane * esz;
     const __amdgpu_buffer_rsrc_t rsY = __builtin_amdgcn_make_buffer_rsrc((void*)p0, (short)0, 0x7FFFFFFF, 0x00020000);
@@ -1137,16 +1114,7 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_wave(const WParams P) {
     const bool cols = Xv0 <= Xv1;
     int fsY = 0, nY = 0, fsC = 0, nC = 0;
     if (cols) {
-        const int xa = x0 + xtab_s[Xv0].s0, xb = x0 + xtab_s[Xv1].s1;
-        fsY = (xa * T::bpp) & ~15;
-        nY = (((xb * T::bpp + T::bpp + 15) & ~15) - fsY) >> 4;
-        if constexpr (FMT == kNV12) {
-            fsC = (2 * (xa >> 1)) & ~15;
-            nC = (((2 * (xb >> 1) + 2 + 15) & ~15) - fsC) >> 4;
-        } else if constexpr (FMT == kI420) {
-            fsC = (xa >> 1) & ~15;
-            nC = ((((xb >> 1) + 1 + 15) & ~15) - fsC) >> 4;
-        }
+        footprint_chunks(FMT, T::bpp, x0 + xtab_s[Xv0].s0, x0 + xtab_s[Xv1].s1, fsY, nY, fsC, nC);
     }
     // per-lane column state for the PX pixels of this lane
     const int Xl = X0 + lane * PX;
@@ -1393,90 +1361,6 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_wave(const WParams P) {
     }
 }
 
-struct Geom {
-    int x0, y0, cw, ch, rw, rh, ox, oy;
-};
-
-// ROI clipping / 4:2:0 even alignment / aspect-ratio geometry (rules documented in include/evam_pp.h).
-// Shared by the host planner and the ROI kernel, which derives every item's geometry from the raw
-// evam_roi on the device. Integer and IEEE-double operations only, so both sides agree bit for bit.
-// Returns 0 or EVAM_PP_ERR_EMPTY_ROI.
-__host__ __device__ inline int roi_clip(int f, int W, int H, bool has_roi, int rx, int ry, int rwid, int rhei, Geom& g) {
-    int x0 = 0, y0 = 0, x1 = W, y1 = H;
-    if (has_roi && rwid > 0 && rhei > 0) {
-        auto cl = [](int v, int hi) { return v < 0 ? 0 : (v > hi ? hi : v); };
-        x0 = cl(rx, W); y0 = cl(ry, H);
-        x1 = cl(rx + rwid, W); y1 = cl(ry + rhei, H);
-        if (f == kNV12 || f == kI420) {
-            x0 &= ~1; y0 &= ~1;
-            x1 = (x1 + 1) & ~1; x1 = x1 < W ? x1 : W;
-            y1 = (y1 + 1) & ~1; y1 = y1 < H ? y1 : H;
-        }
-    }
-    if (x1 - x0 <= 0 || y1 - y0 <= 0) return EVAM_PP_ERR_EMPTY_ROI;
-    g.x0 = x0; g.y0 = y0; g.cw = x1 - x0; g.ch = y1 - y0;
-    return 0;
-}
-
-__host__ __device__ inline int roi_geometry(int f, int W, int H, bool has_roi, int rx, int ry, int rwid, int rhei,
-                                            int mode, int placement, int DW, int DH, Geom& g) {
-    if (roi_clip(f, W, H, has_roi, rx, ry, rwid, rhei, g)) return EVAM_PP_ERR_EMPTY_ROI;
-    g.ox = 0; g.oy = 0;
-    if (mode == EVAM_RESIZE_NO_ASPECT) {
-        g.rw = DW; g.rh = DH;
-        return 0;
-    }
-    const double sx = (double)DW / g.cw, sy = (double)DH / g.ch;
-    const bool x_dom = mode == EVAM_RESIZE_ASPECT ? (sx <= sy) : (sx >= sy);
-    if (x_dom) { g.rw = DW; g.rh = (int)(g.ch * sx); }
-    else { g.rh = DH; g.rw = (int)(g.cw * sy); }
-    g.rw = g.rw > 1 ? g.rw : 1;
-    g.rh = g.rh > 1 ? g.rh : 1;
-    if (mode == EVAM_RESIZE_ASPECT) {
-        g.rw = g.rw < DW ? g.rw : DW;
-        g.rh = g.rh < DH ? g.rh : DH;
-        if (placement == EVAM_PLACE_CENTER) { g.ox = (DW - g.rw) / 2; g.oy = (DH - g.rh) / 2; }
-    } else {
-        g.rw = g.rw > DW ? g.rw : DW;
-        g.rh = g.rh > DH ? g.rh : DH;
-        g.ox = -((g.rw - DW) / 2);
-        g.oy = -((g.rh - DH) / 2);
-    }
-    return 0;
-}
-
-// Source footprint of one item's visible output columns: the 16 B-aligned byte window [fs, fs + 16 n)
-// of a luma / packed row (fsY, nY) and of a chroma row (fsC, nC) that its taps read.
-__host__ __device__ inline void item_footprint(int FMT, int bpp, int x0, int cw, int rw, int ox, double scx, int DW,
-                                               int& fsY, int& nY, int& fsC, int& nC) {
-    fsY = nY = fsC = nC = 0;
-    const int Xv0 = ox > 0 ? ox : 0;
-    const int Xv1 = (ox + rw < DW ? ox + rw : DW) - 1;
-    if (Xv0 > Xv1) return;
-    int sa, sb, c0, c1;
-    linear_coef(Xv0 - ox, scx, cw, true, sa, c0, c1);
-    linear_coef(Xv1 - ox, scx, cw, true, sb, c0, c1);
-    const int xa = x0 + sa, xb = x0 + (sb + 1 < cw - 1 ? sb + 1 : cw - 1);
-    fsY = (xa * bpp) & ~15;
-    nY = (((xb * bpp + bpp + 15) & ~15) - fsY) >> 4;
-    if (FMT == kNV12) {
-        fsC = (2 * (xa >> 1)) & ~15;
-        nC = (((2 * (xb >> 1) + 2 + 15) & ~15) - fsC) >> 4;
-    } else if (FMT == kI420) {
-        fsC = (xa >> 1) & ~15;
-        nC = ((((xb >> 1) + 1 + 15) & ~15) - fsC) >> 4;
-    }
-}
-
-// Upper bound of the staged bytes of one output row of an item whose crop is cw pixels wide (both
-// luma / packed taps plus both chroma taps of every chroma plane), for the host's buffer sizing.
-inline int row_bytes_bound(int f, int cw) {
-    const int bpp = f == kBGRX ? 4 : (f == kBGR ? 3 : 1);
-    const int segY = ((cw * bpp + 15) / 16 + 1) * 16;
-    const int segC = f == kNV12 ? ((cw + 1 + 15) / 16 + 1) * 16 : (f == kI420 ? ((cw / 2 + 1 + 15) / 16 + 1) * 16 : 0);
-    const int npc = f == kI420 ? 2 : (f == kNV12 ? 1 : 0);
-    return 2 * segY + 2 * npc * segC;
-}
 
 static_assert(sizeof(evam_roi) == 20, "evam_roi layout");
 
@@ -1874,8 +1758,6 @@ int fmt_id(int fourcc) {
     }
 }
 
-int fmt_bpp(int f) { return f == kBGRX ? 4 : (f == kBGR ? 3 : 1); }
-int fmt_nplanes(int f) { return f == kNV12 ? 2 : (f == kI420 ? 3 : 1); }
 
 int item_geometry(int f, int W, int H, const evam_roi* roi, const evam_preproc& cfg, int DW, int DH, Geom& g) {
     return roi_geometry(f, W, H, roi != nullptr, roi ? roi->x : 0, roi ? roi->y : 0, roi ? roi->w : 0,
@@ -1900,35 +1782,6 @@ void build_lut(const evam_preproc& cfg, float* lut) {
         }
 }
 
-// Algorithmic bytes of one item: distinct touched source rows x the byte width of
-// the source window feeding the visible output, per plane; plus output bytes.
-int64_t item_src_bytes(int f, const Geom& g, int DW, int DH) {
-    const int dx_lo = std::max(-g.ox, 0), dx_hi = std::min(DW - g.ox, g.rw) - 1;
-    const int dy_lo = std::max(-g.oy, 0), dy_hi = std::min(DH - g.oy, g.rh) - 1;
-    if (dx_lo > dx_hi || dy_lo > dy_hi) return 0;
-    const double scx = 1. / ((double)g.rw / g.cw), scy = 1. / ((double)g.rh / g.ch);
-    int s, c0, c1, sxa, sxb;
-    linear_coef(dx_lo, scx, g.cw, true, sxa, c0, c1);
-    linear_coef(dx_hi, scx, g.cw, true, sxb, c0, c1);
-    int xa = g.x0 + sxa, xb = g.x0 + std::min(sxb + 1, g.cw - 1);
-    if (dx_lo == 0 && dx_hi == g.rw - 1) { xa = g.x0; xb = g.x0 + g.cw - 1; }  // whole crop window
-    int64_t rows = 0, crow = 0;
-    int last = -1, lastc = -1;
-    for (int dy = dy_lo; dy <= dy_hi; dy++) {
-        linear_coef(dy, scy, g.ch, false, s, c0, c1);
-        const int r0 = g.y0 + std::min(std::max(s, 0), g.ch - 1);
-        const int r1 = g.y0 + std::min(std::max(s + 1, 0), g.ch - 1);
-        for (int r : {r0, r1}) {  // rows are non-decreasing in dy
-            if (r > last) { rows++; last = r; }
-            if ((r >> 1) > lastc) { crow++; lastc = r >> 1; }
-        }
-    }
-    const int bpp = fmt_bpp(f);
-    int64_t bytes = rows * (int64_t)(xb - xa + 1) * bpp;
-    if (f == kNV12) bytes += crow * (int64_t)(2 * (xb >> 1) + 2 - 2 * (xa >> 1));
-    if (f == kI420) bytes += 2 * crow * (int64_t)((xb >> 1) - (xa >> 1) + 1);
-    return bytes;
-}
 
 struct TileCfg {
     int TW, TH, offCol, offRow, lds;
@@ -1939,15 +1792,38 @@ int env_int(const char* name, int dflt) {
     return (v && *v) ? atoi(v) : dflt;
 }
 
+// Tuning and diagnostic knobs. Read from the environment once, when a handle is
+// created (evam_pp_create), never on the per-call path. -1 = the measured heuristic default.
+struct Knobs {
+    int staged = 1, wave = 1, rows = 1, roi = 1;   // kernel families allowed (wave 2 = force)
+    int th = -1, tw = -1, xcd = -1;                // staged / generic tiles, XCD-contiguous order
+    int nsegx = 0;                                 // staged tile width in 64-column segments (0: widest that fits)
+    int wth = -1, px = 0, reuse = 1, wave_lds = 40 * 1024;
+    int roi_th = -1, roi_buf = 12 * 1024, roi_px = 1, roi_sort = 1, roi_xcd = 0;
+    int ablate = 0;                                // stage-removal diagnostics (results invalid)
+    void read() {
+        staged = env_int("EVAM_PP_STAGED", staged); wave = env_int("EVAM_PP_WAVE", wave);
+        rows = env_int("EVAM_PP_ROWS", rows); roi = env_int("EVAM_PP_ROI", roi);
+        th = env_int("EVAM_PP_TH", th); tw = env_int("EVAM_PP_TW", tw); xcd = env_int("EVAM_PP_XCD", xcd);
+        nsegx = env_int("EVAM_PP_NSEGX", nsegx);
+        wth = env_int("EVAM_PP_WTH", wth); px = env_int("EVAM_PP_PX", px);
+        reuse = env_int("EVAM_PP_REUSE", reuse); wave_lds = env_int("EVAM_PP_WAVE_LDS", wave_lds);
+        roi_th = env_int("EVAM_PP_ROI_TH", roi_th); roi_buf = env_int("EVAM_PP_ROI_BUF", roi_buf);
+        roi_px = env_int("EVAM_PP_ROI_PX", roi_px); roi_sort = env_int("EVAM_PP_ROI_SORT", roi_sort);
+        roi_xcd = env_int("EVAM_PP_ROI_XCD", roi_xcd);
+        ablate = env_int("EVAM_PP_ABLATE", ablate);
+    }
+};
+
 // Tile shape: up to 512 columns (a whole model-input row when it fits) x enough rows for ~4096 output
 // pixels per 256-thread workgroup, so the per-tile table setup is amortised over ~16 pixels per lane.
 // EVAM_PP_TW / EVAM_PP_TH override (tuning).
-TileCfg choose_tiles(int DW, int DH, int out_dtype) {
+TileCfg choose_tiles(int DW, int DH, int out_dtype, const Knobs& k) {
     TileCfg t{};
     t.TW = std::min(DW, 512);
     t.TH = std::max(1, std::min(DH, 4096 / t.TW));
-    t.TW = std::max(1, std::min(DW, env_int("EVAM_PP_TW", t.TW)));
-    t.TH = std::max(1, std::min(DH, env_int("EVAM_PP_TH", t.TH)));
+    if (k.tw > 0) t.TW = std::max(1, std::min(DW, k.tw));
+    if (k.th > 0) t.TH = std::max(1, std::min(DH, k.th));
     t.offCol = out_dtype == EVAM_DTYPE_F32 ? kLutBytes : 0;
     t.offRow = t.offCol + (int)sizeof(ColEntry) * t.TW;
     t.lds = t.offRow + (int)sizeof(RowEntry) * t.TH;
@@ -1967,27 +1843,7 @@ void build_tables(const Geom& g, int DW, int DH, TabCache& c, XTab* xt, YTab* yt
     if (memcmp(key, c.key, sizeof(key)) != 0) {
         c.x.assign(DW, XTab{});
         c.y.assign(DH, YTab{});
-        const double scx = 1. / ((double)g.rw / g.cw), scy = 1. / ((double)g.rh / g.ch);
-        for (int X = 0; X < DW; X++) {
-            const int dx = X - g.ox;
-            if (dx < 0 || dx >= g.rw) continue;  // padding: s0 = s1 = 0, weights 0
-            int sx, a0, a1;
-            linear_coef(dx, scx, g.cw, true, sx, a0, a1);
-            c.x[X].s0 = sx;
-            c.x[X].s1 = std::min(sx + 1, g.cw - 1);
-            c.x[X].a0 = (uint16_t)(a0 << 4);
-            c.x[X].a1 = (uint16_t)(a1 << 4);
-        }
-        for (int Y = 0; Y < DH; Y++) {
-            const int dy = Y - g.oy;
-            if (dy < 0 || dy >= g.rh) continue;
-            int sy, b0, b1;
-            linear_coef(dy, scy, g.ch, false, sy, b0, b1);
-            c.y[Y].r0 = std::min(std::max(sy, 0), g.ch - 1);
-            c.y[Y].r1 = std::min(std::max(sy + 1, 0), g.ch - 1);
-            c.y[Y].b0 = b0 << 8;
-            c.y[Y].b1 = b1 << 8;
-        }
+        build_tables_into(g, DW, DH, c.x.data(), c.y.data());
         memcpy(c.key, key, sizeof(key));
     }
     memcpy(xt, c.x.data(), sizeof(XTab) * DW);
@@ -2000,16 +1856,16 @@ struct RowCfg {
 
 // Row-kernel tile: TW in {512, 256, 128, 64} (whole 64-pixel segments; 4 waves split them) chosen for
 // the least padding lanes, and enough rows for ~4096 pixels per 256-thread workgroup.
-RowCfg choose_row_tiles(int DW, int DH) {
+RowCfg choose_row_tiles(int DW, int DH, const Knobs& k) {
     RowCfg r{512, 8};
     int best = 1 << 30;
     for (int tw : {512, 256, 128, 64}) {
         const int waste = ((DW + tw - 1) / tw) * tw - DW;
         if (waste < best) { best = waste; r.TW = tw; }
     }
-    r.TW = env_int("EVAM_PP_TW", r.TW);
+    if (k.tw > 0) r.TW = k.tw;
     if (r.TW != 64 && r.TW != 128 && r.TW != 256 && r.TW != 512) r.TW = 512;
-    r.TH = std::max(1, std::min(DH, env_int("EVAM_PP_TH", 4096 / r.TW)));
+    r.TH = std::max(1, std::min(DH, k.th > 0 ? k.th : 4096 / r.TW));
     return r;
 }
 
@@ -2045,18 +1901,6 @@ hipError_t launch_staged(int f, int out, int nsegx, const SParams& p, int grid, 
     }
 }
 
-// Staged kernel geometry: the widest column segment count whose worst-case source footprint fits a
-// kSlot-byte LDS row slot. Returns 0 when none does (the direct row kernel is used instead).
-int staged_nsegx(int f, double ratio) {
-    const int bpp = fmt_bpp(f);
-    for (int n : {4, 2, 1}) {
-        if (kStageRows % (4 / n) != 0) continue;
-        const int tw = 64 * n;
-        const int span = (int)std::ceil((tw - 1) * ratio) + 3;  // source columns touched by one tile row
-        if (span * bpp + 32 <= kSlot) return n;
-    }
-    return 0;
-}
 
 template <int FMT, int OUT>
 hipError_t launch_rows_t(const RParams& p, int grid, int lds, hipStream_t s) {
@@ -2110,22 +1954,21 @@ hipError_t launch_roi_px(const QParams& p, int grid, int lds, hipStream_t s) {
 // one row setup per 4 pixels; EVAM_PP_ROI_PX=4) measured 8 % slower on C3: lanes 4 pixels apart
 // spread their LDS tap reads over 4x more dwords, so the byte reads bank-conflict.
 template <int FMT, int OUT>
-hipError_t launch_roi_t(const QParams& p, int grid, int lds, hipStream_t s) {
-    const int want = env_int("EVAM_PP_ROI_PX", 1);
-    if (want == 4 && p.DW % 4 == 0) return launch_roi_px<FMT, OUT, 4>(p, grid, lds, s);
+hipError_t launch_roi_t(int px, const QParams& p, int grid, int lds, hipStream_t s) {
+    if (px == 4 && p.DW % 4 == 0) return launch_roi_px<FMT, OUT, 4>(p, grid, lds, s);
     return launch_roi_px<FMT, OUT, 1>(p, grid, lds, s);
 }
 
-hipError_t launch_roi(int f, int out, const QParams& p, int grid, int lds, hipStream_t s) {
+hipError_t launch_roi(int f, int out, int px, const QParams& p, int grid, int lds, hipStream_t s) {
     switch (f * 2 + out) {
-    case kNV12 * 2 + 0: return launch_roi_t<kNV12, 0>(p, grid, lds, s);
-    case kNV12 * 2 + 1: return launch_roi_t<kNV12, 1>(p, grid, lds, s);
-    case kI420 * 2 + 0: return launch_roi_t<kI420, 0>(p, grid, lds, s);
-    case kI420 * 2 + 1: return launch_roi_t<kI420, 1>(p, grid, lds, s);
-    case kBGRX * 2 + 0: return launch_roi_t<kBGRX, 0>(p, grid, lds, s);
-    case kBGRX * 2 + 1: return launch_roi_t<kBGRX, 1>(p, grid, lds, s);
-    case kBGR * 2 + 0: return launch_roi_t<kBGR, 0>(p, grid, lds, s);
-    default: return launch_roi_t<kBGR, 1>(p, grid, lds, s);
+    case kNV12 * 2 + 0: return launch_roi_t<kNV12, 0>(px, p, grid, lds, s);
+    case kNV12 * 2 + 1: return launch_roi_t<kNV12, 1>(px, p, grid, lds, s);
+    case kI420 * 2 + 0: return launch_roi_t<kI420, 0>(px, p, grid, lds, s);
+    case kI420 * 2 + 1: return launch_roi_t<kI420, 1>(px, p, grid, lds, s);
+    case kBGRX * 2 + 0: return launch_roi_t<kBGRX, 0>(px, p, grid, lds, s);
+    case kBGRX * 2 + 1: return launch_roi_t<kBGRX, 1>(px, p, grid, lds, s);
+    case kBGR * 2 + 0: return launch_roi_t<kBGR, 0>(px, p, grid, lds, s);
+    default: return launch_roi_t<kBGR, 1>(px, p, grid, lds, s);
     }
 }
 
@@ -2161,33 +2004,25 @@ hipError_t launch_wave(int f, int out, int px, bool reuse, const WParams& p, int
 // Wave-row kernel plan for a uniform-geometry group: pixels per lane PX (the widest whose staging
 // fits the LDS budget and divides DW), the exact per-tile footprint from the host tables, REUSE when
 // consecutive output rows share source rows, and a tile height that gives every CU enough workgroups.
+// The kernel stages each item's footprint from that item's own crop origin x0, and the number of
+// 16-byte chunks a footprint spans depends on x0's alignment: the segments are sized for the worst
+// case over every residue x0 mod 32 present in the group (x0_mask bit r), which covers the 16-byte
+// phase of every plane (luma / packed at bpp 1, 3, 4; NV12 chroma 2 (x >> 1); I420 chroma x >> 1).
 bool plan_wave(int f, const Geom& g, int DW, int DH, int count, int out_dtype, int n_cu, const XTab* xt,
-               const YTab* yt, WParams& w, int& px, bool& reuse, int& lds, int& grid) {
-    const int bpp = fmt_bpp(f);
+               const YTab* yt, uint32_t x0_mask, const Knobs& kn, WParams& w, int& px, bool& reuse, int& lds,
+               int& grid) {
     const int npc = f == kI420 ? 2 : (f == kNV12 ? 1 : 0);
     const int lut = out_dtype == EVAM_DTYPE_F32 ? kLutBytes : 0;
-    const int budget = env_int("EVAM_PP_WAVE_LDS", 40 * 1024);
-    const int want_px = env_int("EVAM_PP_PX", 0);
+    const int budget = kn.wave_lds;
+    const int want_px = kn.px;
+    if (!x0_mask) x0_mask = 1u << (g.x0 & 31);
     px = 0;
     for (int cand : {4, 2, 1}) {
         if (want_px && cand != want_px) continue;
         if (cand > 1 && DW % cand) continue;
         const int tw = 64 * cand;
         int mY = 0, mC = 0;
-        for (int X0 = 0; X0 < DW; X0 += tw) {
-            const int Xv0 = std::max(X0, g.ox), Xv1 = std::min(std::min(X0 + tw, DW), g.ox + g.rw) - 1;
-            if (Xv0 > Xv1) continue;
-            const int xa = g.x0 + xt[Xv0].s0, xb = g.x0 + xt[Xv1].s1;
-            const int fsY = (xa * bpp) & ~15;
-            mY = std::max(mY, (((xb * bpp + bpp + 15) & ~15) - fsY) >> 4);
-            if (f == kNV12) {
-                const int fsC = (2 * (xa >> 1)) & ~15;
-                mC = std::max(mC, (((2 * (xb >> 1) + 2 + 15) & ~15) - fsC) >> 4);
-            } else if (f == kI420) {
-                const int fsC = (xa >> 1) & ~15;
-                mC = std::max(mC, ((((xb >> 1) + 1 + 15) & ~15) - fsC) >> 4);
-            }
-        }
+        wave_segments(f, g.ox, g.rw, DW, xt, x0_mask, tw, mY, mC);
         const int segY = std::max(16, 16 * mY), segC = npc ? std::max(16, 16 * mC) : 0;
         const int wave_bytes = 2 * (2 * segY + 2 * npc * segC);
         const int need = lut + 4 * wave_bytes;
@@ -2206,14 +2041,14 @@ bool plan_wave(int f, const Geom& g, int DW, int DH, int count, int out_dtype, i
         const bool pad0 = (yt[Y].b0 | yt[Y].b1) == 0, pad1 = (yt[Y + 1].b0 | yt[Y + 1].b1) == 0;
         if (!pad0 && !pad1 && yt[Y + 1].r0 <= yt[Y].r1) { reuse = true; break; }
     }
-    if (env_int("EVAM_PP_REUSE", 1) == 0) reuse = false;
+    if (kn.reuse == 0) reuse = false;
     w.DW = DW; w.DH = DH;
     w.tiles_x = (DW + 64 * px - 1) / (64 * px);
     const int per_cu = std::max(1, std::min(8, (160 * 1024) / std::max(lds, 1)));
     const int64_t slots = (int64_t)n_cu * per_cu;
     int64_t rpw = ((int64_t)count * w.tiles_x * DH) / (4 * slots);
     rpw = std::max<int64_t>(2, std::min<int64_t>(32, rpw));
-    w.TH = std::max(1, std::min(std::min(DH, 4 * 64), env_int("EVAM_PP_WTH", (int)(4 * rpw))));  // <= 64 rows per wave
+    w.TH = std::max(1, std::min(std::min(DH, 4 * 64), kn.wth > 0 ? kn.wth : (int)(4 * rpw)));  // <= 64 rows per wave
     w.tiles_per_item = w.tiles_x * ((DH + w.TH - 1) / w.TH);
     const int64_t gr = (int64_t)count * w.tiles_per_item;
     if (gr > 0x7FFFFFFF) return false;
@@ -2225,12 +2060,12 @@ bool plan_wave(int f, const Geom& g, int DW, int DH, int count, int out_dtype, i
 // staging buffer size, sized for the widest crop of the group (max_row_bytes = row_bytes_bound of it).
 // Returns false when the group needs the generic kernel (outputs wider than kRoiK x 256 pixels, or a
 // crop so wide that one output row's segments overflow the LDS budget).
-bool plan_roi(int DW, int DH, int out_dtype, int max_row_bytes, QParams& q, int& lds) {
+bool plan_roi(int DW, int DH, int out_dtype, int max_row_bytes, const Knobs& kn, QParams& q, int& lds) {
     if (DW > kRoiK * kThreads) return false;
-    const int def_buf = env_int("EVAM_PP_ROI_BUF", 12 * 1024);
+    const int def_buf = kn.roi_buf;
     q.DW = DW; q.DH = DH;
     q.TH = (int64_t)DW * DH <= 32768 ? DH : std::max(8, std::min(DH, 16384 / DW));
-    q.TH = std::max(1, std::min(DH, env_int("EVAM_PP_ROI_TH", q.TH)));
+    if (kn.roi_th > 0) q.TH = std::max(1, std::min(DH, kn.roi_th));
     q.tiles_per_item = (DH + q.TH - 1) / q.TH;
     q.offXT = out_dtype == EVAM_DTYPE_F32 ? kLutBytes : 0;
     q.offYT = q.offXT + (int)sizeof(XTab) * DW;
@@ -2291,9 +2126,11 @@ struct evam_pp {
     evam_preproc lut_key{};        // cfg the cached LUT was built from (norm fields + dtype)
     bool lut_valid = false;
     float lut[768];
+    Knobs knobs;                   // EVAM_PP_* tuning knobs, read once at evam_pp_create
     std::vector<int> sc_fmt;       // per-call scratch, kept to avoid reallocation
     std::vector<int> sc_bucket;
     std::vector<int> sc_order;
+    std::vector<int> sc_members;   // item indices grouped by source format
     std::vector<Geom> sc_geo;
 };
 
@@ -2421,6 +2258,7 @@ int evam_pp_create(int hip_device, void* hip_stream, evam_pp** out) {
     evam_pp* h = new (std::nothrow) evam_pp();
     if (!h) return fail(EVAM_PP_ERR_OOM, "evam_pp_create: out of host memory");
     h->device = hip_device;
+    h->knobs.read();
     if (hipDeviceGetAttribute(&h->n_cu, hipDeviceAttributeMultiprocessorCount, hip_device) != hipSuccess || h->n_cu <= 0)
         h->n_cu = 256;
     h->stream = reinterpret_cast<hipStream_t>(hip_stream);
@@ -2524,6 +2362,11 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
     const int64_t plane = (int64_t)DW * DH;
     if (plane * 3 * (int64_t)dst->n > ((int64_t)1 << 40))
         return fail(EVAM_PP_ERR_INVALID_ARG, "evam_pp_run: dst too large");
+    const int esz = cfg->out_dtype == EVAM_DTYPE_F32 ? 4 : 1;
+    // The kernels address one output plane with 32-bit byte offsets.
+    if (plane * esz > INT32_MAX)
+        return fail(EVAM_PP_ERR_INVALID_ARG, "evam_pp_run: dst plane %dx%d exceeds 2 GiB", DW, DH);
+    const Knobs& kn = h->knobs;
 
     // ---- validate sources ----
     for (int i = 0; i < n_srcs; i++) {
@@ -2536,11 +2379,15 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
             return fail(EVAM_PP_ERR_INVALID_ARG, "evam_pp_run: srcs[%d] 4:2:0 frame must have even size (%dx%d)", i, s.width, s.height);
         for (int p = 0; p < fmt_nplanes(f); p++) {
             const int row_bytes = p == 0 ? s.width * fmt_bpp(f) : (f == kNV12 ? s.width : s.width / 2);
+            const int rows = p == 0 ? s.height : s.height / 2;
             if (!s.planes[p]) return fail(EVAM_PP_ERR_INVALID_ARG, "evam_pp_run: srcs[%d].planes[%d] is NULL", i, p);
             if (((uintptr_t)s.planes[p] & 15) || (s.pitch[p] & 15))
                 return fail(EVAM_PP_ERR_ALIGNMENT, "evam_pp_run: srcs[%d] plane %d pointer/pitch (%d) not 16-byte aligned", i, p, s.pitch[p]);
             if (s.pitch[p] < row_bytes)
                 return fail(EVAM_PP_ERR_INVALID_ARG, "evam_pp_run: srcs[%d] plane %d pitch %d < row bytes %d", i, p, s.pitch[p], row_bytes);
+            // the kernels address a plane through buffer resources with 32-bit byte offsets
+            if ((int64_t)s.pitch[p] * rows > INT32_MAX)
+                return fail(EVAM_PP_ERR_INVALID_ARG, "evam_pp_run: srcs[%d] plane %d (%d x %d B) exceeds 2 GiB", i, p, rows, s.pitch[p]);
         }
     }
 
@@ -2552,6 +2399,7 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
     int count[4] = {0, 0, 0, 0};
     int rep[4] = {-1, -1, -1, -1};
     int max_cw[4] = {0, 0, 0, 0};
+    uint32_t x0_mask[4] = {0, 0, 0, 0};  // crop origins x0 mod 32 present (wave-kernel staging bound)
     bool uniform[4] = {true, true, true, true};
     for (int i = 0; i < n_items; i++) {
         const evam_roi* r = items ? &items[i] : nullptr;
@@ -2571,28 +2419,36 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
                         i, r ? r->x : 0, r ? r->y : 0, r ? r->w : 0, r ? r->h : 0, s.width, s.height);
         count[f]++;
         max_cw[f] = std::max(max_cw[f], g.cw);
+        x0_mask[f] |= 1u << (g.x0 & 31);
         if (rep[f] < 0) rep[f] = i;
         else if (g.cw != geo[rep[f]].cw || g.ch != geo[rep[f]].ch) uniform[f] = false;  // geometry = f(cw, ch)
     }
+    // item indices grouped by format, in call order within a format
+    std::vector<int>& members = h->sc_members;
+    members.resize(n_items);
+    int mfirst[5] = {0, 0, 0, 0, 0};
+    for (int f = 0; f < 4; f++) mfirst[f + 1] = mfirst[f] + count[f];
+    {
+        int fill_at[4] = {mfirst[0], mfirst[1], mfirst[2], mfirst[3]};
+        for (int i = 0; i < n_items; i++) members[fill_at[fmt[i]]++] = i;
+    }
 
     // ---- per format group: kernel choice ----
-    //   uniform geometry        -> staged / row kernels, host-built tables, per-item ItemDesc
+    //   uniform geometry        -> staged / wave / row kernels: host-built tables, items in kernel arguments
     //   per-item geometry       -> ROI kernel: raw ROI rect + source (RoiRec), geometry resolved on the device
-    //   ROI plan impossible     -> generic kernel, per-item ItemDesc
+    //   ROI plan impossible     -> generic kernel, per-item ItemDesc in the descriptor block
     enum { kPathNone, kPathUniform, kPathRoi, kPathGeneric };
-    const bool rows_enabled = env_int("EVAM_PP_ROWS", 1) != 0;
-    const bool roi_enabled = env_int("EVAM_PP_ROI", 1) != 0;
     int path[4];
     QParams qp[4];
     int qlds[4] = {0, 0, 0, 0};
-    bool any_desc = false, any_roi = false;
+    bool any_generic = false, any_roi = false;
     for (int f = 0; f < 4; f++) {
         path[f] = kPathNone;
         if (!count[f]) continue;
-        if (uniform[f] && rows_enabled) path[f] = kPathUniform;
-        else if (roi_enabled && plan_roi(DW, DH, cfg->out_dtype, row_bytes_bound(f, max_cw[f]), qp[f], qlds[f])) path[f] = kPathRoi;
+        if (uniform[f] && kn.rows) path[f] = kPathUniform;
+        else if (kn.roi && plan_roi(DW, DH, cfg->out_dtype, row_bytes_bound(f, max_cw[f]), kn, qp[f], qlds[f])) path[f] = kPathRoi;
         else path[f] = kPathGeneric;
-        any_desc |= path[f] != kPathRoi;
+        any_generic |= path[f] == kPathGeneric;
         any_roi |= path[f] == kPathRoi;
     }
     // Full geometry on the host only where something consumes it.
@@ -2601,6 +2457,7 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
     for (int i = 0; i < n_items; i++) {
         const int f = fmt[i];
         if (!all_geo && path[f] == kPathRoi) continue;
+        if (!all_geo && path[f] == kPathUniform && i != rep[f]) continue;  // same crop size: rep's geometry
         Geom& g = geo[i];
         const evam_roi* r = items ? &items[i] : nullptr;
         const evam_image& s = srcs[items ? r->src_index : i];
@@ -2617,14 +2474,15 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
         if (h->opt_stats) src_bytes += item_src_bytes(f, g, DW, DH);
     }
 
-    // ---- descriptor block ----
-    // [LUT][ItemDesc x (items of uniform/generic groups)][per uniform group: XTab x DW, YTab x DH]
+    // ---- descriptor block (device-resident, re-uploaded only when its bytes change) ----
+    // [LUT][ItemDesc x (items of generic groups)][per uniform group: XTab x DW, YTab x DH]
+    // Everything in it is a function of the configuration and the geometry, not of the frames, so a new
+    // set of frames of the same geometry reuses the resident block.
     size_t nbytes = kLutBytes;
-    size_t desc_off = nbytes;
+    const size_t desc_off = nbytes;
     int n_desc = 0;
-    if (any_desc)
-        for (int f = 0; f < 4; f++)
-            if (path[f] == kPathUniform || path[f] == kPathGeneric) n_desc += count[f];
+    for (int f = 0; f < 4; f++)
+        if (path[f] == kPathGeneric) n_desc += count[f];
     nbytes += sizeof(ItemDesc) * (size_t)n_desc;
     size_t tab_off[4] = {0, 0, 0, 0};
     for (int f = 0; f < 4; f++) {
@@ -2661,32 +2519,33 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
         memset(blk, 0, kLutBytes);
     }
     int first[4] = {0, 0, 0, 0};
-    if (any_desc) {
+    {
         ItemDesc* desc = reinterpret_cast<ItemDesc*>(blk + desc_off);
         int order = 0;
         for (int f = 0; f < 4; f++) {
-            if (path[f] != kPathUniform && path[f] != kPathGeneric) continue;
-            first[f] = order;
-            for (int i = 0; i < n_items; i++) {
-                if (fmt[i] != f) continue;
-                const evam_image& s = srcs[items ? items[i].src_index : i];
-                ItemDesc& d = desc[order++];
-                for (int p = 0; p < 3; p++) { d.plane[p] = s.planes[p]; d.pitch[p] = s.pitch[p]; }
-                const Geom& g = geo[i];
-                d.x0 = g.x0; d.y0 = g.y0; d.cw = g.cw; d.ch = g.ch;
-                d.rw = g.rw; d.rh = g.rh; d.ox = g.ox; d.oy = g.oy;
-                d.index = i;  // the slot offset / stride are launch parameters: the block survives clip-ring steps
-                d.pad_ = 0;
-                d.scale_x = 1. / ((double)g.rw / g.cw);
-                d.scale_y = 1. / ((double)g.rh / g.ch);
-            }
-            if (path[f] == kPathUniform) {
+            if (path[f] == kPathGeneric) {
+                first[f] = order;
+                for (int m = mfirst[f]; m < mfirst[f + 1]; m++) {
+                    const int i = members[m];
+                    const evam_image& s = srcs[items ? items[i].src_index : i];
+                    ItemDesc& d = desc[order++];
+                    for (int p = 0; p < 3; p++) { d.plane[p] = s.planes[p]; d.pitch[p] = s.pitch[p]; }
+                    const Geom& g = geo[i];
+                    d.x0 = g.x0; d.y0 = g.y0; d.cw = g.cw; d.ch = g.ch;
+                    d.rw = g.rw; d.rh = g.rh; d.ox = g.ox; d.oy = g.oy;
+                    d.index = i;  // the slot offset / stride are launch parameters: the block survives clip-ring steps
+                    d.pad_ = 0;
+                    d.scale_x = 1. / ((double)g.rw / g.cw);
+                    d.scale_y = 1. / ((double)g.rh / g.ch);
+                }
+            } else if (path[f] == kPathUniform) {
                 XTab* xt = reinterpret_cast<XTab*>(blk + tab_off[f]);
                 YTab* yt = reinterpret_cast<YTab*>(xt + DW);
                 build_tables(geo[rep[f]], DW, DH, h->tab_cache, xt, yt);
             }
         }
     }
+    (void)any_generic;
     HIP_TRY(hipSetDevice(h->device));
     uint8_t* dyn = nullptr;
     const uint8_t* d_dyn = nullptr;
@@ -2695,32 +2554,15 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
         // Launch order: largest estimated work first (counting sort on 64 buckets of the staged
         // bytes, crop width x touched rows). Workgroups are dispatched in order as slots free, so
         // the long ROIs start first and the short ones fill the tail.
-        const bool sort = env_int("EVAM_PP_ROI_SORT", 1) != 0;
-        const bool xcd_group = env_int("EVAM_PP_ROI_XCD", 0) != 0;
+        const bool sort = kn.roi_sort != 0;
+        const bool xcd_group = kn.roi_xcd != 0;
         std::vector<int>& bucket = h->sc_bucket;
         bucket.resize(n_items);
         for (int f = 0; f < 4; f++) {
             if (path[f] != kPathRoi) continue;
             RoiRec* rr = reinterpret_cast<RoiRec*>(dyn + rec_off[f]);
-            int64_t maxw = 1;
-            if (sort)
-                for (int i = 0; i < n_items; i++) {
-                    if (fmt[i] != f) continue;
-                    const int64_t w = (int64_t)geo[i].cw * std::min(geo[i].ch, 2 * DH);
-                    maxw = std::max(maxw, w);
-                }
-            int start[65] = {0};
-            for (int i = 0; i < n_items; i++) {
-                if (fmt[i] != f) continue;
-                const int64_t w = (int64_t)geo[i].cw * std::min(geo[i].ch, 2 * DH);
-                bucket[i] = sort ? 63 - (int)(w * 63 / maxw) : 0;  // 0 = largest
-                start[bucket[i] + 1]++;
-            }
-            for (int b = 0; b < 64; b++) start[b + 1] += start[b];
             std::vector<int>& ord = h->sc_order;
-            ord.assign(start[64], 0);
-            for (int i = 0; i < n_items; i++)
-                if (fmt[i] == f) ord[start[bucket[i]]++] = i;
+            roi_largest_first(members.data() + mfirst[f], count[f], geo.data(), DH, sort, bucket.data(), ord);
             if (xcd_group) {
                 // Record p runs on XCD p % 8: deal each frame's ROIs (frame s -> XCD s % 8, largest
                 // first within the XCD) so overlapping crops of one frame share one L2.
@@ -2757,10 +2599,20 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
     int launches = 0;
     const uint32_t fill = (uint32_t)cfg->fill[0] | ((uint32_t)cfg->fill[1] << 8) | ((uint32_t)cfg->fill[2] << 16);
     const int color_rgb = cfg->color_order == EVAM_COLOR_RGB;
+    const float* lut_d = reinterpret_cast<const float*>(d_block);
+    // Kernel-argument items of one uniform launch: members [m0, m0 + n) of format group f.
+    auto fill_args = [&](ItemArg* a, int m0, int n) {
+        for (int k = 0; k < n; k++) {
+            const int i = members[m0 + k];
+            const evam_image& s = srcs[items ? items[i].src_index : i];
+            for (int p = 0; p < 3; p++) { a[k].plane[p] = s.planes[p]; a[k].pitch[p] = s.pitch[p]; }
+            a[k].x0 = geo[i].x0;
+            a[k].y0 = geo[i].y0;
+            a[k].index = i;
+        }
+    };
     for (int f = 0; f < 4; f++) {
         if (path[f] == kPathNone) continue;
-        const ItemDesc* items_d = reinterpret_cast<const ItemDesc*>(d_block + desc_off) + first[f];
-        const float* lut_d = reinterpret_cast<const float*>(d_block);
         if (path[f] == kPathRoi) {
             QParams q = qp[f];
             q.recs = reinterpret_cast<const RoiRec*>(d_dyn + rec_off[f]);
@@ -2772,17 +2624,20 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
             q.slot_stride = dst->slot_stride;
             q.color_rgb = color_rgb;
             q.fill = fill;
-            q.ablate = env_int("EVAM_PP_ABLATE", 0);
+            q.ablate = kn.ablate;
             const int64_t grid = (int64_t)count[f] * q.tiles_per_item;
             if (grid > 0x7FFFFFFF) return fail(EVAM_PP_ERR_INVALID_ARG, "evam_pp_run: too many tiles");
-            hipError_t e = launch_roi(f, cfg->out_dtype, q, (int)grid, qlds[f], h->stream);
+            hipError_t e = launch_roi(f, cfg->out_dtype, kn.roi_px, q, (int)grid, qlds[f], h->stream);
             if (e != hipSuccess) return fail(EVAM_PP_ERR_HIP, "kernel launch failed: %s", hipGetErrorString(e));
             launches++;
             continue;
         }
         if (path[f] == kPathUniform) {
             const Geom& g0 = geo[rep[f]];
-            if (env_int("EVAM_PP_WAVE", 1)) {
+            const XTab* xt_d = reinterpret_cast<const XTab*>(d_block + tab_off[f]);
+            const YTab* yt_d = reinterpret_cast<const YTab*>(xt_d + DW);
+            const int per_launch = std::min(count[f], kArgItems);
+            if (kn.wave) {
                 WParams w{};
                 int px = 0, lds = 0, grid = 0;
                 bool reuse = false;
@@ -2790,31 +2645,38 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
                 // The wave kernel wins where consecutive output rows share source rows (vertical
                 // upscale: REUSE); for downscales the staged kernel's deeper shared staging is faster.
                 if (plan_wave(f, g0, DW, DH, count[f], cfg->out_dtype, h->n_cu, hx,
-                              reinterpret_cast<const YTab*>(hx + DW), w, px, reuse, lds, grid) &&
-                    (reuse || env_int("EVAM_PP_WAVE", 1) == 2)) {
-                    w.items = items_d;
+                              reinterpret_cast<const YTab*>(hx + DW), x0_mask[f], kn, w, px, reuse, lds, grid) &&
+                    (reuse || kn.wave == 2)) {
+                    w.ox = g0.ox;
+                    w.rw = g0.rw;
                     w.lut = lut_d;
-                    w.xtab = reinterpret_cast<const XTab*>(d_block + tab_off[f]);
-                    w.ytab = reinterpret_cast<const YTab*>(w.xtab + DW);
+                    w.xtab = xt_d;
+                    w.ytab = yt_d;
                     w.dst = dst->data;
                     w.slot_offset = dst->slot_offset;
                     w.slot_stride = dst->slot_stride;
                     w.color_rgb = color_rgb;
                     w.fill = fill;
-                    w.ablate = env_int("EVAM_PP_ABLATE", 0);
-                    hipError_t e = launch_wave(f, cfg->out_dtype, px, reuse, w, grid, lds, h->stream);
-                    if (e != hipSuccess) return fail(EVAM_PP_ERR_HIP, "kernel launch failed: %s", hipGetErrorString(e));
-                    launches++;
+                    w.ablate = kn.ablate;
+                    for (int m0 = mfirst[f]; m0 < mfirst[f + 1]; m0 += kArgItems) {
+                        const int n = std::min(kArgItems, mfirst[f + 1] - m0);
+                        fill_args(w.items, m0, n);
+                        hipError_t e = launch_wave(f, cfg->out_dtype, px, reuse, w, n * w.tiles_per_item, lds, h->stream);
+                        if (e != hipSuccess) return fail(EVAM_PP_ERR_HIP, "kernel launch failed: %s", hipGetErrorString(e));
+                        launches++;
+                    }
                     continue;
                 }
             }
-            const int nsegx = env_int("EVAM_PP_STAGED", 1) ? staged_nsegx(f, (double)g0.cw / g0.rw) : 0;
+            int nsegx = kn.staged ? staged_nsegx(f, (double)g0.cw / g0.rw, kStageRows, kSlot) : 0;
+            if (nsegx && kn.nsegx > 0 && kn.nsegx < nsegx && kStageRows % (4 / kn.nsegx) == 0) nsegx = kn.nsegx;
             if (nsegx) {
                 SParams sp{};
-                sp.items = items_d;
+                sp.ox = g0.ox;
+                sp.rw = g0.rw;
                 sp.lut = lut_d;
-                sp.xtab = reinterpret_cast<const XTab*>(d_block + tab_off[f]);
-                sp.ytab = reinterpret_cast<const YTab*>(sp.xtab + DW);
+                sp.xtab = xt_d;
+                sp.ytab = yt_d;
                 sp.dst = dst->data;
                 sp.slot_offset = dst->slot_offset;
                 sp.slot_stride = dst->slot_stride;
@@ -2825,10 +2687,10 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
                 // 8 workgroups on every CU (a whole clip-ring step is only 32 x 224 x 224 pixels).
                 // At most 16 rows: C4 (tw 128) runs 3-7 % faster at 16 than at 32 (profiles/r01ad_sweep_th*.txt).
                 int th = std::max(kStageRows, std::min(16, 4096 / tw));
-                const int64_t cols = (int64_t)count[f] * sp.tiles_x;
+                const int64_t cols = (int64_t)per_launch * sp.tiles_x;
                 const int64_t want = 8 * (int64_t)h->n_cu;
                 if (cols * ((DH + th - 1) / th) < want) th = (int)std::max<int64_t>(kStageRows, cols * DH / want);
-                sp.TH = std::max(1, std::min(DH, env_int("EVAM_PP_TH", th)));
+                sp.TH = std::max(1, std::min(DH, kn.th > 0 ? kn.th : th));
                 sp.TH = (sp.TH + kStageRows - 1) / kStageRows * kStageRows;
                 sp.tiles_per_item = sp.tiles_x * ((DH + sp.TH - 1) / sp.TH);
                 const int np = f == kI420 ? 3 : (f == kNV12 ? 2 : 1);
@@ -2836,24 +2698,29 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
                 sp.buf_bytes = 2 * kStageRows * np * kSlot;
                 sp.color_rgb = color_rgb;
                 sp.fill = fill;
-                sp.ablate = env_int("EVAM_PP_ABLATE", 0);
-                // XCD-contiguous tiles: C2 -1.4 %, C4 -3 % kernel time; a grid of one workgroup round or
-                // less (C5) gains nothing (profiles/r01ae_sweep_xcd.txt). EVAM_PP_XCD=0/1 forces it.
-                sp.xcd_remap = env_int("EVAM_PP_XCD", (int)(count[f] * (int64_t)sp.tiles_per_item >= 8 * (int64_t)h->n_cu));
-                const int64_t grid = (int64_t)count[f] * sp.tiles_per_item;
-                if (grid > 0x7FFFFFFF) return fail(EVAM_PP_ERR_INVALID_ARG, "evam_pp_run: too many tiles");
+                sp.ablate = kn.ablate;
                 const int lds = sp.offBuf + 2 * sp.buf_bytes;
-                hipError_t e = launch_staged(f, cfg->out_dtype, nsegx, sp, (int)grid, lds, h->stream);
-                if (e != hipSuccess) return fail(EVAM_PP_ERR_HIP, "kernel launch failed: %s", hipGetErrorString(e));
-                launches++;
+                for (int m0 = mfirst[f]; m0 < mfirst[f + 1]; m0 += kArgItems) {
+                    const int n = std::min(kArgItems, mfirst[f + 1] - m0);
+                    fill_args(sp.items, m0, n);
+                    const int64_t grid = (int64_t)n * sp.tiles_per_item;
+                    if (grid > 0x7FFFFFFF) return fail(EVAM_PP_ERR_INVALID_ARG, "evam_pp_run: too many tiles");
+                    // XCD-contiguous tiles: C2 -1.4 %, C4 -3 % kernel time; a grid of one workgroup round or
+                    // less (C5) gains nothing (profiles/r01ae_sweep_xcd.txt). EVAM_PP_XCD=0/1 forces it.
+                    sp.xcd_remap = kn.xcd >= 0 ? kn.xcd : (int)(grid >= 8 * (int64_t)h->n_cu);
+                    hipError_t e = launch_staged(f, cfg->out_dtype, nsegx, sp, (int)grid, lds, h->stream);
+                    if (e != hipSuccess) return fail(EVAM_PP_ERR_HIP, "kernel launch failed: %s", hipGetErrorString(e));
+                    launches++;
+                }
                 continue;
             }
-            const RowCfg rc = choose_row_tiles(DW, DH);
+            const RowCfg rc = choose_row_tiles(DW, DH, kn);
             RParams r{};
-            r.items = items_d;
+            r.ox = g0.ox;
+            r.rw = g0.rw;
             r.lut = lut_d;
-            r.xtab = reinterpret_cast<const XTab*>(d_block + tab_off[f]);
-            r.ytab = reinterpret_cast<const YTab*>(r.xtab + DW);
+            r.xtab = xt_d;
+            r.ytab = yt_d;
             r.dst = dst->data;
             r.slot_offset = dst->slot_offset;
             r.slot_stride = dst->slot_stride;
@@ -2864,16 +2731,21 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
             r.nsegx = rc.TW / 64;
             r.color_rgb = color_rgb;
             r.fill = fill;
-            r.ablate = env_int("EVAM_PP_ABLATE", 0);
-            const int64_t grid = (int64_t)count[f] * r.tiles_per_item;
-            if (grid > 0x7FFFFFFF) return fail(EVAM_PP_ERR_INVALID_ARG, "evam_pp_run: too many tiles");
+            r.ablate = kn.ablate;
             const int lds = cfg->out_dtype == EVAM_DTYPE_F32 ? kLutBytes : 0;
-            hipError_t e = launch_rows(f, cfg->out_dtype, r, (int)grid, lds, h->stream);
-            if (e != hipSuccess) return fail(EVAM_PP_ERR_HIP, "kernel launch failed: %s", hipGetErrorString(e));
-            launches++;
+            for (int m0 = mfirst[f]; m0 < mfirst[f + 1]; m0 += kArgItems) {
+                const int n = std::min(kArgItems, mfirst[f + 1] - m0);
+                fill_args(r.items, m0, n);
+                const int64_t grid = (int64_t)n * r.tiles_per_item;
+                if (grid > 0x7FFFFFFF) return fail(EVAM_PP_ERR_INVALID_ARG, "evam_pp_run: too many tiles");
+                hipError_t e = launch_rows(f, cfg->out_dtype, r, (int)grid, lds, h->stream);
+                if (e != hipSuccess) return fail(EVAM_PP_ERR_HIP, "kernel launch failed: %s", hipGetErrorString(e));
+                launches++;
+            }
             continue;
         }
-        const TileCfg t = choose_tiles(DW, DH, cfg->out_dtype);
+        const ItemDesc* items_d = reinterpret_cast<const ItemDesc*>(d_block + desc_off) + first[f];
+        const TileCfg t = choose_tiles(DW, DH, cfg->out_dtype, kn);
         KParams p{};
         p.items = items_d;
         p.lut = lut_d;
@@ -2892,7 +2764,7 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
         p.offCol = t.offCol; p.offRow = t.offRow;
         p.color_rgb = color_rgb;
         p.fill = fill;
-        p.ablate = env_int("EVAM_PP_ABLATE", 0);
+        p.ablate = kn.ablate;
         const int lds = t.lds;
         if (lds > 64 * 1024) {
             hipError_t e = hipSuccess;
@@ -2918,7 +2790,7 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
     h->stats.n_items = n_items;
     h->stats.n_launches = launches;
     h->stats.src_bytes = h->opt_stats ? src_bytes : 0;
-    h->stats.dst_bytes = (int64_t)n_items * plane * 3 * (cfg->out_dtype == EVAM_DTYPE_F32 ? 4 : 1);
+    h->stats.dst_bytes = (int64_t)n_items * plane * 3 * esz;
     return EVAM_PP_OK;
 }
 

@@ -297,6 +297,17 @@ def _backend_of(el: Element) -> str:
     raise PreProcError(N.ERR_UNSUPPORTED, f"{el.name or el.factory}: unknown pre-process-backend {b!r}")
 
 
+def roi_inside(x: int, y: int, w: int, h: int, W: int, H: int) -> bool:
+    """True when a detected box has a non-empty intersection with its W x H frame.
+
+    Boxes that fail are skipped by gvaclassify stages: for ``evam_roi`` a rect with ``w <= 0`` or
+    ``h <= 0`` means "the whole frame", and a rect that clips to nothing is an error for the whole call.
+    """
+    if w <= 0 or h <= 0:
+        return False
+    return min(x + w, W) - max(x, 0) > 0 and min(y + h, H) - max(y, 0) > 0
+
+
 class _InferenceStage:
     """Common part of gvadetect / gvaclassify: interval gating, model lookup, HIP pre-processor."""
 
@@ -376,6 +387,8 @@ class ClassifyStage(_InferenceStage):
             frames.append(img)
             for r in fr.regions:
                 if self.object_class is None or r.label in self.object_class:
+                    if not roi_inside(r.x, r.y, r.w, r.h, img.width, img.height):
+                        continue  # degenerate box: the C ABI would read w/h <= 0 as "full frame"
                     rois.append(Roi(idx, r.x, r.y, r.w, r.h))
                     owners.append(r)
         if not rois:

@@ -11,7 +11,8 @@ path exports (§8 a11). Results are emitted in the two JSON shapes the reference
 
 Pixel rectangles follow DL Streamer's region-of-interest rule [3P]:
 ``x = floor(x_min * W + 0.5)`` and ``w = floor((x_max - x_min) * W + 0.5)``, on boxes clipped to
-[0, 1]. All three sample rows of ``charts/README.md`` pin this rule (``tests/test_postproc.py``).
+[0, 1]. All three sample rows of ``charts/README.md`` pin this rule
+(``tests/test_pipeline_server.py::test_readme_metadata_rows``, fixture ``tests/golden/readme_metadata.jsonl``).
 """
 from __future__ import annotations
 

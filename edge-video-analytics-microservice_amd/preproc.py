@@ -119,9 +119,18 @@ class RoiBatch:
         if isinstance(rois, np.ndarray):
             a = rois
         else:
-            a = np.array([(r.src_index, r.x, r.y, r.w, r.h) if isinstance(r, Roi) else tuple(r) for r in rois],
-                         dtype=np.int32).reshape(-1, 5)
+            a = np.array([(r.src_index, r.x, r.y, r.w, r.h) if isinstance(r, Roi) else tuple(r) for r in rois])
+            if a.size == 0:
+                a = np.zeros((0, 5), np.int32)
+        # evam_roi is int32: refuse silent truncation (floats) and wrap-around (out-of-range int64)
+        if a.dtype != np.int32:
+            if a.size and not np.issubdtype(a.dtype, np.integer):
+                raise PreProcError(N.ERR_INVALID_ARG, f"ROI array must hold integers, got dtype {a.dtype}")
+            if a.size and (a.min() < -2**31 or a.max() > 2**31 - 1):
+                raise PreProcError(N.ERR_INVALID_ARG, "ROI values outside the int32 range")
         self.array = np.ascontiguousarray(a, dtype=np.int32)
+        if self.array.ndim == 1 and self.array.size == 0:
+            self.array = self.array.reshape(0, 5)
         if self.array.ndim != 2 or self.array.shape[1] != 5:
             raise PreProcError(N.ERR_INVALID_ARG, f"ROI array must be [n, 5] int32, got {self.array.shape}")
         self.c_ptr = self.array.ctypes.data_as(ctypes.POINTER(N.EvamRoi))
@@ -168,6 +177,12 @@ class PreProcInfo:
                 fv = pad["fill_value"]
                 info.fill = tuple(int(v) for v in (fv if isinstance(fv, (list, tuple)) else [fv] * 3))
         return info
+
+    def cache_key(self, out_dtype: int):
+        """Hashable value of every field that reaches the C struct (lists are normalised to tuples)."""
+        t = lambda v: tuple(v) if isinstance(v, list) else v  # noqa: E731
+        return (self.resize, self.crop, self.color_space, t(self.range), t(self.mean), t(self.std),
+                self.placement, t(self.fill), out_dtype)
 
     def resize_mode(self) -> int:
         if self.resize in ("no", "no-aspect-ratio", None):
@@ -333,10 +348,15 @@ class HipPreProcessor:
         info = info or self._default_info
         batch = srcs if isinstance(srcs, ImageBatch) else ImageBatch(srcs)
         t, dt = self._tensor_desc(out, slot_offset, slot_stride)
-        cached = self._cfg_cache.get((id(info), dt))
-        if cached is None or cached[0] is not info:
-            cached = (info, ctypes.byref(info.to_c(dt)))
-            self._cfg_cache[(id(info), dt)] = cached
+        # keyed on the field values (PreProcInfo is mutable; a field changed after a call must not reuse
+        # a stale struct), bounded so callers building a new info per call cannot grow it without limit
+        key = info.cache_key(dt)
+        cached = self._cfg_cache.get(key)
+        if cached is None:
+            if len(self._cfg_cache) >= 64:
+                self._cfg_cache.clear()
+            cached = ctypes.byref(info.to_c(dt))
+            self._cfg_cache[key] = cached
         if rois is not None:
             rb = rois if isinstance(rois, RoiBatch) else RoiBatch(rois)
             n_items = len(rb)
@@ -348,7 +368,7 @@ class HipPreProcessor:
             items_p = None
         xf = (N.EvamTransform * n_items)() if want_transform else None
         self._bind_stream()
-        rc = self._run(self._h, batch.c_array, len(batch), items_p, n_items, cached[1], ctypes.byref(t), xf)
+        rc = self._run(self._h, batch.c_array, len(batch), items_p, n_items, cached, ctypes.byref(t), xf)
         if rc:
             N.check(self._lib, rc)
         if not want_transform:

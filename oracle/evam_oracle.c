@@ -227,7 +227,10 @@ int orc_item_geometry(int fourcc, int W, int H, int x, int y, int w, int h, int 
         x0 = 0; y0 = 0; x1 = W; y1 = H;
     } else {
         x0 = clampi(x, 0, W); y0 = clampi(y, 0, H);
-        x1 = clampi(x + w, 0, W); y1 = clampi(y + h, 0, H);
+        /* x + w in 64 bits: caller-supplied int32 rects may overflow int */
+        long long xe = (long long)x + w, ye = (long long)y + h;
+        x1 = xe < 0 ? 0 : (xe > W ? W : (int)xe);
+        y1 = ye < 0 ? 0 : (ye > H ? H : (int)ye);
         if (fourcc == ORC_NV12 || fourcc == ORC_I420) {
             x0 &= ~1; y0 &= ~1;
             x1 = (x1 + 1) & ~1; if (x1 > W) x1 = W;

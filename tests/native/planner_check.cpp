@@ -1,0 +1,268 @@
+// planner_check.cpp — host-only checks of the planner arithmetic libevam_pp.so shares with its kernels
+// (edge-video-analytics-microservice_amd/csrc/evam_geom.h), built and run under AddressSanitizer +
+// UBSan by tests/test_native_asan.py, together with the C oracle (oracle/evam_oracle.c) exercised on
+// tightly allocated frames so any out-of-bounds read in it is caught too.
+//
+// TEST INFRASTRUCTURE ONLY: links the oracle as the checker of the geometry rules.
+//
+// Every check draws its cases from a fixed-seed generator; a failure prints the case and exits 1.
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <random>
+#include <vector>
+
+#include "../../edge-video-analytics-microservice_amd/csrc/evam_geom.h"
+
+extern "C" {
+typedef struct { int x0, y0, cw, ch, rw, rh, ox, oy; } orc_geom;
+int orc_item_geometry(int fourcc, int W, int H, int x, int y, int w, int h, int mode, int placement, int DW,
+                      int DH, orc_geom* g);
+void orc_linear_table(int ssize, int dsize, int is_x, int32_t* ofs, int16_t* c0, int16_t* c1);
+int orc_preprocess_item(int fourcc, const uint8_t* const planes[3], const int pitch[3], int W, int H, int x, int y,
+                        int w, int h, int mode, int placement, int color_rgb, int out_f32, const float* lut,
+                        const uint8_t fill[3], void* dst, int slot, int DW, int DH, int32_t* geom_out);
+void orc_norm_lut(int norm_flags, const float range[2], const float mean[3], const float std_[3], float* lut);
+}
+
+using namespace evam;
+
+static const int kFourcc[4] = {EVAM_FOURCC_NV12, EVAM_FOURCC_I420, EVAM_FOURCC_BGRX, EVAM_FOURCC_BGR};
+static std::mt19937_64 rng(20261016);
+static int uni(int lo, int hi) { return std::uniform_int_distribution<int>(lo, hi)(rng); }
+static int failures = 0;
+
+#define CHECK(cond, ...)                                                       \
+    do {                                                                       \
+        if (!(cond)) {                                                         \
+            fprintf(stderr, "FAIL %s:%d: %s | ", __FILE__, __LINE__, #cond);   \
+            fprintf(stderr, __VA_ARGS__);                                      \
+            fprintf(stderr, "\n");                                             \
+            if (++failures > 20) exit(1);                                      \
+        }                                                                      \
+    } while (0)
+
+// A rect drawn from the interesting classes: inside, straddling, outside, degenerate, int32 extremes.
+static void random_rect(int W, int H, int& x, int& y, int& w, int& h) {
+    switch (uni(0, 9)) {
+    case 0: x = uni(INT32_MIN / 2, INT32_MAX); y = uni(INT32_MIN / 2, INT32_MAX); w = uni(-5, INT32_MAX); h = uni(-5, INT32_MAX); break;
+    case 1: x = INT32_MAX - uni(0, 3); y = uni(0, H); w = INT32_MAX; h = uni(1, 50); break;
+    case 2: x = uni(-3 * W, 3 * W); y = uni(-3 * H, 3 * H); w = uni(-2, 4 * W); h = uni(-2, 4 * H); break;
+    case 3: x = uni(0, W); y = uni(0, H); w = 0; h = uni(-3, 3); break;
+    default: x = uni(-20, W); y = uni(-20, H); w = uni(1, W + 40); h = uni(1, H + 40); break;
+    }
+}
+
+static void check_geometry() {
+    int n = 0, empty = 0;
+    for (int it = 0; it < 200000; it++) {
+        const int f = uni(0, 3);
+        const bool yuv = f == kNV12 || f == kI420;
+        int W = uni(1, 5000), H = uni(1, 3000);
+        if (yuv) { W = (W + 1) & ~1; H = (H + 1) & ~1; }
+        int x, y, w, h;
+        random_rect(W, H, x, y, w, h);
+        const int mode = uni(0, 2), placement = uni(0, 1), DW = uni(1, 1024), DH = uni(1, 1024);
+        const bool has = uni(0, 7) != 0;
+        Geom g{};
+        orc_geom o{};
+        const int rc = roi_geometry(f, W, H, has, x, y, w, h, mode, placement, DW, DH, g);
+        const int ro = orc_item_geometry(kFourcc[f], W, H, has ? x : 0, has ? y : 0, has ? w : 0, has ? h : 0, mode,
+                                         placement, DW, DH, &o);
+        CHECK((rc != 0) == (ro != 0), "f=%d %dx%d rect(%d,%d,%d,%d) rc %d oracle %d", f, W, H, x, y, w, h, rc, ro);
+        if (rc || ro) { empty++; continue; }
+        n++;
+        CHECK(memcmp(&g, &o, sizeof(g)) == 0, "f=%d %dx%d rect(%d,%d,%d,%d) mode %d: (%d %d %d %d %d %d %d %d) vs oracle "
+              "(%d %d %d %d %d %d %d %d)", f, W, H, x, y, w, h, mode, g.x0, g.y0, g.cw, g.ch, g.rw, g.rh, g.ox, g.oy,
+              o.x0, o.y0, o.cw, o.ch, o.rw, o.rh, o.ox, o.oy);
+        CHECK(g.x0 >= 0 && g.y0 >= 0 && g.x0 + g.cw <= W && g.y0 + g.ch <= H && g.cw > 0 && g.ch > 0,
+              "crop outside the frame");
+        if (yuv) CHECK(!((g.x0 | g.y0) & 1), "4:2:0 crop origin odd");
+    }
+    printf("geometry: %d clipped rects equal to the oracle's, %d empty agreed\n", n, empty);
+}
+
+static void check_linear_tables() {
+    std::vector<int32_t> ofs;
+    std::vector<int16_t> c0, c1;
+    for (int it = 0; it < 3000; it++) {
+        const int ss = uni(1, 4000), ds = uni(1, 2000), is_x = uni(0, 1);
+        ofs.resize(ds); c0.resize(ds); c1.resize(ds);
+        orc_linear_table(ss, ds, is_x, ofs.data(), c0.data(), c1.data());
+        const double scale = 1. / ((double)ds / ss);
+        for (int d = 0; d < ds; d++) {
+            int s, a, b;
+            linear_coef(d, scale, ss, is_x != 0, s, a, b);
+            CHECK(s == ofs[d] && a == c0[d] && b == c1[d], "%d->%d x=%d d=%d: (%d,%d,%d) vs (%d,%d,%d)", ss, ds, is_x, d,
+                  s, a, b, ofs[d], c0[d], c1[d]);
+            if (is_x) CHECK(s >= 0 && s <= ss - 1, "x tap outside the row");
+        }
+    }
+    printf("linear tables: 3000 axes equal to the oracle's\n");
+}
+
+// The ROI kernel stages, per output row, the footprint item_footprint gives; it must cover every tap of
+// every visible column and be the minimal 16-byte-aligned window; the host sizes its LDS buffer with
+// row_bytes_bound, which must bound the staged bytes.
+static void check_footprints() {
+    for (int it = 0; it < 20000; it++) {
+        const int f = uni(0, 3), bpp = fmt_bpp(f);
+        const bool yuv = f == kNV12 || f == kI420;
+        int W = uni(2, 2000) & ~1, H = uni(2, 1200) & ~1;
+        int x, y, w, h;
+        random_rect(W, H, x, y, w, h);
+        const int mode = uni(0, 2), DW = uni(1, 600), DH = uni(1, 400);
+        Geom g{};
+        if (roi_geometry(f, W, H, true, x, y, w, h, mode, uni(0, 1), DW, DH, g)) continue;
+        const double scx = 1. / ((double)g.rw / g.cw);
+        int fsY, nY, fsC, nC;
+        item_footprint(f, bpp, g.x0, g.cw, g.rw, g.ox, scx, DW, fsY, nY, fsC, nC);
+        int lo = INT32_MAX, hi = -1;
+        for (int X = std::max(0, g.ox); X < std::min(DW, g.ox + g.rw); X++) {
+            int s, a, b;
+            linear_coef(X - g.ox, scx, g.cw, true, s, a, b);
+            lo = std::min(lo, g.x0 + s);
+            hi = std::max(hi, g.x0 + std::min(s + 1, g.cw - 1));
+        }
+        if (hi < 0) { CHECK(nY == 0, "no visible column but a footprint"); continue; }
+        CHECK(fsY == ((lo * bpp) & ~15) && fsY + 16 * nY == ((hi * bpp + bpp + 15) & ~15), "luma window");
+        CHECK(fsY + 16 * nY <= ((W * bpp + 15) & ~15), "luma window past the 16-B-rounded row");
+        if (yuv) {
+            const int clo = f == kNV12 ? 2 * (lo >> 1) : lo >> 1, chi = f == kNV12 ? 2 * (hi >> 1) + 2 : (hi >> 1) + 1;
+            CHECK(fsC <= clo && fsC + 16 * nC >= chi && fsC + 16 > clo && fsC + 16 * (nC - 1) < chi, "chroma window");
+        }
+        const int NP = fmt_nplanes(f);
+        CHECK(2 * 16 * nY + 2 * (NP - 1) * 16 * nC <= row_bytes_bound(f, g.cw), "row_bytes_bound f=%d cw=%d", f, g.cw);
+    }
+    printf("footprints: 20000 ROI windows minimal, covering, and within row_bytes_bound\n");
+}
+
+// a uniform group's wave-kernel segments must hold every item's footprint, whatever the
+// item's crop origin. Check wave_segments against each item's own per-tile chunk counts.
+static void check_wave_segments() {
+    int groups = 0, misaligned_needs_more = 0;
+    std::vector<XTab> xt;
+    std::vector<YTab> yt;
+    for (int it = 0; it < 3000; it++) {
+        const int f = uni(0, 3), bpp = fmt_bpp(f);
+        const bool yuv = f == kNV12 || f == kI420;
+        const int W = 1920, H = 1080;
+        int cw = uni(2, 900), ch = uni(2, 600);
+        if (yuv) { cw &= ~1; ch &= ~1; cw = std::max(cw, 2); ch = std::max(ch, 2); }
+        const int DW = uni(1, 700), DH = uni(1, 300), mode = uni(0, 2), placement = uni(0, 1);
+        const int n = uni(1, 40);
+        std::vector<int> x0(n);
+        uint32_t mask = 0;
+        for (int k = 0; k < n; k++) {
+            x0[k] = uni(0, W - cw);
+            if (yuv) x0[k] &= ~1;
+            mask |= 1u << (x0[k] & 31);
+        }
+        Geom g{};
+        if (roi_geometry(f, W, H, true, x0[0], 0, cw, ch, mode, placement, DW, DH, g)) continue;
+        xt.resize(DW); yt.resize(DH);
+        build_tables_into(g, DW, DH, xt.data(), yt.data());
+        for (int tw : {64, 128, 256}) {
+            int mY, mC, rY, rC;
+            wave_segments(f, g.ox, g.rw, DW, xt.data(), mask, tw, mY, mC);
+            wave_segments(f, g.ox, g.rw, DW, xt.data(), 1u << (x0[0] & 31), tw, rY, rC);
+            bool more = false;
+            for (int k = 0; k < n; k++)
+                for (int X0 = 0; X0 < DW; X0 += tw) {
+                    const int Xv0 = std::max(X0, g.ox), Xv1 = std::min(std::min(X0 + tw, DW), g.ox + g.rw) - 1;
+                    if (Xv0 > Xv1) continue;
+                    int fsY, nY, fsC, nC;
+                    footprint_chunks(f, bpp, x0[k] + xt[Xv0].s0, x0[k] + xt[Xv1].s1, fsY, nY, fsC, nC);
+                    CHECK(nY <= mY && nC <= mC, "f=%d cw=%d x0=%d tile %d: (%d,%d) > segments (%d,%d)", f, cw, x0[k], X0,
+                          nY, nC, mY, mC);
+                    more |= nY > rY || nC > rC;
+                }
+            misaligned_needs_more += more;
+        }
+        groups++;
+    }
+    printf("wave segments: %d uniform groups covered; %d tile widths where the first item's origin alone would "
+           "under-size the staging (the r1 bug)\n", groups, misaligned_needs_more);
+    CHECK(misaligned_needs_more > 0, "the generator never produced the misaligned case");
+}
+
+static void check_bytes_and_order() {
+    Geom g{};
+    CHECK(roi_geometry(kNV12, 1920, 1080, false, 0, 0, 0, 0, EVAM_RESIZE_NO_ASPECT, 0, 512, 512, g) == 0, "C2 geometry");
+    CHECK(item_src_bytes(kNV12, g, 512, 512) == 3002880, "C2 algorithmic source bytes %lld",
+          (long long)item_src_bytes(kNV12, g, 512, 512));
+    CHECK(roi_geometry(kNV12, 3840, 2160, false, 0, 0, 0, 0, EVAM_RESIZE_ASPECT, 0, 640, 640, g) == 0, "C4 geometry");
+    CHECK(g.rw == 640 && g.rh == 360, "C4 letterbox size");
+    for (int it = 0; it < 500; it++) {
+        const int n = uni(1, 2000), DH = uni(1, 300);
+        std::vector<Geom> geo(n);
+        std::vector<int> idx(n), bucket(n);
+        for (int i = 0; i < n; i++) {
+            geo[i] = Geom{0, 0, uni(1, 4000), uni(1, 3000), 1, 1, 0, 0};
+            idx[i] = n - 1 - i;
+        }
+        std::vector<int> ord;
+        roi_largest_first(idx.data(), n, geo.data(), DH, it % 5 != 0, bucket.data(), ord);
+        std::vector<int> seen(n, 0);
+        CHECK((int)ord.size() == n, "order size");
+        for (int p = 0; p < n; p++) {
+            seen[ord[p]]++;
+            if (p) CHECK(bucket[ord[p - 1]] <= bucket[ord[p]], "not largest first");
+        }
+        for (int i = 0; i < n; i++) CHECK(seen[i] == 1, "not a permutation");
+    }
+    printf("algorithmic bytes KAT (C2 3,002,880) and ROI launch order checked\n");
+}
+
+// The oracle under ASan: frames allocated to exactly rows x pitch bytes, random crops / modes / formats.
+static void check_oracle_bounds() {
+    float lut[768];
+    const float range[2] = {0.f, 1.f}, mean[3] = {0.1f, 0.2f, 0.3f}, sd[3] = {0.3f, 0.2f, 0.1f};
+    orc_norm_lut(3, range, mean, sd, lut);
+    int runs = 0;
+    for (int it = 0; it < 400; it++) {
+        const int f = uni(0, 3), bpp = fmt_bpp(f);
+        const bool yuv = f == kNV12 || f == kI420;
+        int W = uni(2, 200), H = uni(2, 120);
+        if (yuv) { W &= ~1; H &= ~1; }
+        const int np = fmt_nplanes(f);
+        std::vector<std::vector<uint8_t>> pl(np);
+        const uint8_t* planes[3] = {nullptr, nullptr, nullptr};
+        int pitch[3] = {0, 0, 0};
+        for (int p = 0; p < np; p++) {
+            const int rb = p == 0 ? W * bpp : (f == kNV12 ? W : W / 2);
+            const int rows = p == 0 ? H : H / 2;
+            pitch[p] = rb + uni(0, 1) * 16;
+            pl[p].resize((size_t)pitch[p] * rows);
+            for (auto& b : pl[p]) b = (uint8_t)uni(0, 255);
+            planes[p] = pl[p].data();
+        }
+        int x, y, w, h;
+        random_rect(W, H, x, y, w, h);
+        const int mode = uni(0, 2), DW = uni(1, 96), DH = uni(1, 96), f32 = uni(0, 1);
+        std::vector<uint8_t> out((size_t)3 * DW * DH * (f32 ? 4 : 1));
+        const uint8_t fill[3] = {1, 2, 3};
+        int32_t geom[8];
+        const int rc = orc_preprocess_item(kFourcc[f], planes, pitch, W, H, x, y, w, h, mode, uni(0, 1), uni(0, 1),
+                                           f32, f32 ? lut : nullptr, fill, out.data(), 0, DW, DH, geom);
+        runs += rc == 0;
+    }
+    printf("oracle: %d random items pre-processed on tight allocations\n", runs);
+}
+
+int main() {
+    check_geometry();
+    check_linear_tables();
+    check_footprints();
+    check_wave_segments();
+    check_bytes_and_order();
+    check_oracle_bounds();
+    if (failures) {
+        fprintf(stderr, "%d check(s) failed\n", failures);
+        return 1;
+    }
+    printf("planner_check: all checks passed\n");
+    return 0;
+}

@@ -1,0 +1,68 @@
+"""Multi-rank rehearsal on one GPU: two worker processes share cuda:0 over
+gloo, each pre-processes its ``s mod 2`` streams of a fixed 8-stream set, and every rank's tensors must
+equal a single-process run of the same streams bit for bit; the post-run reduction totals must add up.
+The workers are plain child processes (tools/dist_rehearsal.py), as torchrun would start them."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+WORKER = os.path.join(ROOT, "tools", "dist_rehearsal.py")
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _run(world, config, tmp_path, streams=8):
+    port = _free_port()
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        out = str(tmp_path / f"{config}_w{world}_r{r}.npz")
+        procs.append((subprocess.Popen([sys.executable, WORKER, "--config", config, "--streams", str(streams),
+                                        "--out", out], env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                                       text=True), out))
+    res = []
+    for p, out in procs:
+        try:
+            so, se = p.communicate(timeout=240)
+        except subprocess.TimeoutExpired:
+            for q, _ in procs:
+                q.kill()
+            raise
+        assert p.returncode == 0, se[-2000:]
+        meta = json.loads(so.strip().splitlines()[-1])
+        d = np.load(out)
+        res.append((meta, d["streams"], d["out"]))
+    return res
+
+
+@pytest.mark.parametrize("config", ["c2", "c4"])
+def test_two_ranks_match_single_process(gpu, tmp_path, config):
+    single = _run(1, config, tmp_path)
+    (meta1, s1, out1), = single
+    assert list(s1) == list(range(8)) and meta1["frames"] == 8
+    by_stream = {int(s): out1[i] for i, s in enumerate(s1)}
+    two = _run(2, config, tmp_path)
+    seen = []
+    for meta, streams, out in two:
+        assert meta["world"] == 2
+        assert meta["frames"] == 8 and meta["per_rank_frames"] == [4, 4]
+        assert meta["alg_bytes"] == meta1["alg_bytes"]           # summed over ranks == single process
+        assert list(streams) == list(range(meta["rank"], 8, 2))  # s mod 2 ownership
+        for i, s in enumerate(streams):
+            a, b = out[i], by_stream[int(s)]
+            assert (a.view(np.uint32) == b.view(np.uint32)).all(), f"{config} stream {s} rank {meta['rank']}"
+            seen.append(int(s))
+    assert sorted(seen) == list(range(8))

@@ -1,0 +1,130 @@
+"""GPU parity on the exact BASELINE workloads bench.py times, at full size, bit-exact vs the C oracle.
+
+Each test builds its inputs with bench.py's own generators: the seeded device frames of
+``bench.device_frames`` (copied back to the host for the oracle) and, for C3, the ``bench.seed_rois`` ROI
+sets. So the numbers bench.py reports are quoted on launches whose outputs are checked here element by
+element. Reference anchors: ``models_list/vehicle-detection-0202.json:3`` (C1/C2 default pre-proc),
+``pipelines/object_classification/vehicle_attributes/pipeline.json:4-5`` (C3 gvaclassify ROIs),
+``models_list/action-recognition-0001.json:3-13`` (C5 aspect-ratio + central crop).
+"""
+import numpy as np
+import pytest
+
+import bench
+from test_gpu_parity import assert_same, info_lut
+
+pytestmark = pytest.mark.gpu
+
+
+def host_frames(O, imgs):
+    """Host copies of bench's device frames (same bytes, same pitches) for the oracle."""
+    return [O.HostFrame(im.fourcc, im.width, im.height, [p.cpu().numpy() for p in im.planes]) for im in imgs]
+
+
+def oracle_items(O, coracle, frames, items, out_shape, dtype, info, slot=lambda i: i):
+    ref = np.zeros(out_shape, np.float32 if dtype == "f32" else np.uint8)
+    lut = (info_lut(O, info) if info.range is not None or info.mean is not None else O.np_norm_lut(0)) \
+        if dtype == "f32" else None
+    mode = info.resize_mode()
+    placement = 1 if info.placement == "center" else 0
+    for i, (si, x, y, w, h) in enumerate(items):
+        coracle.preprocess_item(frames[si], (x, y, w, h), ref, slot(i), mode=mode, placement=placement,
+                                color_rgb=info.color_space == "RGB", lut=lut, fill=info.fill)
+    return ref
+
+
+def test_c1_bench_batch(evam, O, coracle, gpu):
+    """C1: 32 x 768x432 NV12 -> 32x3x512x512 u8 (the wave kernel's REUSE path), bench frames."""
+    import torch
+
+    wl = bench.WORKLOADS["c1"]
+    imgs = bench.device_frames(evam, torch, wl, 32, gpu, seed=1234)
+    info = bench.make_info(evam, wl)
+    out = torch.full((32, 3, 512, 512), 7, dtype=torch.uint8, device=gpu)
+    pp = evam.HipPreProcessor(device=0)
+    pp.convert(imgs, out, info)
+    torch.cuda.synchronize()
+    ref = oracle_items(O, coracle, host_frames(O, imgs), [(i, 0, 0, 0, 0) for i in range(32)], out.shape, "u8", info)
+    assert_same(out.cpu().numpy(), ref, "C1 bench batch")
+    pp.close()
+
+
+def test_c2_bench_batch(evam, O, coracle, gpu):
+    """C2 headline: 32 distinct 1080p NV12 frames (pitch 1920) -> 32x3x512x512 fp32 normalised."""
+    import torch
+
+    wl = bench.WORKLOADS["c2"]
+    imgs = bench.device_frames(evam, torch, wl, 32, gpu, seed=1234)
+    assert imgs[0].pitches == [1920, 1920]
+    info = bench.make_info(evam, wl)
+    out = torch.full((32, 3, 512, 512), 7, dtype=torch.float32, device=gpu)
+    pp = evam.HipPreProcessor(device=0)
+    pp.convert(imgs, out, info)
+    torch.cuda.synchronize()
+    ref = oracle_items(O, coracle, host_frames(O, imgs), [(i, 0, 0, 0, 0) for i in range(32)], out.shape, "f32", info)
+    assert_same(out.cpu().numpy(), ref, "C2 bench batch")
+    pp.close()
+
+
+@pytest.mark.parametrize("seed", [0, 3])
+def test_c3_bench_roi_set(evam, O, coracle, gpu, seed):
+    """C3: bench.py's seeded ROI set (50 per frame, w 24..400, h 24..300) on 32 bench 1080p NV12 frames ->
+    1600x3x72x72 fp32 through the ROI kernel."""
+    import torch
+
+    wl = bench.WORKLOADS["c3"]
+    imgs = bench.device_frames(evam, torch, wl, 32, gpu, seed=1234)
+    rois = bench.seed_rois(wl["rois"], 32, *wl["src"], seed=seed)
+    assert len(rois) == 1600
+    info = bench.make_info(evam, wl)
+    out = torch.full((1600, 3, 72, 72), 7, dtype=torch.float32, device=gpu)
+    pp = evam.HipPreProcessor(device=0)
+    pp.convert(imgs, out, info, rois=evam.RoiBatch(np.array(rois, dtype=np.int32)))
+    torch.cuda.synchronize()
+    ref = oracle_items(O, coracle, host_frames(O, imgs), rois, out.shape, "f32", info)
+    assert_same(out.cpu().numpy(), ref, f"C3 bench ROI set seed {seed}")
+    pp.close()
+
+
+@pytest.mark.parametrize("placement", ["top_left", "center"])
+def test_c4_random_4k_letterbox(evam, O, coracle, gpu, placement):
+    """C4: random (not constant) 3840x2160 NV12 bench frames letterboxed to 640x640 fp32: every 6x gather
+    (column taps 6dx+2, weights 1024/1024) on the real 4K pitch is checked, in both placements."""
+    import torch
+
+    wl = bench.WORKLOADS["c4"]
+    imgs = bench.device_frames(evam, torch, wl, 2, gpu, seed=1234)
+    info = bench.make_info(evam, wl)
+    info.placement = placement
+    out = torch.full((2, 3, 640, 640), 7, dtype=torch.float32, device=gpu)
+    pp = evam.HipPreProcessor(device=0)
+    xf = pp.convert(imgs, out, info, want_transform=True)
+    torch.cuda.synchronize()
+    assert (xf[0].resized_w, xf[0].resized_h, xf[0].pad_y) == (640, 360, 140 if placement == "center" else 0)
+    ref = oracle_items(O, coracle, host_frames(O, imgs), [(0, 0, 0, 0, 0), (1, 0, 0, 0, 0)], out.shape, "f32", info)
+    assert_same(out.cpu().numpy(), ref, f"C4 4K letterbox {placement}")
+    pp.close()
+
+
+def test_c5_ring_step(evam, O, coracle, gpu):
+    """C5: a 32-stream clip-ring step (1080p NV12 -> aspect(max) 398x224 -> central crop 224x224 fp32 into
+    slot t % 16 of a [32, 16, 3, 224, 224] ring), two steps with different frames and slots."""
+    import torch
+
+    wl = bench.WORKLOADS["c5"]
+    info = bench.make_info(evam, wl)
+    ring = torch.full((32 * 16, 3, 224, 224), 7, dtype=torch.float32, device=gpu)
+    pp = evam.HipPreProcessor(device=0)
+    for t in (0, 17):
+        imgs = bench.device_frames(evam, torch, wl, 32, gpu, seed=1234 + t)
+        pp.convert(imgs, ring, info, slot_offset=t % 16, slot_stride=16)
+        torch.cuda.synchronize()
+        slots = [s * 16 + t % 16 for s in range(32)]
+        got = ring[slots].cpu().numpy()
+        ref = oracle_items(O, coracle, host_frames(O, imgs), [(s, 0, 0, 0, 0) for s in range(32)],
+                           (32, 3, 224, 224), "f32", info)
+        assert_same(got, ref, f"C5 ring step t={t}")
+    # slots no step wrote keep their initial value
+    untouched = [s * 16 + 5 for s in range(32)]
+    assert (ring[untouched] == 7).all().item()
+    pp.close()

@@ -466,3 +466,50 @@ def test_roi_kernel_xcd_order(evam, O, coracle, gpu, fmt, monkeypatch):
                      rois=[evam.Roi(*r) for r in rois])
     ref, _ = run_oracle(O, coracle, frames, shape, "f32", info, rois=rois)
     assert_same(got, ref, f"roi xcd order {fmt}")
+
+
+@pytest.mark.parametrize("fmt", FORMATS)
+@pytest.mark.parametrize("variant", ["wave", "staged"])
+def test_uniform_rois_varied_x0(evam, O, coracle, gpu, fmt, variant, monkeypatch):
+    """Equal-size ROIs (one uniform-geometry group) at crop origins covering every x0 mod 32 residue, upscaled
+    so the wave kernel's REUSE path runs: its LDS row segments must hold the widest 16-byte-aligned footprint
+    of ANY item's origin, not just the first item's (a misaligned origin needs one more chunk)."""
+    import torch
+
+    monkeypatch.setenv("EVAM_PP_WAVE", "2" if variant == "wave" else "0")
+    rng = np.random.default_rng(zlib.crc32(f"x0{fmt}".encode()))
+    W, H = 256, 120
+    frames = [O.random_frame(rng, fc(O, fmt), W, H, pattern="gradient" if i else "uniform") for i in range(2)]
+    yuv = fmt in ("NV12", "I420")
+    cw, ch = 40, 24  # even: 4:2:0 origins stay on even x (same clipped size for every ROI)
+    xs = list(range(0, 64, 2 if yuv else 1))
+    rois = [(k % 2, x, (7 * k) % (H - ch) & ~1, cw, ch) for k, x in enumerate(xs)]
+    for dst, dtype in (((96, 64), "u8"), ((120, 72), "f32")):
+        info = evam.PreProcInfo(**({"range": (0.0, 1.0), "mean": (0.1, 0.2, 0.3), "std": (0.3, 0.2, 0.1)}
+                                   if dtype == "f32" else {}))
+        shape = (len(rois), 3, dst[1], dst[0])
+        got, _ = run_hip(evam, torch, upload(evam, frames, gpu), shape,
+                         torch.float32 if dtype == "f32" else torch.uint8, info, rois=[evam.Roi(*r) for r in rois])
+        ref, _ = run_oracle(O, coracle, frames, shape, dtype, info, rois=rois)
+        assert_same(got, ref, f"uniform ROIs varied x0 {fmt} {dst} {variant}")
+
+
+def test_many_items_chunked_launches(evam, O, coracle, gpu):
+    """Uniform batches larger than one launch's kernel-argument item table (64) split into several
+    launches; every item still lands in its own slot, including clip-ring slot strides."""
+    import torch
+
+    rng = np.random.default_rng(21)
+    frames = [O.random_frame(rng, O.NV12, 96, 54) for _ in range(7)]
+    imgs = upload(evam, frames, gpu)
+    n = 150
+    batch = [imgs[i % 7] for i in range(n)]
+    info = evam.PreProcInfo(range=(0.0, 1.0))
+    pp = evam.HipPreProcessor(device=0)
+    pp.set_option(evam.native.OPT_STATS, 1)
+    got, _ = run_hip(evam, torch, batch, (n, 3, 40, 64), torch.float32, info, pp=pp)
+    assert pp.stats().n_launches == 3
+    ref1, _ = run_oracle(O, coracle, frames, (7, 3, 40, 64), "f32", info)
+    for i in range(n):
+        assert_same(got[i], ref1[i % 7], f"item {i}")
+    pp.close()

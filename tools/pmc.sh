@@ -20,8 +20,9 @@ fi
 for grp in "${GROUPS_DEFAULT[@]}"; do
   i=$((i+1))
   timeout -k 10 240 rocprofv3 --pmc $grp --output-format csv -d "$OUT/p$i" -o run -- \
-    python3 "$ROOT/bench.py" --config "$CFG" --steps 20 --warmup 5 --no-cpu-baseline > "$OUT/p$i.json" 2> "$OUT/p$i.err" \
+    python3 "$ROOT/bench.py" --config "$CFG" --steps 20 --warmup 5 --no-cpu-baseline --resident-steps 0 ${PMC_BENCH_ARGS:-} > "$OUT/p$i.json" 2> "$OUT/p$i.err" \
     || { echo "pass $i ($grp) failed"; tail -5 "$OUT/p$i.err"; exit 1; }
 done
 FR=$(python3 -c "import json;print(json.load(open('$OUT/p1.json'))['config']['frames_per_gpu_per_step'])")
-python3 "$ROOT/tools/pmc_summary.py" "$OUT" "$CFG" "$FR" "$ROOT/gpurun_out/pmc_traffic.json" | tee "$OUT/summary.txt"
+PS=$(python3 -c "import json;print(json.load(open('$OUT/p1.json'))['config']['pool_sets'])")
+python3 "$ROOT/tools/pmc_summary.py" "$OUT" "$CFG" "$FR" "$ROOT/gpurun_out/pmc_traffic.json" "$PS" | tee "$OUT/summary.txt"

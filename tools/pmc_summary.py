@@ -6,7 +6,7 @@ import os
 import sys
 
 
-def main(d, config=None, frames_per_launch=None, traffic_json=None):
+def main(d, config=None, frames_per_launch=None, traffic_json=None, pool_sets=1):
     vals = {}
     for f in sorted(glob.glob(os.path.join(d, "p*", "**", "*counter_collection.csv"), recursive=True)):
         for r in csv.DictReader(open(f)):
@@ -24,7 +24,8 @@ def main(d, config=None, frames_per_launch=None, traffic_json=None):
         print(f"hbm_bytes_per_launch (fetch x2 corrected + write) = {fetch + write:.6g}  (fetch {fetch:.6g}, write {write:.6g})")
         if traffic_json and config:
             t = json.load(open(traffic_json)) if os.path.exists(traffic_json) else {}
-            t[config] = {"frames_per_launch": frames_per_launch, "hbm_bytes_per_launch": int(fetch + write),
+            t[config] = {"frames_per_launch": frames_per_launch, "pool_sets": pool_sets,
+                         "hbm_bytes_per_launch": int(fetch + write),
                          "fetch_bytes": int(fetch), "write_bytes": int(write),
                          "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes, mean per dispatch "
                                    "of the evam_pp kernel; FETCH_SIZE (KB) x2 for the gfx950 half-count of wide "
@@ -36,4 +37,5 @@ def main(d, config=None, frames_per_launch=None, traffic_json=None):
 
 if __name__ == "__main__":
     a = sys.argv[1:]
-    main(a[0], *(a[1:2] or [None]), *( [int(a[2])] if len(a) > 2 else [None]), *(a[3:4] or [None]))
+    main(a[0], *(a[1:2] or [None]), *([int(a[2])] if len(a) > 2 else [None]), *(a[3:4] or [None]),
+         *([int(a[4])] if len(a) > 4 else []))
