@@ -137,10 +137,6 @@ struct RParams {
     int ablate;
 };
 
-#ifndef EVAM_PP_STAGE_ROWS
-#define EVAM_PP_STAGE_ROWS 2
-#endif
-constexpr int kStageRows = EVAM_PP_STAGE_ROWS;  // output rows per staged group (R)
 constexpr int kSlot = 1024;  // bytes of one staged source-row segment = one wave-wide 16 B/lane LDS-DMA
 
 struct SParams {
@@ -720,37 +716,57 @@ struct LaneRows {
     __device__ __forceinline__ int B1(int i) const { return __builtin_amdgcn_readlane(b1, i); }
 };
 
+// Wait until at most n vector-memory operations of this wave are outstanding (n wave-uniform). s_waitcnt
+// takes an immediate, so n is rounded DOWN to one of a few levels (always safe: it only waits longer) by
+// a short ladder of scalar compares; a full 64-way switch cost more SALU and branch issue per row group
+// than it saved.
+__device__ __forceinline__ void vmcnt_at_most(int n) {
+    n = __builtin_amdgcn_readfirstlane(n);
+    if (n >= 24) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+    else if (n >= 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    else if (n >= 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else if (n >= 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 // Staged uniform-geometry kernel. A workgroup owns a TW x TH tile (TW = 64 x NSEGX) and walks it in
 // groups of R output rows. For each group the source row segments its taps need (two luma rows and
 // two chroma rows per output row, each at most kSlot bytes wide) are brought into LDS by LDS-DMA —
-// one 16 B/lane buffer_load ... lds per row segment, the row offset in the SGPR offset — while the
-// previous group is being converted out of the other staging buffer. Taps are then LDS byte reads
-// with immediate slot offsets, so neither the staging nor the gather costs VALU address arithmetic,
-// and VMEM carries only wide loads and the planar stores. Only the stores and the DMA use vmcnt; the
-// wait for group g+1 is vmcnt(stores issued after it), so the stores are never drained in the loop.
-template <int FMT, int OUT, int R, int NSEGX>
+// one 16 B/lane buffer_load ... lds per row segment, the row offset in the SGPR offset — into one of
+// NBUF staging buffers, NBUF - 1 groups ahead of the group being converted: the DMA of several groups
+// is in flight while the workgroup converts, which is what hides HBM latency when the frames stream
+// from HBM rather than from the Infinity Cache. Taps are then LDS byte reads with immediate slot
+// offsets, so neither the staging nor the gather costs VALU address arithmetic, and VMEM carries only
+// wide loads and the planar stores. The DMA and the stores share vmcnt, which retires in issue order:
+// every wave counts the VMEM operations it issues (all its branches are wave-uniform, so the count is
+// exact) and waits for group g with vmcnt(operations issued after group g's DMA), so stores and later
+// groups' DMA stay in flight.
+template <int FMT, int OUT, int R, int NSEGX, int NBUF>
 __global__ EVAM_KERNEL_BOUNDS void evam_pp_staged(const SParams P) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     using T = FmtTraits<FMT>;
     constexpr bool kYUV = FMT == kNV12 || FMT == kI420;
     constexpr int NP = FMT == kI420 ? 3 : (FMT == kNV12 ? 2 : 1);  // staged planes
     constexpr int NS = 2 * R * NP;                                   // slots per staging buffer
-    constexpr int RSTEP = 4 / NSEGX;                                 // waves sharing a column segment
+    constexpr int SPW = NSEGX > 4 ? NSEGX / 4 : 1;                   // column segments per wave
+    constexpr int RSTEP = NSEGX >= 4 ? 1 : 4 / NSEGX;                // waves sharing a column segment
     constexpr int RPW = R / RSTEP;                                   // rows per wave per group
-    constexpr int kStores = 3 * RPW;                                 // stores per wave per full group
+    constexpr int SLOT = NSEGX > 4 ? 2 * kSlot : kSlot;              // bytes of one staged row segment
     static_assert(R % RSTEP == 0, "R must be a multiple of 4 / NSEGX");
+    static_assert(NSEGX <= 4 || R == 1, "full-width (2 KB slot) tiles stage one row per group");
+    static_assert(NBUF >= 2 && NBUF <= 3, "2 or 3 staging buffers");
     constexpr int TW = 64 * NSEGX;
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    if (P.ablate & 128) return;  // diagnostics: launch cost only
     const int t = P.xcd_remap ? xcd_tile(blockIdx.x, gridDim.x) : (int)blockIdx.x;
     const int item = t / P.tiles_per_item;
     const int tile = t - item * P.tiles_per_item;
     const int ty = tile / P.tiles_x;
     const int tx = tile - ty * P.tiles_x;
     const ItemArg& it = P.items[item];
-    const __attribute__((address_space(4))) YTab* ytab = (const __attribute__((address_space(4))) YTab*)(P.ytab);
     const __attribute__((address_space(4))) XTab* xtab_s = (const __attribute__((address_space(4))) XTab*)(P.xtab);
     const uint8_t* p0 = it.plane[0];
     const uint8_t* p1 = it.plane[1];
@@ -777,7 +793,7 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_staged(const SParams P) {
     const uint32_t fillv[3] = {(P.color_rgb ? fq2 : fq0) << fsh, fq1 << fsh, (P.color_rgb ? fq0 : fq2) << fsh};
 
     const int X0 = tx * TW, Y0 = ty * P.TH, Y1 = min(Y0 + P.TH, P.DH);
-    const int seg = wave % NSEGX, rph = wave / NSEGX;
+    const int rph = NSEGX >= 4 ? 0 : wave / NSEGX;
     // visible (non-padding) columns of the tile -> source footprint (wave-uniform)
     const int Xv0 = max(X0, ox), Xv1 = min(min(X0 + TW, P.DW), ox + rw) - 1;
     const bool cols = Xv0 <= Xv1;
@@ -785,72 +801,94 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_staged(const SParams P) {
     if (cols) {
         footprint_chunks(FMT, T::bpp, x0 + xtab_s[Xv0].s0, x0 + xtab_s[Xv1].s1, fsY, nY, fsC, nC);
     }
-    // per-lane column state (filled once the first DMA is in flight): LDS byte offsets of the taps
+    // per-lane column state for each of this wave's SPW 64-column segments (seg = wave + 4 j, or
+    // wave % NSEGX for narrow tiles), filled once the first DMA is in flight: LDS byte offsets of the taps
     // inside a slot, weights
-    const int X = X0 + seg * 64 + lane;
-    const bool xin = X < P.DW;
-    uint32_t lY0 = 0, lY1 = 0, lC0 = 0, lC1 = 0, wa = 0, wp = 0;  // wp: plain 11-bit weights a0 | a1 << 16
-    (void)wp;
-    const uint32_t xo = (uint32_t)(xin ? X : 0) * (uint32_t)esz;
-    const bool wave_stores = X0 + seg * 64 < P.DW;  // some lane of this wave stores (wave-uniform)
+    int X[SPW];
+    bool xin[SPW], wave_stores[SPW];  // wave_stores: lane 0 of this wave stores segment j (wave-uniform)
+    uint32_t lY0[SPW], lY1[SPW], lC0[SPW], lC1[SPW], wa[SPW], wp[SPW], xo[SPW];  // wp: a0 | a1 << 16, plain
+#pragma unroll
+    for (int j = 0; j < SPW; j++) {
+        const int seg = NSEGX >= 4 ? wave + 4 * j : wave % NSEGX;
+        X[j] = X0 + seg * 64 + lane;
+        xin[j] = X[j] < P.DW;
+        wave_stores[j] = X0 + seg * 64 < P.DW;
+        xo[j] = (uint32_t)(xin[j] ? X[j] : 0) * (uint32_t)esz;
+        lY0[j] = lY1[j] = lC0[j] = lC1[j] = wa[j] = wp[j] = 0;
+    }
     const int rows = Y1 - Y0;
     const int ngroups = (rows + R - 1) / R;
+    // The tile's row table (<= 64 rows, host-checked), one row per lane in every wave: per-group lookups
+    // are v_readlane instead of dependent scalar loads from L2 (~1 us per group in the loop's critical
+    // path when the frames stream from HBM, profiles/r02_skeleton.txt).
+    LaneRows lr;
+    lr.load(P.ytab, Y0, rows, lane);
 
     // ---- LDS-DMA of group g into buffer `buf` (slot s = plane * 2R + 2 * row + tap) ----
-    // Static DMA roles: with R = 2 the 2R (row, tap) pairs of a group are exactly the four waves, so
-    // wave w stages row w >> 1, tap w & 1 of every plane. One row-table fetch per group and no
-    // per-slot plane / resource selection in the scalar unit.
+    // Returns the number of VMEM instructions this wave issued (wave-uniform; nY, nC >= 1 whenever
+    // `cols`, so lane 0 is active in every issued instruction).
+    // Static DMA roles: with 2R = 4 the (row, tap) pairs of a group are exactly the four waves, so wave
+    // w stages row w >> 1, tap w & 1 of every plane. Otherwise the slots are dealt round-robin.
     const int dr = wave >> 1, dtap = wave & 1;
-    auto issue = [&](int g, uint8_t* buf) {
-        if (!cols || (P.ablate & 16)) return;
-#ifndef EVAM_PP_DYN_ROLES
-        if constexpr (2 * R == 4) {
+    auto issue = [&](int g, uint8_t* buf) -> int {
+        if (!cols || (P.ablate & 16)) return 0;
+        if constexpr (2 * R == 4 && SLOT == kSlot) {
             const int Y = Y0 + g * R + dr;
-            if (Y >= Y1) return;
-            const int b0 = ytab[Y].b0, b1 = ytab[Y].b1;
-            if ((b0 | b1) == 0) return;  // padding row: nothing to stage
-            const int ya = y0 + ytab[Y].r0, yb = y0 + ytab[Y].r1;
+            if (Y >= Y1) return 0;
+            const int b0 = lr.B0(Y - Y0), b1 = lr.B1(Y - Y0);
+            if ((b0 | b1) == 0) return 0;  // padding row: nothing to stage
+            const int ya = y0 + lr.R0(Y - Y0), yb = y0 + lr.R1(Y - Y0);
             const int yr = dtap ? yb : ya;
             if (lane < nY)
                 __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                    rsY, (__attribute__((address_space(3))) void*)(buf + wave * kSlot), 16, lane * 16, yr * pitch0 + fsY, 0, 0);
+                    rsY, (__attribute__((address_space(3))) void*)(buf + wave * SLOT), 16, lane * 16, yr * pitch0 + fsY, 0, 0);
             if constexpr (NP >= 2) {
-                if (dtap && (ya >> 1) == (yb >> 1)) return;  // chroma row shared by both taps
+                if (dtap && (ya >> 1) == (yb >> 1)) return 1;  // chroma row shared by both taps
                 if (lane < nC) {
                     __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                        rsC, (__attribute__((address_space(3))) void*)(buf + (2 * R + wave) * kSlot), 16, lane * 16,
+                        rsC, (__attribute__((address_space(3))) void*)(buf + (2 * R + wave) * SLOT), 16, lane * 16,
                         (yr >> 1) * pitch1 + fsC, 0, 0);
                     if constexpr (NP >= 3)
                         __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                            rsV, (__attribute__((address_space(3))) void*)(buf + (4 * R + wave) * kSlot), 16, lane * 16,
+                            rsV, (__attribute__((address_space(3))) void*)(buf + (4 * R + wave) * SLOT), 16, lane * 16,
                             (yr >> 1) * pitch2 + fsC, 0, 0);
                 }
+                return NP;
             }
-            return;
-        }
-#endif
+            return 1;
+        } else {
+            int n = 0;
 #pragma unroll
-        for (int s0 = 0; s0 < NS; s0 += 4) {
-            const int s = s0 + wave;
-            const int pl = s / (2 * R), loc = s - pl * 2 * R, r = loc >> 1, tap = loc & 1;
-            const int Y = Y0 + g * R + r;
-            if (Y >= Y1) continue;
-            const int b0 = ytab[Y].b0, b1 = ytab[Y].b1;
-            if ((b0 | b1) == 0) continue;  // padding row: nothing to stage
-            const int ya = y0 + ytab[Y].r0, yb = y0 + ytab[Y].r1;
-            const int yr = tap ? yb : ya;
-            if (pl > 0 && tap && (ya >> 1) == (yb >> 1)) continue;  // chroma row shared by both taps
-            const int nck = pl == 0 ? nY : nC;
-            if (lane < nck) {
-                __attribute__((address_space(3))) void* dstl =
-                    (__attribute__((address_space(3))) void*)(buf + s * kSlot);
-                if (pl == 0)
-                    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsY, dstl, 16, lane * 16, yr * pitch0 + fsY, 0, 0);
-                else if (pl == 1)
-                    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsC, dstl, 16, lane * 16, (yr >> 1) * pitch1 + fsC, 0, 0);
-                else
-                    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsV, dstl, 16, lane * 16, (yr >> 1) * pitch2 + fsC, 0, 0);
+            for (int s0 = 0; s0 < NS; s0 += 4) {
+                const int s = s0 + wave;
+                if (s >= NS) continue;
+                const int pl = s / (2 * R), loc = s - pl * 2 * R, r = loc >> 1, tap = loc & 1;
+                const int Y = Y0 + g * R + r;
+                if (Y >= Y1) continue;
+                const int b0 = lr.B0(Y - Y0), b1 = lr.B1(Y - Y0);
+                if ((b0 | b1) == 0) continue;  // padding row: nothing to stage
+                const int ya = y0 + lr.R0(Y - Y0), yb = y0 + lr.R1(Y - Y0);
+                const int yr = tap ? yb : ya;
+                if (pl > 0 && tap && (ya >> 1) == (yb >> 1)) continue;  // chroma row shared by both taps
+                const int nck = pl == 0 ? nY : nC;
+#pragma unroll
+                for (int c0 = 0; c0 < SLOT / 16; c0 += 64) {  // one wave-wide 1 KB DMA per 64 chunks
+                    if (c0 >= nck) break;
+                    __attribute__((address_space(3))) void* dstl =
+                        (__attribute__((address_space(3))) void*)(buf + s * SLOT + c0 * 16);
+                    if (lane + c0 < nck) {
+                        const int co = (lane + c0) * 16;
+                        if (pl == 0)
+                            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsY, dstl, 16, co, yr * pitch0 + fsY, 0, 0);
+                        else if (pl == 1)
+                            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsC, dstl, 16, co, (yr >> 1) * pitch1 + fsC, 0, 0);
+                        else
+                            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsV, dstl, 16, co, (yr >> 1) * pitch2 + fsC, 0, 0);
+                    }
+                    n++;
+                }
             }
+            return n;
         }
     };
 
@@ -859,91 +897,100 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_staged(const SParams P) {
     // RGB order, through swapped plane resources; the LDS LUT is loaded with its sections in source
     // channel order (prologue), so the per-pixel path carries no swap. For fp32 output the vertical
     // pass yields 4 * v, the LUT byte offset, directly ((x + 2) & ~3 instead of (x + 2) >> 2).
-    auto compute = [&](int g, const uint8_t* buf) {
+    // Returns the number of stores this wave issued: 3 per owned row when the wave stores at all (the
+    // padding-column select is branchless, so every storing row issues exactly three).
+    auto compute = [&](int g, const uint8_t* buf) -> int {
+        int n = 0;
 #pragma unroll
-        for (int k = 0; k < RPW; k++) {
+        for (int kj = 0; kj < RPW * SPW; kj++) {
+            const int k = kj / SPW, j = kj % SPW;
             const int r = rph + k * RSTEP;
             const int Y = Y0 + g * R + r;
-            if (Y >= Y1) continue;
-            const int b0 = ytab[Y].b0, b1 = ytab[Y].b1;
+            if (Y >= Y1 || !wave_stores[j]) continue;
+            const int b0 = lr.B0(Y - Y0), b1 = lr.B1(Y - Y0);
             const int sO = (int)((uint32_t)(Y * P.DW) * (uint32_t)esz);
-            if (!xin) continue;
+            n += 3;
             auto put = [&](const uint32_t (&v)[3]) {
                 if (P.ablate & 4) {
                     asm volatile("" :: "v"(v[0]), "v"(v[1]), "v"(v[2]));
                     return;
                 }
+                if (!xin[j]) return;  // lane 0 is in: the wave still issues all three stores
                 if constexpr (OUT == 1) {
                     const uint8_t* lb = reinterpret_cast<const uint8_t*>(lut_s);
-                    __builtin_amdgcn_raw_buffer_store_b32(*reinterpret_cast<const uint32_t*>(lb + v[0]), rsD0, xo, sO, 0);
-                    __builtin_amdgcn_raw_buffer_store_b32(*reinterpret_cast<const uint32_t*>(lb + 1024 + v[1]), rsD1, xo, sO, 0);
-                    __builtin_amdgcn_raw_buffer_store_b32(*reinterpret_cast<const uint32_t*>(lb + 2048 + v[2]), rsD2, xo, sO, 0);
+                    __builtin_amdgcn_raw_buffer_store_b32(*reinterpret_cast<const uint32_t*>(lb + v[0]), rsD0, xo[j], sO, 0);
+                    __builtin_amdgcn_raw_buffer_store_b32(*reinterpret_cast<const uint32_t*>(lb + 1024 + v[1]), rsD1, xo[j], sO, 0);
+                    __builtin_amdgcn_raw_buffer_store_b32(*reinterpret_cast<const uint32_t*>(lb + 2048 + v[2]), rsD2, xo[j], sO, 0);
                 } else {
-                    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v[0], rsD0, xo, sO, 0);
-                    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v[1], rsD1, xo, sO, 0);
-                    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v[2], rsD2, xo, sO, 0);
+                    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v[0], rsD0, xo[j], sO, 0);
+                    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v[1], rsD1, xo[j], sO, 0);
+                    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v[2], rsD2, xo[j], sO, 0);
                 }
             };
-            if ((b0 | b1) == 0 || wa == 0 || (P.ablate & 2)) {  // padding row / column
+            if ((b0 | b1) == 0 || (P.ablate & 2)) {  // padding row (wave-uniform)
                 put(fillv);
                 continue;
             }
+            const bool padc = wa[j] == 0;  // letterbox padding column: taps at valid offsets, value replaced
             const uint32_t wb0 = (uint32_t)b0, wb1 = (uint32_t)b1;
-            const uint8_t* sy0 = buf + (2 * r) * kSlot;
-            const uint8_t* sy1 = sy0 + kSlot;
-            const uint8_t* sc0 = buf + (2 * R + 2 * r) * kSlot;
+            const uint8_t* sy0 = buf + (2 * r) * SLOT;
+            const uint8_t* sy1 = sy0 + SLOT;
+            const uint8_t* sc0 = buf + (2 * R + 2 * r) * SLOT;
+            const uint32_t lY0j = lY0[j], lY1j = lY1[j], lC0j = lC0[j], lC1j = lC1[j], wpj = wp[j];
             uint32_t v[3];
 #ifndef EVAM_PP_NO_SAT
             if constexpr (kYUV) {
-                const int ya = y0 + ytab[Y].r0, yb = y0 + ytab[Y].r1;
+                const int ya = y0 + lr.R0(Y - Y0), yb = y0 + lr.R1(Y - Y0);
                 const bool share = (ya >> 1) == (yb >> 1);
-                const uint8_t* sc1 = share ? sc0 : sc0 + kSlot;
+                const uint8_t* sc1 = share ? sc0 : sc0 + SLOT;
                 // NV12: U and V of a tap are adjacent bytes of the staged UV row; I420: same offset in the
                 // U and V slots.
-                const uint8_t* sv0 = FMT == kNV12 ? sc0 + 1 : sc0 + 2 * R * kSlot;
-                const uint8_t* sv1 = FMT == kNV12 ? sc1 + 1 : sc1 + 2 * R * kSlot;
-                const UVs tA = uv_terms_sat(sc0[lC0], sv0[lC0]);
-                const UVs tB = uv_terms_sat(sc0[lC1], sv0[lC1]);
-                const UVs tC = uv_terms_sat(sc1[lC0], sv1[lC0]);
-                const UVs tD = uv_terms_sat(sc1[lC1], sv1[lC1]);
-                const uint32_t yA = luma_term(sy0[lY0]), yB = luma_term(sy0[lY1]);
-                const uint32_t yC = luma_term(sy1[lY0]), yD = luma_term(sy1[lY1]);
-                v[0] = vfinal<OUT>(hpass_sat(yA, tA.b, yB, tB.b, wp), hpass_sat(yC, tC.b, yD, tD.b, wp), wb0, wb1);
-                v[1] = vfinal<OUT>(hpass_sat(yA, tA.g, yB, tB.g, wp), hpass_sat(yC, tC.g, yD, tD.g, wp), wb0, wb1);
-                v[2] = vfinal<OUT>(hpass_sat(yA, tA.r, yB, tB.r, wp), hpass_sat(yC, tC.r, yD, tD.r, wp), wb0, wb1);
+                const uint8_t* sv0 = FMT == kNV12 ? sc0 + 1 : sc0 + 2 * R * SLOT;
+                const uint8_t* sv1 = FMT == kNV12 ? sc1 + 1 : sc1 + 2 * R * SLOT;
+                const UVs tA = uv_terms_sat(sc0[lC0j], sv0[lC0j]);
+                const UVs tB = uv_terms_sat(sc0[lC1j], sv0[lC1j]);
+                const UVs tC = uv_terms_sat(sc1[lC0j], sv1[lC0j]);
+                const UVs tD = uv_terms_sat(sc1[lC1j], sv1[lC1j]);
+                const uint32_t yA = luma_term(sy0[lY0j]), yB = luma_term(sy0[lY1j]);
+                const uint32_t yC = luma_term(sy1[lY0j]), yD = luma_term(sy1[lY1j]);
+                v[0] = vfinal<OUT>(hpass_sat(yA, tA.b, yB, tB.b, wpj), hpass_sat(yC, tC.b, yD, tD.b, wpj), wb0, wb1);
+                v[1] = vfinal<OUT>(hpass_sat(yA, tA.g, yB, tB.g, wpj), hpass_sat(yC, tC.g, yD, tD.g, wpj), wb0, wb1);
+                v[2] = vfinal<OUT>(hpass_sat(yA, tA.r, yB, tB.r, wpj), hpass_sat(yC, tC.r, yD, tD.r, wpj), wb0, wb1);
+#pragma unroll
+                for (int c = 0; c < 3; c++) v[c] = padc ? fillv[c] : v[c];
                 put(v);
                 continue;
             }
 #endif
-            const uint32_t a0 = wa & 0xFFFF, a1 = wa >> 16;  // 15-bit
+            const uint32_t a0 = wa[j] & 0xFFFF, a1 = wa[j] >> 16;  // 15-bit
             int c[4][3];
             if constexpr (kYUV) {
-                const int ya = y0 + ytab[Y].r0, yb = y0 + ytab[Y].r1;
+                const int ya = y0 + lr.R0(Y - Y0), yb = y0 + lr.R1(Y - Y0);
                 const bool share = (ya >> 1) == (yb >> 1);
-                const uint8_t* sc1 = share ? sc0 : sc0 + kSlot;
+                const uint8_t* sc1 = share ? sc0 : sc0 + SLOT;
                 Chroma<FMT> cA, cB, cC, cD;
                 if constexpr (FMT == kNV12) {
-                    cA.u = *reinterpret_cast<const uint16_t*>(sc0 + lC0);
-                    cB.u = *reinterpret_cast<const uint16_t*>(sc0 + lC1);
-                    cC.u = *reinterpret_cast<const uint16_t*>(sc1 + lC0);
-                    cD.u = *reinterpret_cast<const uint16_t*>(sc1 + lC1);
+                    cA.u = *reinterpret_cast<const uint16_t*>(sc0 + lC0j);
+                    cB.u = *reinterpret_cast<const uint16_t*>(sc0 + lC1j);
+                    cC.u = *reinterpret_cast<const uint16_t*>(sc1 + lC0j);
+                    cD.u = *reinterpret_cast<const uint16_t*>(sc1 + lC1j);
                 } else {
-                    const uint8_t* sv0 = sc0 + 2 * R * kSlot;
-                    const uint8_t* sv1 = sc1 + 2 * R * kSlot;
-                    cA.u = sc0[lC0]; cA.v = sv0[lC0];
-                    cB.u = sc0[lC1]; cB.v = sv0[lC1];
-                    cC.u = sc1[lC0]; cC.v = sv1[lC0];
-                    cD.u = sc1[lC1]; cD.v = sv1[lC1];
+                    const uint8_t* sv0 = sc0 + 2 * R * SLOT;
+                    const uint8_t* sv1 = sc1 + 2 * R * SLOT;
+                    cA.u = sc0[lC0j]; cA.v = sv0[lC0j];
+                    cB.u = sc0[lC1j]; cB.v = sv0[lC1j];
+                    cC.u = sc1[lC0j]; cC.v = sv1[lC0j];
+                    cD.u = sc1[lC1j]; cD.v = sv1[lC1j];
                 }
-                y_plus_uv((int)sy0[lY0], chroma_terms<FMT>(cA), c[0][0], c[0][1], c[0][2]);
-                y_plus_uv((int)sy0[lY1], chroma_terms<FMT>(cB), c[1][0], c[1][1], c[1][2]);
-                y_plus_uv((int)sy1[lY0], chroma_terms<FMT>(cC), c[2][0], c[2][1], c[2][2]);
-                y_plus_uv((int)sy1[lY1], chroma_terms<FMT>(cD), c[3][0], c[3][1], c[3][2]);
+                y_plus_uv((int)sy0[lY0j], chroma_terms<FMT>(cA), c[0][0], c[0][1], c[0][2]);
+                y_plus_uv((int)sy0[lY1j], chroma_terms<FMT>(cB), c[1][0], c[1][1], c[1][2]);
+                y_plus_uv((int)sy1[lY0j], chroma_terms<FMT>(cC), c[2][0], c[2][1], c[2][2]);
+                y_plus_uv((int)sy1[lY1j], chroma_terms<FMT>(cD), c[3][0], c[3][1], c[3][2]);
             } else {
                 const uint8_t* rowp[2] = {sy0, sy1};
 #pragma unroll
                 for (int q = 0; q < 4; q++) {
-                    const uint8_t* sp = rowp[q >> 1] + ((q & 1) ? lY1 : lY0);
+                    const uint8_t* sp = rowp[q >> 1] + ((q & 1) ? lY1j : lY0j);
                     if constexpr (FMT == kBGRX) {
                         const uint32_t px = *reinterpret_cast<const uint32_t*>(sp);
                         c[q][0] = px & 0xFF; c[q][1] = (px >> 8) & 0xFF; c[q][2] = (px >> 16) & 0xFF;
@@ -956,49 +1003,66 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_staged(const SParams P) {
             for (int ch3 = 0; ch3 < 3; ch3++) {
                 const uint32_t D0 = __umul24(c[0][ch3], a0) + __umul24(c[1][ch3], a1);
                 const uint32_t D1 = __umul24(c[2][ch3], a0) + __umul24(c[3][ch3], a1);
-                v[ch3] = vfinal<OUT>(D0, D1, wb0, wb1);
+                v[ch3] = padc ? fillv[ch3] : vfinal<OUT>(D0, D1, wb0, wb1);
             }
             put(v);
         }
+        return n;
     };
 
-    uint8_t* const buf0 = smem + P.offBuf;
-    uint8_t* const buf1 = buf0 + P.buf_bytes;
-    // Prologue: the first group's DMA goes out before the LUT and column-table loads, so their
-    // latencies overlap instead of adding up.
-    issue(0, buf0);
+    uint8_t* const bufs = smem + P.offBuf;
+    // Prologue: the first NBUF - 1 groups' DMA goes out before the LUT and column-table loads, so their
+    // latencies overlap instead of adding up. q[j]: VMEM operations issued up to the end of the DMA of
+    // group g + j (j < NBUF - 1), for the counted waits below.
+    int issued = 0;
+    int q[NBUF - 1];
+#pragma unroll
+    for (int j = 0; j < NBUF - 1; j++) {
+        if (j < ngroups) issued += __builtin_amdgcn_readfirstlane(issue(j, bufs + j * P.buf_bytes));
+        q[j] = issued;
+    }
     asm volatile("" ::: "memory");
     if constexpr (OUT == 1) {  // sections in source channel order (B, G, R): see compute
-        for (int i = tid; i < 768; i += kThreads) lut_s[i] = P.lut[P.color_rgb ? 512 - (i & ~255) + (i & 255) : i];
+        if (!(P.ablate & 32))   // diagnostics: 32 skips the LUT load
+            for (int i = tid; i < 768; i += kThreads) lut_s[i] = P.lut[P.color_rgb ? 512 - (i & ~255) + (i & 255) : i];
     }
-    {
-        const XTab xt = P.xtab[xin ? X : 0];
-        wa = (uint32_t)xt.a0 | ((uint32_t)xt.a1 << 16);
-        wp = (wa >> 4) & 0x0FFF0FFFu;
-        if (xin && wa != 0) {
+#pragma unroll
+    for (int j = 0; j < SPW; j++) {
+        const XTab xt = P.xtab[xin[j] ? X[j] : 0];
+        wa[j] = (uint32_t)xt.a0 | ((uint32_t)xt.a1 << 16);
+        wp[j] = (wa[j] >> 4) & 0x0FFF0FFFu;
+        if (xin[j] && wa[j] != 0) {
             const int ca = x0 + xt.s0, cb = x0 + xt.s1;
-            lY0 = (uint32_t)(ca * T::bpp - fsY);
-            lY1 = (uint32_t)(cb * T::bpp - fsY);
-            lC0 = FMT == kNV12 ? (uint32_t)(2 * (ca >> 1) - fsC) : (uint32_t)((ca >> 1) - fsC);
-            lC1 = FMT == kNV12 ? (uint32_t)(2 * (cb >> 1) - fsC) : (uint32_t)((cb >> 1) - fsC);
+            lY0[j] = (uint32_t)(ca * T::bpp - fsY);
+            lY1[j] = (uint32_t)(cb * T::bpp - fsY);
+            lC0[j] = FMT == kNV12 ? (uint32_t)(2 * (ca >> 1) - fsC) : (uint32_t)((ca >> 1) - fsC);
+            lC1[j] = FMT == kNV12 ? (uint32_t)(2 * (cb >> 1) - fsC) : (uint32_t)((cb >> 1) - fsC);
         }
     }
+    int bi = 0;                 // buffer of group g
+    int bn = NBUF - 1;          // buffer of group g + NBUF - 1
+    if ((P.ablate & 64) && ngroups != -7) {  // diagnostics: prologue only
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("" :: "v"(lY0[0]), "v"(lC0[0]), "v"(wa[0]), "v"(lY1[0]), "v"(lC1[0]));
+        return;
+    }
     for (int g = 0; g < ngroups; g++) {
-        // DMA of group g landed (this wave's share), while the previous group's stores stay in flight
-        // — unless that group was partial or its lanes skipped stores: then drain everything.
-        const bool prev_full = g > 0 && (g * R <= rows) && wave_stores;
-        if (prev_full) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(kStores) : "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        // This wave's share of group g's DMA landed; everything issued after it (later groups' DMA, the
+        // previous groups' stores) may stay in flight. The first iteration also covers the prologue's
+        // global loads (LUT, column table), which were issued after the DMA.
+        if (g == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        else vmcnt_at_most(issued - q[0]);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();  // every wave's DMA for g landed; every wave done reading g-1
-        if (g + 1 < ngroups) issue(g + 1, (g & 1) ? buf0 : buf1);
-#ifndef EVAM_PP_NO_FENCE_TEST
-        asm volatile("" ::: "memory");  // the next group's DMA stays ahead of this group's stores
-#endif
-        compute(g, (g & 1) ? buf1 : buf0);
-#ifndef EVAM_PP_NO_FENCE_TEST
+#pragma unroll
+        for (int j = 0; j + 1 < NBUF - 1; j++) q[j] = q[j + 1];
+        if (g + NBUF - 1 < ngroups) issued += __builtin_amdgcn_readfirstlane(issue(g + NBUF - 1, bufs + bn * P.buf_bytes));
+        q[NBUF - 2] = issued;
+        asm volatile("" ::: "memory");  // the next groups' DMA stays ahead of this group's stores
+        issued += __builtin_amdgcn_readfirstlane(compute(g, bufs + bi * P.buf_bytes));
         asm volatile("" ::: "memory");
-#endif
+        bi = bi + 1 == NBUF ? 0 : bi + 1;
+        bn = bn + 1 == NBUF ? 0 : bn + 1;
     }
 }
 
@@ -1798,6 +1862,7 @@ struct Knobs {
     int staged = 1, wave = 1, rows = 1, roi = 1;   // kernel families allowed (wave 2 = force)
     int th = -1, tw = -1, xcd = -1;                // staged / generic tiles, XCD-contiguous order
     int nsegx = 0;                                 // staged tile width in 64-column segments (0: widest that fits)
+    int stage_r = -1, stage_nbuf = -1;             // staged pipeline: rows per group, staging buffers
     int wth = -1, px = 0, reuse = 1, wave_lds = 40 * 1024;
     int roi_th = -1, roi_buf = 12 * 1024, roi_px = 1, roi_sort = 1, roi_xcd = 0;
     int ablate = 0;                                // stage-removal diagnostics (results invalid)
@@ -1806,6 +1871,7 @@ struct Knobs {
         rows = env_int("EVAM_PP_ROWS", rows); roi = env_int("EVAM_PP_ROI", roi);
         th = env_int("EVAM_PP_TH", th); tw = env_int("EVAM_PP_TW", tw); xcd = env_int("EVAM_PP_XCD", xcd);
         nsegx = env_int("EVAM_PP_NSEGX", nsegx);
+        stage_r = env_int("EVAM_PP_STAGE_R", stage_r); stage_nbuf = env_int("EVAM_PP_STAGE_NBUF", stage_nbuf);
         wth = env_int("EVAM_PP_WTH", wth); px = env_int("EVAM_PP_PX", px);
         reuse = env_int("EVAM_PP_REUSE", reuse); wave_lds = env_int("EVAM_PP_WAVE_LDS", wave_lds);
         roi_th = env_int("EVAM_PP_ROI_TH", roi_th); roi_buf = env_int("EVAM_PP_ROI_BUF", roi_buf);
@@ -1869,35 +1935,58 @@ RowCfg choose_row_tiles(int DW, int DH, const Knobs& k) {
     return r;
 }
 
-template <int FMT, int OUT, int NSEGX>
+// Staged-kernel pipeline shapes: (output rows per group R, staging buffers NBUF). One variant per
+// (format, dtype, column segments) is instantiated for each shape listed here.
+struct StagedShape { int R, nbuf; };
+constexpr StagedShape kStagedShapes[] = {{2, 2}, {1, 2}};
+
+// Valid (column segments, rows per group): four waves split NSEGX x R evenly.
+constexpr bool staged_valid(int nsegx, int R) { return nsegx > 4 ? R == 1 : (nsegx == 4 ? true : R % (4 / nsegx) == 0); }
+
+template <int FMT, int OUT, int NSEGX, int R, int NBUF>
 hipError_t launch_staged_t(const SParams& p, int grid, int lds, hipStream_t s) {
-    if constexpr (kStageRows % (4 / NSEGX) == 0) {
-        hipLaunchKernelGGL((evam_pp_staged<FMT, OUT, kStageRows, NSEGX>), dim3(grid), dim3(kThreads), lds, s, p);
+    if constexpr (staged_valid(NSEGX, R)) {
+        if (lds > 64 * 1024) {
+            hipError_t e = hipFuncSetAttribute((const void*)evam_pp_staged<FMT, OUT, R, NSEGX, NBUF>,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+            if (e != hipSuccess) return e;
+        }
+        hipLaunchKernelGGL((evam_pp_staged<FMT, OUT, R, NSEGX, NBUF>), dim3(grid), dim3(kThreads), lds, s, p);
         return hipGetLastError();
     } else {
-        return hipErrorInvalidValue;  // never selected: staged_nsegx() only returns compatible widths
+        return hipErrorInvalidValue;  // never selected: staged_plan() only returns compatible shapes
     }
+}
+
+template <int FMT, int OUT, int NSEGX>
+hipError_t launch_staged_s(int R, int nbuf, const SParams& p, int grid, int lds, hipStream_t s) {
+    (void)nbuf;
+    if (R == 2) return launch_staged_t<FMT, OUT, NSEGX, 2, 2>(p, grid, lds, s);
+    if (R == 1) return launch_staged_t<FMT, OUT, NSEGX, 1, 2>(p, grid, lds, s);
+    return hipErrorInvalidValue;
 }
 
 template <int FMT, int OUT>
-hipError_t launch_staged_n(int nsegx, const SParams& p, int grid, int lds, hipStream_t s) {
+hipError_t launch_staged_n(int nsegx, int R, int nbuf, const SParams& p, int grid, int lds, hipStream_t s) {
     switch (nsegx) {
-    case 4: return launch_staged_t<FMT, OUT, 4>(p, grid, lds, s);
-    case 2: return launch_staged_t<FMT, OUT, 2>(p, grid, lds, s);
-    default: return launch_staged_t<FMT, OUT, 1>(p, grid, lds, s);
+    case 8: return launch_staged_s<FMT, OUT, 8>(R, nbuf, p, grid, lds, s);
+    case 4: return launch_staged_s<FMT, OUT, 4>(R, nbuf, p, grid, lds, s);
+    case 2: return launch_staged_s<FMT, OUT, 2>(R, nbuf, p, grid, lds, s);
+    default: return launch_staged_s<FMT, OUT, 1>(R, nbuf, p, grid, lds, s);
     }
 }
 
-hipError_t launch_staged(int f, int out, int nsegx, const SParams& p, int grid, int lds, hipStream_t s) {
+hipError_t launch_staged(int f, int out, int nsegx, int R, int nbuf, const SParams& p, int grid, int lds,
+                         hipStream_t s) {
     switch (f * 2 + out) {
-    case kNV12 * 2 + 0: return launch_staged_n<kNV12, 0>(nsegx, p, grid, lds, s);
-    case kNV12 * 2 + 1: return launch_staged_n<kNV12, 1>(nsegx, p, grid, lds, s);
-    case kI420 * 2 + 0: return launch_staged_n<kI420, 0>(nsegx, p, grid, lds, s);
-    case kI420 * 2 + 1: return launch_staged_n<kI420, 1>(nsegx, p, grid, lds, s);
-    case kBGRX * 2 + 0: return launch_staged_n<kBGRX, 0>(nsegx, p, grid, lds, s);
-    case kBGRX * 2 + 1: return launch_staged_n<kBGRX, 1>(nsegx, p, grid, lds, s);
-    case kBGR * 2 + 0: return launch_staged_n<kBGR, 0>(nsegx, p, grid, lds, s);
-    default: return launch_staged_n<kBGR, 1>(nsegx, p, grid, lds, s);
+    case kNV12 * 2 + 0: return launch_staged_n<kNV12, 0>(nsegx, R, nbuf, p, grid, lds, s);
+    case kNV12 * 2 + 1: return launch_staged_n<kNV12, 1>(nsegx, R, nbuf, p, grid, lds, s);
+    case kI420 * 2 + 0: return launch_staged_n<kI420, 0>(nsegx, R, nbuf, p, grid, lds, s);
+    case kI420 * 2 + 1: return launch_staged_n<kI420, 1>(nsegx, R, nbuf, p, grid, lds, s);
+    case kBGRX * 2 + 0: return launch_staged_n<kBGRX, 0>(nsegx, R, nbuf, p, grid, lds, s);
+    case kBGRX * 2 + 1: return launch_staged_n<kBGRX, 1>(nsegx, R, nbuf, p, grid, lds, s);
+    case kBGR * 2 + 0: return launch_staged_n<kBGR, 0>(nsegx, R, nbuf, p, grid, lds, s);
+    default: return launch_staged_n<kBGR, 1>(nsegx, R, nbuf, p, grid, lds, s);
     }
 }
 
@@ -2668,9 +2757,23 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
                     continue;
                 }
             }
-            int nsegx = kn.staged ? staged_nsegx(f, (double)g0.cw / g0.rw, kStageRows, kSlot) : 0;
-            if (nsegx && kn.nsegx > 0 && kn.nsegx < nsegx && kStageRows % (4 / kn.nsegx) == 0) nsegx = kn.nsegx;
+            const double ratio = (double)g0.cw / g0.rw;
+            int nsegx = kn.staged ? staged_nsegx(f, ratio, 2, kSlot) : 0;
+            if (nsegx && kn.nsegx > 0 && kn.nsegx < nsegx && 2 % (4 / kn.nsegx) == 0) nsegx = kn.nsegx;
+            // Full-width tiles (512 columns, 2 KB row slots, one row per group): whole source rows per DMA
+            // and whole output rows per store sweep (EVAM_PP_NSEGX=8).
+            if (nsegx == 4 && kn.nsegx == 8 && DW > 256) {
+                const int span = (int)std::ceil(511 * ratio) + 3;  // source columns of a 512-column tile row
+                if (span * fmt_bpp(f) + 32 <= 2 * kSlot) nsegx = 8;
+            }
             if (nsegx) {
+                // Pipeline shape: R output rows per group, NBUF staging buffers (NBUF - 1 groups of DMA in
+                // flight).
+                int R = kn.stage_r > 0 ? kn.stage_r : 2, nbuf = kn.stage_nbuf > 0 ? kn.stage_nbuf : 2;
+                if (nsegx == 8) R = 1;
+                bool shape_ok = false;
+                for (const StagedShape& ss : kStagedShapes) shape_ok |= ss.R == R && ss.nbuf == nbuf;
+                if (!shape_ok || !staged_valid(nsegx, R)) { R = 2; nbuf = 2; }
                 SParams sp{};
                 sp.ox = g0.ox;
                 sp.rw = g0.rw;
@@ -2686,20 +2789,20 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
                 // ~4096 pixels per workgroup, but short enough tiles that small batches still put
                 // 8 workgroups on every CU (a whole clip-ring step is only 32 x 224 x 224 pixels).
                 // At most 16 rows: C4 (tw 128) runs 3-7 % faster at 16 than at 32 (profiles/r01ad_sweep_th*.txt).
-                int th = std::max(kStageRows, std::min(16, 4096 / tw));
+                int th = std::max(2, std::min(16, 4096 / tw));
                 const int64_t cols = (int64_t)per_launch * sp.tiles_x;
                 const int64_t want = 8 * (int64_t)h->n_cu;
-                if (cols * ((DH + th - 1) / th) < want) th = (int)std::max<int64_t>(kStageRows, cols * DH / want);
-                sp.TH = std::max(1, std::min(DH, kn.th > 0 ? kn.th : th));
-                sp.TH = (sp.TH + kStageRows - 1) / kStageRows * kStageRows;
+                if (cols * ((DH + th - 1) / th) < want) th = (int)std::max<int64_t>(2, cols * DH / want);
+                sp.TH = std::max(1, std::min(std::min(DH, 64), kn.th > 0 ? kn.th : th));  // <= 64: lane-held rows
+                sp.TH = std::min(64, (sp.TH + R - 1) / R * R);
                 sp.tiles_per_item = sp.tiles_x * ((DH + sp.TH - 1) / sp.TH);
                 const int np = f == kI420 ? 3 : (f == kNV12 ? 2 : 1);
                 sp.offBuf = cfg->out_dtype == EVAM_DTYPE_F32 ? kLutBytes : 0;
-                sp.buf_bytes = 2 * kStageRows * np * kSlot;
+                sp.buf_bytes = 2 * R * np * (nsegx > 4 ? 2 * kSlot : kSlot);
                 sp.color_rgb = color_rgb;
                 sp.fill = fill;
                 sp.ablate = kn.ablate;
-                const int lds = sp.offBuf + 2 * sp.buf_bytes;
+                const int lds = sp.offBuf + nbuf * sp.buf_bytes;
                 for (int m0 = mfirst[f]; m0 < mfirst[f + 1]; m0 += kArgItems) {
                     const int n = std::min(kArgItems, mfirst[f + 1] - m0);
                     fill_args(sp.items, m0, n);
@@ -2708,7 +2811,7 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
                     // XCD-contiguous tiles: C2 -1.4 %, C4 -3 % kernel time; a grid of one workgroup round or
                     // less (C5) gains nothing (profiles/r01ae_sweep_xcd.txt). EVAM_PP_XCD=0/1 forces it.
                     sp.xcd_remap = kn.xcd >= 0 ? kn.xcd : (int)(grid >= 8 * (int64_t)h->n_cu);
-                    hipError_t e = launch_staged(f, cfg->out_dtype, nsegx, sp, (int)grid, lds, h->stream);
+                    hipError_t e = launch_staged(f, cfg->out_dtype, nsegx, R, nbuf, sp, (int)grid, lds, h->stream);
                     if (e != hipSuccess) return fail(EVAM_PP_ERR_HIP, "kernel launch failed: %s", hipGetErrorString(e));
                     launches++;
                 }

@@ -49,9 +49,18 @@ def test_c1_bench_batch(evam, O, coracle, gpu):
     pp.close()
 
 
-def test_c2_bench_batch(evam, O, coracle, gpu):
-    """C2 headline: 32 distinct 1080p NV12 frames (pitch 1920) -> 32x3x512x512 fp32 normalised."""
+STAGED_SHAPES = {"default": {}, "r2": {"EVAM_PP_STAGE_R": "2", "EVAM_PP_NSEGX": "4"},
+                 "r1": {"EVAM_PP_STAGE_R": "1", "EVAM_PP_NSEGX": "4"}, "wide": {"EVAM_PP_NSEGX": "8"}}
+
+
+@pytest.mark.parametrize("shape", sorted(STAGED_SHAPES))
+def test_c2_bench_batch(evam, O, coracle, gpu, shape, monkeypatch):
+    """C2 headline: 32 distinct 1080p NV12 frames (pitch 1920) -> 32x3x512x512 fp32 normalised, through every
+    staged-kernel pipeline shape (rows per group x staging buffers)."""
     import torch
+
+    for k, v in STAGED_SHAPES[shape].items():
+        monkeypatch.setenv(k, v)
 
     wl = bench.WORKLOADS["c2"]
     imgs = bench.device_frames(evam, torch, wl, 32, gpu, seed=1234)
@@ -87,11 +96,14 @@ def test_c3_bench_roi_set(evam, O, coracle, gpu, seed):
 
 
 @pytest.mark.parametrize("placement", ["top_left", "center"])
-def test_c4_random_4k_letterbox(evam, O, coracle, gpu, placement):
+@pytest.mark.parametrize("shape", ["default", "r2", "wide"])
+def test_c4_random_4k_letterbox(evam, O, coracle, gpu, placement, shape, monkeypatch):
     """C4: random (not constant) 3840x2160 NV12 bench frames letterboxed to 640x640 fp32: every 6x gather
     (column taps 6dx+2, weights 1024/1024) on the real 4K pitch is checked, in both placements."""
     import torch
 
+    for k, v in STAGED_SHAPES[shape].items():
+        monkeypatch.setenv(k, v)
     wl = bench.WORKLOADS["c4"]
     imgs = bench.device_frames(evam, torch, wl, 2, gpu, seed=1234)
     info = bench.make_info(evam, wl)

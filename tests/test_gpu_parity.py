@@ -361,7 +361,8 @@ def test_stats_and_timing(evam, O, gpu):
     ((300, 180), (131, 97), "aspect-ratio"),        # odd DW -> PX 1, letterbox
     ((480, 270), (224, 224), "aspect-crop"),        # C5 shape: central crop
 ])
-@pytest.mark.parametrize("variant", ["auto", "wave", "px1", "px2", "noreuse", "staged", "staged_xcd"])
+@pytest.mark.parametrize("variant", ["auto", "wave", "px1", "px2", "noreuse", "staged", "staged_xcd", "staged_r1",
+                                     "staged_wide"])
 def test_wave_kernel_variants(evam, O, coracle, gpu, fmt, src, dst, resize, variant, monkeypatch):
     """Uniform-geometry batches through the default kernel choice, the wave-row kernel forced
     (EVAM_PP_WAVE=2; every PX / REUSE choice) and the staged kernel (EVAM_PP_WAVE=0; with the
@@ -371,7 +372,9 @@ def test_wave_kernel_variants(evam, O, coracle, gpu, fmt, src, dst, resize, vari
 
     env = {"wave": {"EVAM_PP_WAVE": "2"}, "px1": {"EVAM_PP_WAVE": "2", "EVAM_PP_PX": "1"},
            "px2": {"EVAM_PP_WAVE": "2", "EVAM_PP_PX": "2"}, "noreuse": {"EVAM_PP_WAVE": "2", "EVAM_PP_REUSE": "0"},
-           "staged": {"EVAM_PP_WAVE": "0"}, "staged_xcd": {"EVAM_PP_WAVE": "0", "EVAM_PP_XCD": "1"}}.get(variant, {})
+           "staged": {"EVAM_PP_WAVE": "0"}, "staged_xcd": {"EVAM_PP_WAVE": "0", "EVAM_PP_XCD": "1"},
+           "staged_r1": {"EVAM_PP_WAVE": "0", "EVAM_PP_STAGE_R": "1"},
+           "staged_wide": {"EVAM_PP_WAVE": "0", "EVAM_PP_NSEGX": "8"}}.get(variant, {})
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     if variant == "px2" and dst[0] % 2:
