@@ -36,6 +36,10 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+# VALU issue ceiling in wave64 instructions/s: 256 CUs x 4 SIMDs, one wave-instruction per 2 cycles per SIMD
+# (32 lanes/cycle), 2.4 GHz max clock (MI355X_MICROARCH.md, Wave scheduling / chip parameters)
+VALU_PEAK_GINST = 256 * 4 * 2.4e9 / 2 / 1e9
+VALU_BOUND_CONFIGS = ("c1",)  # u8 output: a fifth of C2's bytes for the same pixels, integer-issue bound
 METRIC = "pre-processed frames/sec (1080p NV12→512² NCHW fp32) 1–8 GPU; % HBM peak"
 BGR_MEAN = (0.406, 0.456, 0.485)
 BGR_STD = (0.225, 0.224, 0.229)
@@ -154,6 +158,94 @@ def load_pmc_traffic(config_name: str, n_frames_per_launch: int, pool: int):
     return None
 
 
+PIPE_TEMPLATE = {
+    "type": "GStreamer",
+    "template": ["{auto_source} ! decodebin",
+                 " ! gvadetect model={models[bench_detector][1][network]} name=detection",
+                 " ! gvametaconvert name=metaconvert ! appsink name=appsink"],
+    "description": "bench: full-frame detection pre-processing through the pipeline-server counterpart",
+    "parameters": {"type": "object", "properties": {
+        "detection-properties": {"element": {"name": "detection", "format": "element-properties"}}}},
+}
+IR_STUB = ('<?xml version="1.0"?><net name="bench_detector" version="11"><layers><layer id="0" name="data" '
+           'type="Parameter" version="opset1"><data shape="1,3,{h},{w}" element_type="f32"/></layer></layers></net>')
+
+
+def via_pipeline(args, evam, torch, wl, device_index):
+    """C2 frames through PipelineServer: `streams` application-source pipelines on one device, each fed
+    `frames` device-resident frames; the per-device batching hub coalesces them into batched launches.
+    The registered detector returns no detections, so the line measures pre-processing plus the pipeline
+    machinery (queues, per-frame results, hub hand-off), not a model."""
+    import queue
+    import tempfile
+
+    ps = evam.pipeline_server
+    tmp = tempfile.mkdtemp(prefix="evam_bench_")
+    pdir = os.path.join(tmp, "pipelines", "object_detection", "bench")
+    os.makedirs(pdir)
+    json.dump(PIPE_TEMPLATE, open(os.path.join(pdir, "pipeline.json"), "w"))
+    DW, DH = wl["dst"]
+    mdir = os.path.join(tmp, "models", "bench_detector", "1")
+    os.makedirs(os.path.join(mdir, "FP32"))
+    open(os.path.join(mdir, "FP32", "bench_detector.xml"), "w").write(IR_STUB.format(w=DW, h=DH))
+    proc = {"input_preproc": [{"format": "image", "params": {"range": [0.0, 1.0], "mean": list(BGR_MEAN),
+                                                             "std": list(BGR_STD)}}] if wl["norm"] else []}
+    json.dump(proc, open(os.path.join(mdir, "bench_detector.json"), "w"))
+    empty = torch.full((1, 1, 7), -1.0)
+
+    def detector(t):
+        return empty.expand(t.shape[0], 1, 7)
+
+    S, F = args.streams, args.frames_per_stream
+    ps.PipelineServer.start({"pipeline_dir": os.path.join(tmp, "pipelines"), "model_dir": os.path.join(tmp, "models"),
+                             "device": device_index, "batch_max": args.hub_batch, "batch_wait_ms": 1.0,
+                             "batch_target": args.hub_batch})
+    ps.PipelineServer.register_model("bench_detector/1", ps.InferenceModel(detector, (DW, DH), name="bench"))
+    pool = device_frames(evam, torch, wl, 2 * S, torch.device(f"cuda:{device_index}"), seed=99)
+
+    def run(frames_per_stream):
+        qs, pipes = [], []
+        for k in range(S):
+            q = queue.Queue()
+            for t in range(frames_per_stream):
+                q.put(pool[(k + t * S) % len(pool)])
+            q.put(None)
+            qs.append(q)
+        t0 = time.perf_counter()
+        for k in range(S):
+            p = ps.PipelineServer.pipeline("object_detection", "bench")
+            p.start(source={"type": "application", "input": qs[k]}, destination={},
+                    parameters={"detection-properties": {"batch-size": args.stream_batch}})
+            pipes.append(p)
+        for p in pipes:
+            st = p.wait(600)
+            if st["state"] != "COMPLETED":
+                raise RuntimeError(f"pipeline ended {st}")
+        torch.cuda.synchronize()
+        return time.perf_counter() - t0
+
+    run(max(2, args.stream_batch))  # warm-up: hub thread, handles, CUDA context
+    ps.PipelineServer.hub().batches.clear()
+    el = run(F)
+    sizes = [b[1] for b in ps.PipelineServer.hub().batches]
+    ps.PipelineServer.stop()
+    return {"value": round(S * F / el, 1), "elapsed_s": round(el, 4), "streams": S, "frames_per_stream": F,
+            "stream_batch_size": args.stream_batch, "hub_launches": len(sizes),
+            "mean_frames_per_launch": round(float(np.mean(sizes)), 2) if sizes else 0.0}
+
+
+def load_pmc_valu(config_name: str, n_frames_per_launch: int, pool: int):
+    """Wave-level VALU instructions per launch from the committed rocprofv3 PMC summary, if any."""
+    path = os.path.join(ROOT, "profiles", "pmc_valu.json")
+    try:
+        e = json.load(open(path)).get(config_name)
+        if e and e.get("frames_per_launch") == n_frames_per_launch and e.get("pool_sets", 1) == pool:
+            return int(e["valu_insts_per_launch"])
+    except Exception:
+        return None
+    return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -171,6 +263,14 @@ def main():
                          "1: one resident set)")
     ap.add_argument("--resident-steps", type=int, default=200,
                     help="extra steps on one resident set, reported as roofline.resident (0: skip)")
+    ap.add_argument("--via", choices=["direct", "pipeline"], default="direct",
+                    help="pipeline: drive the workload's frames through PipelineServer (application-source "
+                         "pipelines, one per stream, batched across streams by the per-device hub); reported "
+                         "as its own line next to the direct kernel rate")
+    ap.add_argument("--streams", type=int, default=32, help="--via pipeline: pipelines (streams)")
+    ap.add_argument("--frames-per-stream", type=int, default=256, help="--via pipeline: frames per stream")
+    ap.add_argument("--stream-batch", type=int, default=8, help="--via pipeline: gvadetect batch-size per stream")
+    ap.add_argument("--hub-batch", type=int, default=128, help="--via pipeline: max frames per hub launch")
     args = ap.parse_args()
 
     import torch
@@ -196,6 +296,18 @@ def main():
     torch.cuda.set_device(device)
 
     wl = WORKLOADS[args.config]
+    if args.via == "pipeline":
+        if world > 1 or wl.get("rois") or wl.get("ring"):
+            raise SystemExit("--via pipeline is wired for one process and full-frame detection configs (c1, c2, c4)")
+        r = via_pipeline(args, evam, torch, wl, local)
+        print(json.dumps({
+            "metric": f"{METRIC} [{args.config}, via PipelineServer]", "value": r["value"], "unit": "frames/s",
+            "n_gpus": 1, "higher_is_better": True, "dtype": "u8" if wl["dtype"] == "u8" else "u8->f32",
+            "data": "synthetic device-resident frames through application sources; null detector",
+            "config": {"workload": wl["desc"], **r,
+                       "path": "Pipeline thread per stream -> gvadetect stage -> per-device BatchHub -> one "
+                               "evam_pp_run per tick -> model -> per-frame results"}}), flush=True)
+        return
     n = args.frames or wl["frames"]
     strong = args.config == "c4" and world > 1 and not args.frames
     if strong:  # C4 is a fixed set of 64 streams, partitioned s mod G (strong split)
@@ -344,6 +456,18 @@ def main():
                          "algorithmic_bytes_per_launch": alg_bytes, "mean_launch_ms": round(kern_ms, 5),
                          "launch_ms_p10_p50_p90": [pct[10], pct[50], pct[90]], "resident": resident},
         }
+        valu = load_pmc_valu(args.config, n, P) if args.config in VALU_BOUND_CONFIGS else None
+        if valu:
+            # integer-issue-bound workload: the roofline that bounds it is the VALU issue rate; the HBM
+            # figures stay as a secondary block
+            r = res["roofline"]
+            hbm = {k: r[k] for k in ("achieved", "peak", "unit", "frac", "traffic")}
+            g = valu / (kern_ms * 1e-3) / 1e9
+            res["roofline"] = {"bound": "valu", "achieved": round(g, 1), "peak": VALU_PEAK_GINST,
+                               "unit": "G wave64-VALU-inst/s", "frac": round(g / VALU_PEAK_GINST, 4),
+                               "traffic": r["traffic"], "valu_insts_per_launch": valu, "hbm": hbm,
+                               **{k: r[k] for k in ("algorithmic_bytes_per_launch", "mean_launch_ms",
+                                                    "launch_ms_p10_p50_p90", "resident")}}
         if feed is not None:
             res["h2d"] = {"bytes_per_step": feed.bytes_per_batch,
                           "GBps": round(feed.bytes_per_batch * args.steps / wall_max / 1e9, 2),

@@ -949,8 +949,13 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_staged(const SParams P) {
                 const uint8_t* sv1 = FMT == kNV12 ? sc1 + 1 : sc1 + 2 * R * SLOT;
                 const UVs tA = uv_terms_sat(sc0[lC0j], sv0[lC0j]);
                 const UVs tB = uv_terms_sat(sc0[lC1j], sv0[lC1j]);
-                const UVs tC = uv_terms_sat(sc1[lC0j], sv1[lC0j]);
-                const UVs tD = uv_terms_sat(sc1[lC1j], sv1[lC1j]);
+                // both vertical taps in one chroma row (wave-uniform, ~half the rows of a 2:1 chroma
+                // downscale): its terms are reused instead of read and converted again
+                UVs tC = tA, tD = tB;
+                if (!share) {
+                    tC = uv_terms_sat(sc1[lC0j], sv1[lC0j]);
+                    tD = uv_terms_sat(sc1[lC1j], sv1[lC1j]);
+                }
                 const uint32_t yA = luma_term(sy0[lY0j]), yB = luma_term(sy0[lY1j]);
                 const uint32_t yC = luma_term(sy1[lY0j]), yD = luma_term(sy1[lY1j]);
                 v[0] = vfinal<OUT>(hpass_sat(yA, tA.b, yB, tB.b, wpj), hpass_sat(yC, tC.b, yD, tD.b, wpj), wb0, wb1);

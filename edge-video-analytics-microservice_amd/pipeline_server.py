@@ -20,12 +20,17 @@ templates. Loading a template covers:
   - ``"format": "json"``;
   - defaults, including ``{env[VAR]}``.
 
-The inference elements are ``gvadetect``, ``gvaclassify`` and ``gvaactionrecognitionbin``. Each one
-with ``pre-process-backend=hip`` gets a ``HipPreProcessor``; ``hip`` is also the default when the
-property is absent. Each element then runs:
-1. batched frame or ROI pre-processing on the GPU;
-2. the registered model (a torch callable: OpenVINO is not part of this stack);
-3. post-processing (``postproc.py``: transform-mapped boxes, ``tensor_to_label``, gvametaconvert JSON).
+The inference elements are ``gvadetect``, ``gvaclassify`` and ``gvaactionrecognitionbin``; each one
+with ``pre-process-backend=hip`` runs on the HIP path (``hip`` is also the default when the property is
+absent). Each element:
+1. gates and selects its stream's work on the pipeline's thread (``inference-interval``, ``object-class``,
+   ``reclassify-interval``);
+2. hands it to the device's :class:`BatchHub`, which coalesces the requests of every pipeline with an
+   interchangeable element into ONE batched pre-processing launch and one model call per tick (bounded
+   by a unit count and a latency budget) — the reference runs one pipeline per stream and never batches
+   across them (``evas/manager.py:127-141``);
+3. runs the registered model (a torch callable: OpenVINO is not part of this stack);
+4. post-processes (``postproc.py``: transform-mapped boxes, ``tensor_to_label``, gvametaconvert JSON).
 
 Decode stays upstream. An ``application`` source delivers decoded frames:
 device ``Image``s, or host planes uploaded on arrival.
@@ -308,13 +313,129 @@ def roi_inside(x: int, y: int, w: int, h: int, W: int, H: int) -> bool:
     return min(x + w, W) - max(x, 0) > 0 and min(y + h, H) - max(y, 0) > 0
 
 
+class _Request:
+    """One pipeline's share of a hub batch: its items, and an event the pipeline thread waits on."""
+
+    __slots__ = ("stage", "items", "units", "t0", "done", "error")
+
+    def __init__(self, stage, items, units):
+        self.stage = stage
+        self.items = items
+        self.units = units
+        self.t0 = time.perf_counter()
+        self.done = threading.Event()
+        self.error = None
+
+
+class BatchHub:
+    """Per-device batching hub: one ``evam_pp_run`` (and one model call) per stage key per tick, over the
+    frames / ROIs of every pipeline the device owns.
+
+    The reference runs one GStreamer pipeline per camera stream (``evas/manager.py:127-141``) and each
+    inference element batches only its own stream's frames (``batch-size``). On a GPU that leaves the
+    launch nearly empty: one 1080p frame is ~1 us of HBM work against a ~5 us launch floor. The hub
+    coalesces the requests of all pipelines whose inference elements are interchangeable (same model,
+    same pre-processing, same element properties: ``stage.hub_key()``) into one batch, bounded by
+    ``max_batch`` units (frames, or ROIs for gvaclassify) and a latency budget ``max_wait_s`` after the
+    oldest pending request; ``target`` flushes as soon as that many units are pending. Every pipeline
+    thread blocks only on its own request, so a slow stream never holds up a tick beyond the budget.
+    """
+
+    def __init__(self, device: int, max_batch: int = 64, max_wait_s: float = 0.002, target: int | None = None):
+        self.device = int(device)
+        self.max_batch = max(1, int(max_batch))
+        self.max_wait_s = float(max_wait_s)
+        self.target = int(target) if target else None
+        self._pending: dict = {}
+        self._cv = threading.Condition()
+        self._stop = False
+        self._pp = None
+        self.batches: list = []        # (key, units, requests) per executed batch (inspection / tests)
+        self._thread = threading.Thread(target=self._loop, name=f"evam-hub-{device}", daemon=True)
+        self._thread.start()
+
+    def pp(self):
+        if self._pp is None:
+            from .preproc import HipPreProcessor
+
+            self._pp = HipPreProcessor(device=self.device)
+        return self._pp
+
+    def submit(self, stage, items, units: int):
+        """Queue ``items`` of ``stage`` and block until the batch holding them ran (re-raises its error)."""
+        if units <= 0:
+            return
+        req = _Request(stage, items, units)
+        with self._cv:
+            if self._stop:
+                raise RuntimeError("batch hub is closed")
+            self._pending.setdefault(stage.hub_key(), []).append(req)
+            self._cv.notify_all()
+        req.done.wait()
+        if req.error is not None:
+            raise req.error
+
+    def _ready(self, now):
+        """(key, requests) to run now, or (None, wait seconds)."""
+        wait = None
+        for key, reqs in self._pending.items():
+            units = sum(r.units for r in reqs)
+            if units >= (self.target or self.max_batch) or now - reqs[0].t0 >= self.max_wait_s:
+                take, n = [], 0
+                while reqs and (not take or n + reqs[0].units <= self.max_batch):
+                    n += reqs[0].units
+                    take.append(reqs.pop(0))
+                if not reqs:
+                    del self._pending[key]
+                return key, take
+            left = self.max_wait_s - (now - reqs[0].t0)
+            wait = left if wait is None else min(wait, left)
+        return None, wait
+
+    def _loop(self):
+        while True:
+            with self._cv:
+                while True:
+                    if self._stop and not self._pending:
+                        return
+                    key, take = self._ready(time.perf_counter())
+                    if key is not None:
+                        break
+                    self._cv.wait(timeout=take)
+            try:
+                take[0].stage.run_batch(take, self.pp())
+                self.batches.append((key, sum(r.units for r in take), len(take)))
+                if len(self.batches) > 4096:
+                    del self.batches[:2048]
+            except BaseException as e:  # noqa: BLE001 — delivered to every waiting pipeline
+                for r in take:
+                    r.error = e
+            for r in take:
+                r.done.set()
+
+    def close(self):
+        with self._cv:
+            self._stop = True
+            self._cv.notify_all()
+        self._thread.join(10)
+        if self._pp is not None:
+            self._pp.close()
+            self._pp = None
+
+
 class _InferenceStage:
-    """Common part of gvadetect / gvaclassify: interval gating, model lookup, HIP pre-processor."""
+    """Common part of gvadetect / gvaclassify: interval gating, model lookup, HIP pre-processing.
+
+    ``process(items)`` runs on the pipeline's own thread: it gates and selects the work of this stream,
+    then hands it to the server's per-device :class:`BatchHub`, which executes ``run_batch`` for the
+    requests of all pipelines sharing ``hub_key()``.
+    """
 
     def __init__(self, el: Element, server, device: int):
         self.el = el
         self.backend = _backend_of(el)
         self.device = device
+        self.server = server
         net = el.properties.get("model") or el.properties.get("enc-model")
         self.model = server.model_for(net)
         if self.model is None:
@@ -328,6 +449,13 @@ class _InferenceStage:
         self.batch_size = int(el.properties.get("batch-size", 1))
         self._pp = None
         self.info = self.model.preproc_info()
+
+    def out_dtype(self) -> int:
+        return N.DTYPE_F32 if self.model.out_dtype == "f32" else N.DTYPE_U8
+
+    def hub_key(self):
+        """Stages with equal keys are interchangeable: their requests run as one batch."""
+        return (self.el.factory, id(self.model), self.info.cache_key(self.out_dtype()), self.threshold)
 
     def pp(self):
         if self._pp is None:
@@ -353,10 +481,13 @@ class DetectStage(_InferenceStage):
     def process(self, items):
         """items: list of (frame_index, Image, FrameResult). Appends regions to each FrameResult."""
         run = [it for it in items if it[0] % self.interval == 0]
-        if not run:
-            return
+        self.server.hub().submit(self, run, len(run))
+
+    def run_batch(self, reqs, pp):
+        """One launch over the frames of every request (hub thread)."""
+        run = [it for r in reqs for it in r.items]
         out = self._tensor(len(run))
-        xfs = self.pp().convert([img for _, img, _ in run], out, self.info, want_transform=True)
+        xfs = pp.convert([img for _, img, _ in run], out, self.info, want_transform=True)
         raw = self.model.fn(out)
         raw = raw.detach().float().cpu().numpy() if hasattr(raw, "detach") else raw
         W, H = self.model.input_size
@@ -370,31 +501,71 @@ class DetectStage(_InferenceStage):
 
 
 class ClassifyStage(_InferenceStage):
+    """gvaclassify: the regions of each frame whose label matches ``object-class``, batched across pipelines.
+
+    ``reclassify-interval`` (``pipelines/object_classification/vehicle_attributes/pipeline.json:68-71``):
+    as in DL Streamer, it applies to tracked objects (regions with a non-zero ``object_id``, from gvatrack):
+    such an object is classified again only every N-th frame of its stream, and in between its last
+    results are attached again. Untracked regions (object_id 0) are classified on every gated frame.
+    """
+
     def __init__(self, el, server, device):
         super().__init__(el, server, device)
         oc = el.properties.get("object-class")
         self.object_class = set(str(oc).split(",")) if oc else None
-        self.reclassify = int(el.properties.get("reclassify-interval", 1))
+        self.reclassify = max(1, int(el.properties.get("reclassify-interval", 1)))
+        self._cache: dict = {}   # object_id -> (frame index classified at, tensors)
+
+    def hub_key(self):
+        oc = tuple(sorted(self.object_class)) if self.object_class else None
+        return super().hub_key() + (oc,)
 
     def process(self, items):
-        from .preproc import Roi
-
-        frames, rois, owners = [], [], []
+        work = []          # (frame_index, Image, [regions to classify])
         for fi, img, fr in items:
             if fi % self.interval:
                 continue
-            idx = len(frames)
-            frames.append(img)
+            todo = []
             for r in fr.regions:
-                if self.object_class is None or r.label in self.object_class:
-                    if not roi_inside(r.x, r.y, r.w, r.h, img.width, img.height):
-                        continue  # degenerate box: the C ABI would read w/h <= 0 as "full frame"
-                    rois.append(Roi(idx, r.x, r.y, r.w, r.h))
+                if self.object_class is not None and r.label not in self.object_class:
+                    continue
+                if not roi_inside(r.x, r.y, r.w, r.h, img.width, img.height):
+                    continue  # degenerate box: the C ABI would read w/h <= 0 as "full frame"
+                if r.object_id and self.reclassify > 1:
+                    hit = self._cache.get(r.object_id)
+                    if hit is not None and fi - hit[0] < self.reclassify:
+                        r.tensors.extend(hit[1])
+                        continue
+                todo.append(r)
+            if todo:
+                work.append((fi, img, todo))
+        self.server.hub().submit(self, work, sum(len(t) for _, _, t in work))
+        if self.reclassify > 1:
+            for fi, _, todo in work:
+                for r in todo:
+                    if r.object_id:
+                        self._cache[r.object_id] = (fi, [t for t in r.tensors if t.model == self.model.name])
+            if len(self._cache) > 65536:
+                self._cache.clear()
+
+    def run_batch(self, reqs, pp):
+        """One ROI launch over the regions of every request (hub thread)."""
+        import numpy as np
+
+        frames, rois, owners = [], [], []
+        for req in reqs:
+            for _, img, todo in req.items:
+                idx = len(frames)
+                frames.append(img)
+                for r in todo:
+                    rois.append((idx, r.x, r.y, r.w, r.h))
                     owners.append(r)
         if not rois:
             return
+        from .preproc import RoiBatch
+
         out = self._tensor(len(rois))
-        self.pp().convert(frames, out, self.info, rois=rois)
+        pp.convert(frames, out, self.info, rois=RoiBatch(np.asarray(rois, dtype=np.int32)))
         res = self.model.fn(out)
         posts = self.model.postprocs() or [{}]
         if not isinstance(res, dict):
@@ -410,7 +581,11 @@ class ClassifyStage(_InferenceStage):
 
 
 class ActionRecognitionStage(_InferenceStage):
-    """gvaactionrecognitionbin encoder input: aspect+central-crop into a 16-slot per-stream clip ring."""
+    """gvaactionrecognitionbin encoder input: aspect+central-crop into a 16-slot per-stream clip ring.
+
+    Runs on the pipeline's own handle, not through the hub: each stream owns its ring and writes slot
+    ``t % 16`` of it, so frames of different streams land in different tensors at different slots.
+    """
 
     CLIP = 16
 
@@ -625,6 +800,25 @@ class _Server:
         self.instances: list[Pipeline] = []
         self.started = False
         self.device = 0
+        self._hub = None
+        self._hub_lock = threading.Lock()
+
+    def hub(self) -> BatchHub:
+        """The device's batching hub (created on first use; options ``batch_max``, ``batch_wait_ms``,
+        ``batch_target``)."""
+        with self._hub_lock:
+            if self._hub is None:
+                o = self.options
+                self._hub = BatchHub(self.device, max_batch=int(o.get("batch_max", 64)),
+                                     max_wait_s=float(o.get("batch_wait_ms", 2.0)) / 1e3,
+                                     target=o.get("batch_target"))
+            return self._hub
+
+    def close_hub(self):
+        with self._hub_lock:
+            if self._hub is not None:
+                self._hub.close()
+                self._hub = None
 
     def start(self, options=None):
         o = dict(options or {})
@@ -719,4 +913,10 @@ class PipelineServer:
         for p in list(_SERVER.instances):
             p.wait(5.0)
         _SERVER.instances.clear()
+        _SERVER.close_hub()
         _SERVER.started = False
+
+    @staticmethod
+    def hub():
+        """The per-device batching hub (inspection: ``hub().batches``)."""
+        return _SERVER.hub()

@@ -306,3 +306,120 @@ def test_end_to_end_action_ring(ps, evam, model_dir, gpu, O):
         c.preprocess_item(frames[i], None, ref, i, mode=2, lut=O.np_norm_lut(0))
     assert np.array_equal(seen[0].cpu().numpy(), ref)
     ps.PipelineServer.stop()
+
+
+@pytest.mark.gpu
+def test_hub_batches_across_pipelines(ps, evam, model_dir, gpu, O):
+    """Four application-source pipelines on one device: the batching hub runs ONE detection launch over the
+    four streams' frames and ONE ROI launch over their vehicles per tick (the reference runs one pipeline
+    per stream, evas/manager.py:127-141, and never batches across them), and every classifier input row is
+    bit-exact with the oracle's pre-processing of that stream's ROI."""
+    import torch
+
+    calls, cls_inputs = [], []
+
+    def detector(t):
+        calls.append(("det", tuple(t.shape)))
+        n = t.shape[0]
+        out = torch.full((n, 3, 7), -1.0)
+        out[:, 0] = torch.tensor([0, 1, 0.9, 0.25, 0.25, 0.5, 0.75])     # car
+        out[:, 1] = torch.tensor([0, 2, 0.8, 0.0, 0.0, 0.1, 0.1])        # person (not classified)
+        return out
+
+    def classifier(t):
+        calls.append(("cls", tuple(t.shape)))
+        cls_inputs.append(t.detach().cpu().numpy().copy())
+        m = t.mean(dim=(1, 2, 3))
+        return {"color": torch.stack([1 - m, m], 1)}
+
+    ps.PipelineServer.start({"pipeline_dir": PIPES, "model_dir": model_dir, "batch_target": 4,
+                             "batch_wait_ms": 20000})
+    ps.PipelineServer.register_model("det_alias/det_ver", ps.InferenceModel(detector, (64, 64), name="det"))
+    ps.PipelineServer.register_model("cls_alias/cls_ver", ps.InferenceModel(classifier, (24, 24), name="cls"))
+    rng = np.random.default_rng(17)
+    frames = [O.random_frame(rng, O.NV12, 320, 180) for _ in range(4)]
+    pipes, outs = [], []
+    for f in frames:
+        qin, qout = queue.Queue(), queue.Queue()
+        qin.put({"fourcc": f.fourcc, "width": f.width, "height": f.height, "planes": f.planes})
+        qin.put(None)
+        p = ps.PipelineServer.pipeline("detect_classify", "hip")
+        p.start(source={"type": "application", "input": qin},
+                destination={"metadata": {"type": "application", "output": qout, "mode": "json"}})
+        pipes.append(p)
+        outs.append(qout)
+    for p in pipes:
+        st = p.wait(120)
+        assert st["state"] == "COMPLETED", st
+    assert calls.count(("det", (4, 3, 64, 64))) == 1 and calls.count(("cls", (4, 3, 24, 24))) == 1, calls
+    assert len(calls) == 2
+    hub_batches = ps.PipelineServer.hub().batches
+    assert sorted(b[1:] for b in hub_batches) == [(4, 4), (4, 4)]     # (units, requests) per launch
+    # every classifier row is one stream's car ROI, pre-processed exactly as the oracle does
+    info = ps.InferenceModel(None, (24, 24), json.load(open(os.path.join(
+        model_dir, "cls_alias", "cls_ver", "cls_alias-cls_ver.json")))).preproc_info()
+    c = O.COracle()
+    ref = np.zeros((4, 3, 24, 24), np.float32)
+    lut = O.np_norm_lut(1, info.range)
+    for i, f in enumerate(frames):
+        c.preprocess_item(f, (80, 45, 80, 90), ref, i, color_rgb=True, lut=lut)
+    got = cls_inputs[0]
+    matched = sorted(next(j for j in range(4) if np.array_equal(got[k], ref[j])) for k in range(4))
+    assert matched == [0, 1, 2, 3]
+    for q in outs:
+        d = json.loads(q.get(timeout=5))
+        car = d["objects"][0]
+        assert (car["x"], car["y"], car["w"], car["h"]) == (80, 45, 80, 90) and "color" in car
+    ps.PipelineServer.stop()
+
+
+def test_classify_reclassify_interval(ps, evam):
+    """gvaclassify reclassify-interval (pipelines/object_classification/vehicle_attributes/pipeline.json:68-71):
+    a tracked region (object_id != 0) is sent for classification only every N-th frame of its stream and gets
+    its last results attached in between; untracked regions are classified every frame; degenerate boxes are
+    never sent (the C ABI would read w/h <= 0 as the full frame)."""
+    P = evam.postproc
+
+    class FakeHub:
+        def __init__(self):
+            self.sent = []
+
+        def submit(self, stage, items, units):
+            for fi, img, todo in items:
+                for r in todo:
+                    self.sent.append((fi, r.object_id))
+                    r.tensors.append(P.Tensor("color", 0.9, 1, "light", model="cls"))
+
+    hub = FakeHub()
+
+    class FakeServer:
+        device = 0
+
+        def model_for(self, net):
+            return ps.InferenceModel(None, (24, 24), {"input_preproc": []}, name="cls")
+
+        def hub(self):
+            return hub
+
+    el = ps.Element("gvaclassify", {"model": "m.xml", "reclassify-interval": "3", "object-class": "car"})
+    st = ps.ClassifyStage(el, FakeServer(), 0)
+
+    class Img:
+        width, height = 320, 180
+
+    def region(oid, x=10, w=40, label="car"):
+        return P.Region(x, 10, w, 30, (0, 0, 0.1, 0.1), label, 1, 0.9, object_id=oid)
+
+    results = []
+    for fi in range(7):
+        fr = P.FrameResult(320, 180, regions=[region(5), region(0), region(6, label="person"), region(7, x=400),
+                                             region(8, w=0)])
+        st.process([(fi, Img(), fr)])
+        results.append(fr)
+    tracked = [fi for fi, oid in hub.sent if oid == 5]
+    untracked = [fi for fi, oid in hub.sent if oid == 0]
+    assert tracked == [0, 3, 6] and untracked == list(range(7))
+    assert {oid for _, oid in hub.sent} == {0, 5}                   # person, off-frame, zero-width: never sent
+    for fr in results:
+        assert len(fr.regions[0].tensors) == 1 and fr.regions[0].tensors[0].label == "light"
+        assert fr.regions[2].tensors == [] and fr.regions[3].tensors == [] and fr.regions[4].tensors == []

@@ -113,6 +113,34 @@ __global__ __launch_bounds__(256) void shape(const uint8_t* __restrict__ src, fl
         for (int r = 0; r < BAND; r++) { loads(r); stores(r); }
         return;
     }
+    if (MODE == 4 || MODE == 5) {
+        // stores of row r carry a value derived from row r's loads (read back from LDS after a barrier):
+        // the staged kernel's dependency, with MODE 5 prefetching one row ahead (double buffer)
+        auto stores_dep = [&](int r, uint32_t v) {
+            const int oy = band * BAND + r;
+            float* o = dst + (size_t)frame * kDW * kDH * 3 + (size_t)oy * kDW + tx * WCOLS;
+            for (int x = tid; x < WCOLS; x += 256)
+                for (int pl = 0; pl < 3; pl++) o[(size_t)pl * kDW * kDH + x] = (float)(v + pl);
+        };
+        if (MODE == 4) {
+            for (int r = 0; r < BAND; r++) {
+                loads(r);
+                __syncthreads();
+                stores_dep(r, stage[tid >> 6][tid & 63].x);
+                __syncthreads();
+            }
+        } else {
+            loads(0);
+            for (int r = 0; r < BAND; r++) {
+                __syncthreads();
+                const uint32_t v = stage[tid >> 6][tid & 63].x;
+                __syncthreads();
+                if (r + 1 < BAND) loads(r + 1);
+                stores_dep(r, v);
+            }
+        }
+        return;
+    }
     if (MODE != 2) for (int r = 0; r < BAND; r++) loads(r);
     if (MODE != 1) for (int r = 0; r < BAND; r++) stores(r);
 }
@@ -167,5 +195,6 @@ int main() {
     SHAPE(256, 16, 0, alg) SHAPE(256, 16, 1, 96.1e6) SHAPE(256, 16, 2, 100.66e6) SHAPE(256, 16, 3, alg)
     SHAPE(512, 4, 0, alg) SHAPE(512, 4, 1, 96.1e6) SHAPE(512, 4, 2, 100.66e6) SHAPE(512, 4, 3, alg)
     SHAPE(512, 2, 0, alg) SHAPE(512, 2, 3, alg)
+    SHAPE(256, 16, 4, alg) SHAPE(256, 16, 5, alg) SHAPE(512, 8, 4, alg) SHAPE(512, 8, 5, alg)
     return 0;
 }

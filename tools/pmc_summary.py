@@ -32,6 +32,18 @@ def main(d, config=None, frames_per_launch=None, traffic_json=None, pool_sets=1)
                                    "streaming reads (MI355X_MICROARCH.md, HBM), WRITE_SIZE (KB) as is",
                          "source": os.path.relpath(d)}
             json.dump(t, open(traffic_json, "w"), indent=1)
+    if "SQ_INSTS_VALU" in out and traffic_json and config:
+        vj = os.path.join(os.path.dirname(traffic_json), "pmc_valu.json")
+        t = json.load(open(vj)) if os.path.exists(vj) else {}
+        t[config] = {"frames_per_launch": frames_per_launch, "pool_sets": pool_sets,
+                     "valu_insts_per_launch": int(out["SQ_INSTS_VALU"]),
+                     **{k: out[k] for k in ("SQ_ACTIVE_INST_VALU", "SQ_INSTS_SALU", "SQ_WAVES", "GRBM_GUI_ACTIVE",
+                                            "SQ_INSTS_LDS", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES") if k in out},
+                     "method": "rocprofv3 --pmc SQ_INSTS_VALU ..., mean per dispatch of the evam_pp kernel "
+                               "(wave-level VALU instructions)",
+                     "source": os.path.relpath(d)}
+        json.dump(t, open(vj, "w"), indent=1)
+        print(f"valu_insts_per_launch = {int(out['SQ_INSTS_VALU'])}")
     json.dump(out, open(os.path.join(d, "summary.json"), "w"), indent=1)
 
 
