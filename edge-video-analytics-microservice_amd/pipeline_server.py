@@ -50,6 +50,7 @@ from dataclasses import dataclass, field
 from . import _native as N
 from . import postproc as P
 from ._native import PreProcError
+from .preproc import Image
 
 INFERENCE_ELEMENTS = ("gvadetect", "gvaclassify", "gvaactionrecognitionbin", "gvainference")
 HIP_BACKENDS = ("hip",)
@@ -494,10 +495,11 @@ class DetectStage(_InferenceStage):
         labels = None
         for pp_ in self.model.postprocs():
             labels = pp_.get("labels", labels)
-        for k, (_, img, fr) in enumerate(run):
-            dets = P.parse_ssd(raw[k], self.threshold)
-            fr.regions.extend(P.detections_to_regions(dets, xfs[k], img.width, img.height, W, H, labels,
-                                                      model=self.model.name))
+        for k, dets in enumerate(P.parse_ssd_batch(raw, self.threshold)):
+            if dets:
+                _, img, fr = run[k]
+                fr.regions.extend(P.detections_to_regions(dets, xfs[k], img.width, img.height, W, H, labels,
+                                                          model=self.model.name))
 
 
 class ClassifyStage(_InferenceStage):
@@ -709,9 +711,19 @@ class Pipeline:
                     item = q.get(timeout=0.1)
                 except queue.Empty:
                     continue
-                if item is None:            # end of stream
-                    return
-                yield item
+                # then whatever is already queued, without blocking again: one wake-up per burst of
+                # frames rather than per frame (the pipeline threads of all streams share the GIL)
+                burst = [item]
+                while item is not None and len(burst) < 64:
+                    try:
+                        item = q.get_nowait()
+                    except queue.Empty:
+                        break
+                    burst.append(item)
+                for item in burst:
+                    if item is None:        # end of stream
+                        return
+                    yield item
         elif src.get("type") == "frames":
             yield from src.get("frames", [])
         else:
@@ -719,8 +731,6 @@ class Pipeline:
                                                   "build; use an 'application' source of decoded frames")
 
     def _as_image(self, item):
-        from .preproc import Image
-
         if isinstance(item, Image):
             return item
         if isinstance(item, dict):         # host frame {fourcc, width, height, planes}

@@ -105,6 +105,21 @@ def parse_ssd(raw, threshold: float):
     return out
 
 
+def parse_ssd_batch(raw, threshold: float):
+    """``parse_ssd`` over a whole ``[N, K, 7]`` batch at once: per item, the rows before its first
+    ``image_id < 0`` terminator with confidence >= threshold. Items without detections cost no Python
+    loop (a batched detector's output is parsed in one vectorised pass)."""
+    a = np.asarray(raw, dtype=np.float32)
+    a = a.reshape(a.shape[0], -1, 7)
+    live = np.cumsum(a[:, :, 0] < 0, axis=1) == 0          # rows before the terminator
+    keep = live & (a[:, :, 2] >= threshold)
+    out = [[] for _ in range(a.shape[0])]
+    for i in np.flatnonzero(keep.any(axis=1)):
+        for row in a[i][keep[i]]:
+            out[i].append((int(row[0]), int(row[1]), float(row[2]), tuple(float(v) for v in row[3:7])))
+    return out
+
+
 def detections_to_regions(dets, xf, frame_w, frame_h, tensor_w, tensor_h, labels=None, model=None):
     """Parsed detections of one item -> frame ``Region``s."""
     regions = []

@@ -423,3 +423,17 @@ def test_classify_reclassify_interval(ps, evam):
     for fr in results:
         assert len(fr.regions[0].tensors) == 1 and fr.regions[0].tensors[0].label == "light"
         assert fr.regions[2].tensors == [] and fr.regions[3].tensors == [] and fr.regions[4].tensors == []
+
+
+def test_parse_ssd_batch_matches_per_item(evam):
+    """The vectorised batch parse equals parse_ssd item by item (terminator, threshold, empty items)."""
+    P = evam.postproc
+    rng = np.random.default_rng(4)
+    raw = rng.uniform(0, 1, size=(9, 6, 7)).astype(np.float32)
+    raw[:, :, 0] = 0
+    raw[1, 2, 0] = -1          # terminator mid-way
+    raw[3, 0, 0] = -1          # empty item
+    raw[5, :, 2] = 0.1         # all below threshold
+    got = P.parse_ssd_batch(raw, 0.5)
+    assert got == [P.parse_ssd(raw[i], 0.5) for i in range(9)]
+    assert got[3] == [] and got[5] == []
