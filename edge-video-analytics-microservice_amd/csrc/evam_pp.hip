@@ -150,7 +150,8 @@ struct SParams {
     int DW, DH;
     int TH, tiles_x, tiles_per_item;
     int offBuf;          // LDS offset of staging buffer 0 (after the LUT)
-    int buf_bytes;       // one staging buffer: slots x kSlot
+    int buf_bytes;       // one staging buffer: 2 R planes x slot_bytes
+    int slot_bytes;      // one staged row segment: the widest 16-byte-aligned footprint of the launch
     int color_rgb;
     uint32_t fill;
     int ablate;
@@ -751,7 +752,8 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_staged(const SParams P) {
     constexpr int SPW = NSEGX > 4 ? NSEGX / 4 : 1;                   // column segments per wave
     constexpr int RSTEP = NSEGX >= 4 ? 1 : 4 / NSEGX;                // waves sharing a column segment
     constexpr int RPW = R / RSTEP;                                   // rows per wave per group
-    constexpr int SLOT = NSEGX > 4 ? 2 * kSlot : kSlot;              // bytes of one staged row segment
+    constexpr int SLOT_MAX = NSEGX > 4 ? 2 * kSlot : kSlot;          // largest staged row segment
+    const int SLOT = P.slot_bytes;                                   // this launch's segment (<= SLOT_MAX)
     static_assert(R % RSTEP == 0, "R must be a multiple of 4 / NSEGX");
     static_assert(NSEGX <= 4 || R == 1, "full-width (2 KB slot) tiles stage one row per group");
     static_assert(NBUF >= 2 && NBUF <= 3, "2 or 3 staging buffers");
@@ -832,7 +834,7 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_staged(const SParams P) {
     const int dr = wave >> 1, dtap = wave & 1;
     auto issue = [&](int g, uint8_t* buf) -> int {
         if (!cols || (P.ablate & 16)) return 0;
-        if constexpr (2 * R == 4 && SLOT == kSlot) {
+        if constexpr (2 * R == 4 && SLOT_MAX == kSlot) {
             const int Y = Y0 + g * R + dr;
             if (Y >= Y1) return 0;
             const int b0 = lr.B0(Y - Y0), b1 = lr.B1(Y - Y0);
@@ -872,7 +874,7 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_staged(const SParams P) {
                 if (pl > 0 && tap && (ya >> 1) == (yb >> 1)) continue;  // chroma row shared by both taps
                 const int nck = pl == 0 ? nY : nC;
 #pragma unroll
-                for (int c0 = 0; c0 < SLOT / 16; c0 += 64) {  // one wave-wide 1 KB DMA per 64 chunks
+                for (int c0 = 0; c0 < SLOT_MAX / 16; c0 += 64) {  // one wave-wide 1 KB DMA per 64 chunks
                     if (c0 >= nck) break;
                     __attribute__((address_space(3))) void* dstl =
                         (__attribute__((address_space(3))) void*)(buf + s * SLOT + c0 * 16);
@@ -1446,7 +1448,7 @@ struct alignas(64) RoiRec {  // 64 B
 static_assert(sizeof(RoiRec) == 64, "RoiRec layout");
 
 #ifndef EVAM_PP_ROI_K
-#define EVAM_PP_ROI_K 8
+#define EVAM_PP_ROI_K 6
 #endif
 constexpr int kRoiK = EVAM_PP_ROI_K;  // max pixels per lane per row group in the ROI kernel
 
@@ -1869,7 +1871,7 @@ struct Knobs {
     int nsegx = 0;                                 // staged tile width in 64-column segments (0: widest that fits)
     int stage_r = -1, stage_nbuf = -1;             // staged pipeline: rows per group, staging buffers
     int wth = -1, px = 0, reuse = 1, wave_lds = 40 * 1024;
-    int roi_th = -1, roi_buf = 12 * 1024, roi_px = 1, roi_sort = 1, roi_xcd = 0;
+    int roi_th = -1, roi_buf = -1, roi_px = 1, roi_sort = 1, roi_xcd = 0;  // roi_buf -1: sized for one round
     int ablate = 0;                                // stage-removal diagnostics (results invalid)
     void read() {
         staged = env_int("EVAM_PP_STAGED", staged); wave = env_int("EVAM_PP_WAVE", wave);
@@ -1943,7 +1945,7 @@ RowCfg choose_row_tiles(int DW, int DH, const Knobs& k) {
 // Staged-kernel pipeline shapes: (output rows per group R, staging buffers NBUF). One variant per
 // (format, dtype, column segments) is instantiated for each shape listed here.
 struct StagedShape { int R, nbuf; };
-constexpr StagedShape kStagedShapes[] = {{2, 2}, {1, 2}};
+constexpr StagedShape kStagedShapes[] = {{2, 2}, {1, 2}, {2, 3}};
 
 // Valid (column segments, rows per group): four waves split NSEGX x R evenly.
 constexpr bool staged_valid(int nsegx, int R) { return nsegx > 4 ? R == 1 : (nsegx == 4 ? true : R % (4 / nsegx) == 0); }
@@ -1965,7 +1967,7 @@ hipError_t launch_staged_t(const SParams& p, int grid, int lds, hipStream_t s) {
 
 template <int FMT, int OUT, int NSEGX>
 hipError_t launch_staged_s(int R, int nbuf, const SParams& p, int grid, int lds, hipStream_t s) {
-    (void)nbuf;
+    if (R == 2 && nbuf == 3) return launch_staged_t<FMT, OUT, NSEGX, 2, 3>(p, grid, lds, s);
     if (R == 2) return launch_staged_t<FMT, OUT, NSEGX, 2, 2>(p, grid, lds, s);
     if (R == 1) return launch_staged_t<FMT, OUT, NSEGX, 1, 2>(p, grid, lds, s);
     return hipErrorInvalidValue;
@@ -2154,9 +2156,15 @@ bool plan_wave(int f, const Geom& g, int DW, int DH, int count, int out_dtype, i
 // staging buffer size, sized for the widest crop of the group (max_row_bytes = row_bytes_bound of it).
 // Returns false when the group needs the generic kernel (outputs wider than kRoiK x 256 pixels, or a
 // crop so wide that one output row's segments overflow the LDS budget).
-bool plan_roi(int DW, int DH, int out_dtype, int max_row_bytes, const Knobs& kn, QParams& q, int& lds) {
+// The staging buffers are sized so that the whole grid fits on the chip in one round when it can: a ROI
+// batch is about one workgroup per CU slot (C3: 1,600 ROIs), and a second round would pay every
+// workgroup's setup latency (record, geometry, tables) again at the tail. Occupancy is capped by the
+// kernel's registers (kRoiWavesPerSimd), so the buffers take what that occupancy leaves of the LDS,
+// between the widest crop's row and 12 KB (EVAM_PP_ROI_BUF fixes it).
+constexpr int kRoiWavesPerSimd = 7;  // evam_pp_roi<*, *, 1> at kRoiK = 6: <= 72 VGPRs
+bool plan_roi(int DW, int DH, int out_dtype, int max_row_bytes, int count, int n_cu, const Knobs& kn, QParams& q,
+              int& lds) {
     if (DW > kRoiK * kThreads) return false;
-    const int def_buf = kn.roi_buf;
     q.DW = DW; q.DH = DH;
     q.TH = (int64_t)DW * DH <= 32768 ? DH : std::max(8, std::min(DH, 16384 / DW));
     if (kn.roi_th > 0) q.TH = std::max(1, std::min(DH, kn.roi_th));
@@ -2164,7 +2172,13 @@ bool plan_roi(int DW, int DH, int out_dtype, int max_row_bytes, const Knobs& kn,
     q.offXT = out_dtype == EVAM_DTYPE_F32 ? kLutBytes : 0;
     q.offYT = q.offXT + (int)sizeof(XTab) * DW;
     q.offBuf = q.offYT + (int)sizeof(YTab) * q.TH;
-    q.buf_bytes = (std::max(def_buf, max_row_bytes) + 15) & ~15;
+    int buf = kn.roi_buf;
+    if (buf <= 0) {
+        const int64_t grid = (int64_t)count * q.tiles_per_item;
+        const int per_cu = (int)std::max<int64_t>(1, std::min<int64_t>(kRoiWavesPerSimd, (grid + n_cu - 1) / n_cu));
+        buf = std::min(12 * 1024, ((160 * 1024 / per_cu - q.offBuf) / 2) & ~15);
+    }
+    q.buf_bytes = (std::max(buf, max_row_bytes) + 15) & ~15;
     lds = q.offBuf + 2 * q.buf_bytes;
     return q.buf_bytes <= 32 * 1024 && lds <= 160 * 1024;
 }
@@ -2540,7 +2554,7 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
         path[f] = kPathNone;
         if (!count[f]) continue;
         if (uniform[f] && kn.rows) path[f] = kPathUniform;
-        else if (kn.roi && plan_roi(DW, DH, cfg->out_dtype, row_bytes_bound(f, max_cw[f]), kn, qp[f], qlds[f])) path[f] = kPathRoi;
+        else if (kn.roi && plan_roi(DW, DH, cfg->out_dtype, row_bytes_bound(f, max_cw[f]), count[f], h->n_cu, kn, qp[f], qlds[f])) path[f] = kPathRoi;
         else path[f] = kPathGeneric;
         any_generic |= path[f] == kPathGeneric;
         any_roi |= path[f] == kPathRoi;
@@ -2803,7 +2817,13 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
                 sp.tiles_per_item = sp.tiles_x * ((DH + sp.TH - 1) / sp.TH);
                 const int np = f == kI420 ? 3 : (f == kNV12 ? 2 : 1);
                 sp.offBuf = cfg->out_dtype == EVAM_DTYPE_F32 ? kLutBytes : 0;
-                sp.buf_bytes = 2 * R * np * (nsegx > 4 ? 2 * kSlot : kSlot);
+                {   // staged row segment: the widest footprint of any tile and crop origin of this group
+                    const XTab* hx = reinterpret_cast<const XTab*>(h->h_block.data() + tab_off[f]);
+                    int mY = 0, mC = 0;
+                    wave_segments(f, g0.ox, g0.rw, DW, hx, x0_mask[f], tw, mY, mC);
+                    sp.slot_bytes = std::min(nsegx > 4 ? 2 * kSlot : kSlot, 16 * std::max(1, std::max(mY, mC)));
+                }
+                sp.buf_bytes = 2 * R * np * sp.slot_bytes;
                 sp.color_rgb = color_rgb;
                 sp.fill = fill;
                 sp.ablate = kn.ablate;

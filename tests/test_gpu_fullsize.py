@@ -50,7 +50,8 @@ def test_c1_bench_batch(evam, O, coracle, gpu):
 
 
 STAGED_SHAPES = {"default": {}, "r2": {"EVAM_PP_STAGE_R": "2", "EVAM_PP_NSEGX": "4"},
-                 "r1": {"EVAM_PP_STAGE_R": "1", "EVAM_PP_NSEGX": "4"}, "wide": {"EVAM_PP_NSEGX": "8"}}
+                 "r1": {"EVAM_PP_STAGE_R": "1", "EVAM_PP_NSEGX": "4"}, "wide": {"EVAM_PP_NSEGX": "8"},
+                 "b3": {"EVAM_PP_STAGE_NBUF": "3"}}
 
 
 @pytest.mark.parametrize("shape", sorted(STAGED_SHAPES))
@@ -96,7 +97,7 @@ def test_c3_bench_roi_set(evam, O, coracle, gpu, seed):
 
 
 @pytest.mark.parametrize("placement", ["top_left", "center"])
-@pytest.mark.parametrize("shape", ["default", "r2", "wide"])
+@pytest.mark.parametrize("shape", ["default", "r2", "wide", "b3"])
 def test_c4_random_4k_letterbox(evam, O, coracle, gpu, placement, shape, monkeypatch):
     """C4: random (not constant) 3840x2160 NV12 bench frames letterboxed to 640x640 fp32: every 6x gather
     (column taps 6dx+2, weights 1024/1024) on the real 4K pitch is checked, in both placements."""
@@ -118,11 +119,14 @@ def test_c4_random_4k_letterbox(evam, O, coracle, gpu, placement, shape, monkeyp
     pp.close()
 
 
-def test_c5_ring_step(evam, O, coracle, gpu):
+@pytest.mark.parametrize("shape", ["default", "b3"])
+def test_c5_ring_step(evam, O, coracle, gpu, shape, monkeypatch):
     """C5: a 32-stream clip-ring step (1080p NV12 -> aspect(max) 398x224 -> central crop 224x224 fp32 into
     slot t % 16 of a [32, 16, 3, 224, 224] ring), two steps with different frames and slots."""
     import torch
 
+    for k, v in STAGED_SHAPES[shape].items():
+        monkeypatch.setenv(k, v)
     wl = bench.WORKLOADS["c5"]
     info = bench.make_info(evam, wl)
     ring = torch.full((32 * 16, 3, 224, 224), 7, dtype=torch.float32, device=gpu)

@@ -362,7 +362,7 @@ def test_stats_and_timing(evam, O, gpu):
     ((480, 270), (224, 224), "aspect-crop"),        # C5 shape: central crop
 ])
 @pytest.mark.parametrize("variant", ["auto", "wave", "px1", "px2", "noreuse", "staged", "staged_xcd", "staged_r1",
-                                     "staged_wide"])
+                                     "staged_wide", "staged_b3"])
 def test_wave_kernel_variants(evam, O, coracle, gpu, fmt, src, dst, resize, variant, monkeypatch):
     """Uniform-geometry batches through the default kernel choice, the wave-row kernel forced
     (EVAM_PP_WAVE=2; every PX / REUSE choice) and the staged kernel (EVAM_PP_WAVE=0; with the
@@ -374,7 +374,8 @@ def test_wave_kernel_variants(evam, O, coracle, gpu, fmt, src, dst, resize, vari
            "px2": {"EVAM_PP_WAVE": "2", "EVAM_PP_PX": "2"}, "noreuse": {"EVAM_PP_WAVE": "2", "EVAM_PP_REUSE": "0"},
            "staged": {"EVAM_PP_WAVE": "0"}, "staged_xcd": {"EVAM_PP_WAVE": "0", "EVAM_PP_XCD": "1"},
            "staged_r1": {"EVAM_PP_WAVE": "0", "EVAM_PP_STAGE_R": "1"},
-           "staged_wide": {"EVAM_PP_WAVE": "0", "EVAM_PP_NSEGX": "8"}}.get(variant, {})
+           "staged_wide": {"EVAM_PP_WAVE": "0", "EVAM_PP_NSEGX": "8"},
+           "staged_b3": {"EVAM_PP_WAVE": "0", "EVAM_PP_STAGE_NBUF": "3"}}.get(variant, {})
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     if variant == "px2" and dst[0] % 2:
