@@ -38,6 +38,6 @@ echo "[gpu_check] rocprofv3 kernel trace"; date
 export TMPDIR=/tmp
 cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$TAG" -o bench -- \
-  python3 "$ROOT/bench.py" --steps 200 --warmup 50 --no-cpu-baseline > "$OUT/prof_bench_$TAG.json" 2> "$OUT/prof_$TAG.err" || { tail -20 "$OUT/prof_$TAG.err"; exit 1; }
+  python3 "$ROOT/bench.py" --steps 200 --warmup 50 --no-cpu-baseline --resident-steps 0 > "$OUT/prof_bench_$TAG.json" 2> "$OUT/prof_$TAG.err" || { tail -20 "$OUT/prof_$TAG.err"; exit 1; }
 find "$OUT/prof_$TAG" -name "*stats*" | head
 echo "[gpu_check] done"; date

@@ -11,7 +11,7 @@ cd /tmp
 for c in $CFGS; do
   echo "[prof] $c"; date
   timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_${TAG}_$c" -o run -- \
-    python3 "$ROOT/bench.py" --config "$c" --steps ${STEPS:-200} --warmup 50 --no-cpu-baseline \
+    python3 "$ROOT/bench.py" --config "$c" --steps ${STEPS:-200} --warmup 50 --no-cpu-baseline --resident-steps 0 \
     > "$OUT/prof_${TAG}_$c.json" 2> "$OUT/prof_${TAG}_$c.err" || { tail -20 "$OUT/prof_${TAG}_$c.err"; exit 1; }
   python3 - "$OUT/prof_${TAG}_$c" "$OUT/prof_${TAG}_$c.json" "$c" <<'EOF' | tee -a "$OUT/prof_$TAG.txt"
 import csv, glob, json, sys
