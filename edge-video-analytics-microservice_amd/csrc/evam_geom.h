@@ -177,19 +177,6 @@ inline void wave_segments(int f, int ox, int rw, int DW, const XTab* xt, uint32_
     }
 }
 
-// Staged kernel geometry: the widest column segment count (of 4 / 2 / 1 x 64 output columns) whose
-// worst-case source footprint fits a slot-byte LDS row slot. Returns 0 when none does.
-inline int staged_nsegx(int f, double ratio, int stage_rows, int slot) {
-    const int bpp = fmt_bpp(f);
-    for (int n : {4, 2, 1}) {
-        if (stage_rows % (4 / n) != 0) continue;
-        const int tw = 64 * n;
-        const int span = (int)std::ceil((tw - 1) * ratio) + 3;  // source columns touched by one tile row
-        if (span * bpp + 32 <= slot) return n;
-    }
-    return 0;
-}
-
 // Algorithmic bytes of one item: distinct touched source rows x the byte width of
 // the source window feeding the visible output, per plane; plus output bytes.
 inline int64_t item_src_bytes(int f, const Geom& g, int DW, int DH) {

@@ -28,6 +28,8 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <string>
 #include <type_traits>
 #include <vector>
@@ -752,7 +754,7 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_staged(const SParams P) {
     constexpr int SPW = NSEGX > 4 ? NSEGX / 4 : 1;                   // column segments per wave
     constexpr int RSTEP = NSEGX >= 4 ? 1 : 4 / NSEGX;                // waves sharing a column segment
     constexpr int RPW = R / RSTEP;                                   // rows per wave per group
-    constexpr int SLOT_MAX = NSEGX > 4 ? 2 * kSlot : kSlot;          // largest staged row segment
+    constexpr int SLOT_MAX = NSEGX >= 4 ? 2 * kSlot : kSlot;         // largest staged row segment
     const int SLOT = P.slot_bytes;                                   // this launch's segment (<= SLOT_MAX)
     static_assert(R % RSTEP == 0, "R must be a multiple of 4 / NSEGX");
     static_assert(NSEGX <= 4 || R == 1, "full-width (2 KB slot) tiles stage one row per group");
@@ -834,30 +836,41 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_staged(const SParams P) {
     const int dr = wave >> 1, dtap = wave & 1;
     auto issue = [&](int g, uint8_t* buf) -> int {
         if (!cols || (P.ablate & 16)) return 0;
-        if constexpr (2 * R == 4 && SLOT_MAX == kSlot) {
+        if constexpr (2 * R == 4) {
             const int Y = Y0 + g * R + dr;
             if (Y >= Y1) return 0;
             const int b0 = lr.B0(Y - Y0), b1 = lr.B1(Y - Y0);
             if ((b0 | b1) == 0) return 0;  // padding row: nothing to stage
             const int ya = y0 + lr.R0(Y - Y0), yb = y0 + lr.R1(Y - Y0);
             const int yr = dtap ? yb : ya;
-            if (lane < nY)
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                    rsY, (__attribute__((address_space(3))) void*)(buf + wave * SLOT), 16, lane * 16, yr * pitch0 + fsY, 0, 0);
-            if constexpr (NP >= 2) {
-                if (dtap && (ya >> 1) == (yb >> 1)) return 1;  // chroma row shared by both taps
-                if (lane < nC) {
+            int n = 0;
+#pragma unroll
+            for (int c0 = 0; c0 < SLOT_MAX / 16; c0 += 64) {  // one wave-wide 1 KB DMA per 64 chunks
+                if (c0 >= nY) break;
+                if (lane + c0 < nY)
                     __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                        rsC, (__attribute__((address_space(3))) void*)(buf + (2 * R + wave) * SLOT), 16, lane * 16,
-                        (yr >> 1) * pitch1 + fsC, 0, 0);
-                    if constexpr (NP >= 3)
-                        __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                            rsV, (__attribute__((address_space(3))) void*)(buf + (4 * R + wave) * SLOT), 16, lane * 16,
-                            (yr >> 1) * pitch2 + fsC, 0, 0);
-                }
-                return NP;
+                        rsY, (__attribute__((address_space(3))) void*)(buf + wave * SLOT + c0 * 16), 16, (lane + c0) * 16,
+                        yr * pitch0 + fsY, 0, 0);
+                n++;
             }
-            return 1;
+            if constexpr (NP >= 2) {
+                if (dtap && (ya >> 1) == (yb >> 1)) return n;  // chroma row shared by both taps
+#pragma unroll
+                for (int c0 = 0; c0 < SLOT_MAX / 16; c0 += 64) {
+                    if (c0 >= nC) break;
+                    if (lane + c0 < nC) {
+                        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                            rsC, (__attribute__((address_space(3))) void*)(buf + (2 * R + wave) * SLOT + c0 * 16), 16,
+                            (lane + c0) * 16, (yr >> 1) * pitch1 + fsC, 0, 0);
+                        if constexpr (NP >= 3)
+                            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                                rsV, (__attribute__((address_space(3))) void*)(buf + (4 * R + wave) * SLOT + c0 * 16), 16,
+                                (lane + c0) * 16, (yr >> 1) * pitch2 + fsC, 0, 0);
+                    }
+                    n += NP - 1;
+                }
+            }
+            return n;
         } else {
             int n = 0;
 #pragma unroll
@@ -1447,13 +1460,33 @@ struct alignas(64) RoiRec {  // 64 B
 };
 static_assert(sizeof(RoiRec) == 64, "RoiRec layout");
 
+// Compact form used when the call's frames fit the kernel arguments (n_srcs <= kArgItems): the frame
+// (planes, pitches, size) is a FrameArg in the launch's kernel arguments and the record carries only
+// the host-clipped crop, the frame index and the item index. The records are read over PCIe from the
+// pinned slot, one per workgroup at its start: 16 instead of 64 bytes each cuts that read from ~6 us
+// to ~3 us of the C3 launch (1,600 records; EVAM_PP_ABLATE=64 profile).
+struct alignas(16) RoiRecC {  // 16 B
+    uint16_t x0, y0, cw, ch;  // clipped crop (roi_clip of the caller's rect): re-clipping is the identity
+    uint16_t frame, pad;
+    int32_t item;
+};
+static_assert(sizeof(RoiRecC) == 16, "RoiRecC layout");
+struct FrameArg {  // 48 B
+    const uint8_t* plane[3];
+    int32_t pitch[3];
+    int32_t width, height, pad;
+};
+static_assert(sizeof(FrameArg) == 48, "FrameArg layout");
+
 #ifndef EVAM_PP_ROI_K
 #define EVAM_PP_ROI_K 6
 #endif
 constexpr int kRoiK = EVAM_PP_ROI_K;  // max pixels per lane per row group in the ROI kernel
 
 struct QParams {
-    const RoiRec* recs;       // this launch's ROIs in launch order (largest work first)
+    FrameArg frames[kArgItems];  // nframes > 0: the call's frames (records are RoiRecC)
+    int nframes;
+    const void* recs;         // this launch's ROIs in launch order (largest work first): RoiRec / RoiRecC
     const float* lut;         // [3][256]
     void* dst;
     int DW, DH;
@@ -1510,12 +1543,30 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_roi(const QParams P) {
     const int t = blockIdx.x;
     const int li = t / P.tiles_per_item;
     const int ty = t - li * P.tiles_per_item;
-    const __attribute__((address_space(4))) RoiRec* roi = (const __attribute__((address_space(4))) RoiRec*)(P.recs) + li;
-    const int item = roi->item;
-    const __attribute__((address_space(4))) RoiRec* src = roi;
+    int item, fw, fh, rx, ry, rwd, rht, pitch0, pitch1, pitch2;
+    const uint8_t *p0, *p1, *p2;
+    if (P.nframes > 0) {
+        const __attribute__((address_space(4))) RoiRecC* rc = (const __attribute__((address_space(4))) RoiRecC*)(P.recs) + li;
+        const uint32_t xy = *(const __attribute__((address_space(4))) uint32_t*)&rc->x0;
+        const uint32_t wh = *(const __attribute__((address_space(4))) uint32_t*)&rc->cw;
+        const int fi = rc->frame;
+        item = rc->item;
+        rx = xy & 0xFFFF; ry = xy >> 16; rwd = wh & 0xFFFF; rht = wh >> 16;
+        const FrameArg& fa = P.frames[fi];
+        p0 = fa.plane[0]; p1 = fa.plane[1]; p2 = fa.plane[2];
+        pitch0 = fa.pitch[0]; pitch1 = fa.pitch[1]; pitch2 = fa.pitch[2];
+        fw = fa.width; fh = fa.height;
+    } else {
+        const __attribute__((address_space(4))) RoiRec* roi = (const __attribute__((address_space(4))) RoiRec*)(P.recs) + li;
+        item = roi->item;
+        rx = roi->x; ry = roi->y; rwd = roi->w; rht = roi->h;
+        p0 = roi->plane[0]; p1 = roi->plane[1]; p2 = roi->plane[2];
+        pitch0 = roi->pitch[0]; pitch1 = roi->pitch[1]; pitch2 = roi->pitch[2];
+        fw = roi->width; fh = roi->height;
+    }
     Geom g;
-    roi_geometry(FMT, src->width, src->height, true, roi->x, roi->y, roi->w, roi->h, P.mode, P.placement, P.DW,
-                 P.DH, g);  // never empty: the host validated every item
+    roi_geometry(FMT, fw, fh, true, rx, ry, rwd, rht, P.mode, P.placement, P.DW, P.DH,
+                 g);  // never empty: the host validated every item
     const int x0 = __builtin_amdgcn_readfirstlane(g.x0), y0 = __builtin_amdgcn_readfirstlane(g.y0);
     const int cw = __builtin_amdgcn_readfirstlane(g.cw), ch = __builtin_amdgcn_readfirstlane(g.ch);
     const int rw = __builtin_amdgcn_readfirstlane(g.rw), rh = __builtin_amdgcn_readfirstlane(g.rh);
@@ -1523,10 +1574,6 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_roi(const QParams P) {
     // diagnostics: stop after the geometry (64) / after the per-lane setup (32)
     if ((P.ablate & 64) && rw != -7) return;
     const double scx = 1. / ((double)rw / cw), scy = 1. / ((double)rh / ch);
-    const uint8_t* p0 = src->plane[0];
-    const uint8_t* p1 = src->plane[1];
-    const uint8_t* p2 = src->plane[2];
-    const int pitch0 = src->pitch[0], pitch1 = src->pitch[1], pitch2 = src->pitch[2];
     const size_t plane = (size_t)P.DW * P.DH;
     const size_t esz = OUT == 1 ? 4 : 1;
     const int slot = P.slot_offset + item * P.slot_stride;
@@ -1869,21 +1916,23 @@ struct Knobs {
     int staged = 1, wave = 1, rows = 1, roi = 1;   // kernel families allowed (wave 2 = force)
     int th = -1, tw = -1, xcd = -1;                // staged / generic tiles, XCD-contiguous order
     int nsegx = 0;                                 // staged tile width in 64-column segments (0: widest that fits)
+    int wide_slot = 0;                             // 1: 256-column staged tiles may take 2 KB row segments
     int stage_r = -1, stage_nbuf = -1;             // staged pipeline: rows per group, staging buffers
     int wth = -1, px = 0, reuse = 1, wave_lds = 40 * 1024;
     int roi_th = -1, roi_buf = -1, roi_px = 1, roi_sort = 1, roi_xcd = 0;  // roi_buf -1: sized for one round
+    int roi_compact = 1;                           // 16-byte ROI records + frames in the kernel arguments
     int ablate = 0;                                // stage-removal diagnostics (results invalid)
     void read() {
         staged = env_int("EVAM_PP_STAGED", staged); wave = env_int("EVAM_PP_WAVE", wave);
         rows = env_int("EVAM_PP_ROWS", rows); roi = env_int("EVAM_PP_ROI", roi);
         th = env_int("EVAM_PP_TH", th); tw = env_int("EVAM_PP_TW", tw); xcd = env_int("EVAM_PP_XCD", xcd);
-        nsegx = env_int("EVAM_PP_NSEGX", nsegx);
+        nsegx = env_int("EVAM_PP_NSEGX", nsegx); wide_slot = env_int("EVAM_PP_WIDE_SLOT", wide_slot);
         stage_r = env_int("EVAM_PP_STAGE_R", stage_r); stage_nbuf = env_int("EVAM_PP_STAGE_NBUF", stage_nbuf);
         wth = env_int("EVAM_PP_WTH", wth); px = env_int("EVAM_PP_PX", px);
         reuse = env_int("EVAM_PP_REUSE", reuse); wave_lds = env_int("EVAM_PP_WAVE_LDS", wave_lds);
         roi_th = env_int("EVAM_PP_ROI_TH", roi_th); roi_buf = env_int("EVAM_PP_ROI_BUF", roi_buf);
         roi_px = env_int("EVAM_PP_ROI_PX", roi_px); roi_sort = env_int("EVAM_PP_ROI_SORT", roi_sort);
-        roi_xcd = env_int("EVAM_PP_ROI_XCD", roi_xcd);
+        roi_xcd = env_int("EVAM_PP_ROI_XCD", roi_xcd); roi_compact = env_int("EVAM_PP_ROI_COMPACT", roi_compact);
         ablate = env_int("EVAM_PP_ABLATE", ablate);
     }
 };
@@ -2097,6 +2146,45 @@ hipError_t launch_wave(int f, int out, int px, bool reuse, const WParams& p, int
     }
 }
 
+template <int FMT, int OUT>
+const void* wave_fn_t(int px, bool reuse) {
+    switch (px * 2 + (reuse ? 1 : 0)) {
+    case 9: return (const void*)evam_pp_wave<FMT, OUT, 4, true>;
+    case 8: return (const void*)evam_pp_wave<FMT, OUT, 4, false>;
+    case 5: return (const void*)evam_pp_wave<FMT, OUT, 2, true>;
+    case 4: return (const void*)evam_pp_wave<FMT, OUT, 2, false>;
+    case 3: return (const void*)evam_pp_wave<FMT, OUT, 1, true>;
+    default: return (const void*)evam_pp_wave<FMT, OUT, 1, false>;
+    }
+}
+const void* wave_fn(int f, int out, int px, bool reuse) {
+    switch (f * 2 + out) {
+    case kNV12 * 2 + 0: return wave_fn_t<kNV12, 0>(px, reuse);
+    case kNV12 * 2 + 1: return wave_fn_t<kNV12, 1>(px, reuse);
+    case kI420 * 2 + 0: return wave_fn_t<kI420, 0>(px, reuse);
+    case kI420 * 2 + 1: return wave_fn_t<kI420, 1>(px, reuse);
+    case kBGRX * 2 + 0: return wave_fn_t<kBGRX, 0>(px, reuse);
+    case kBGRX * 2 + 1: return wave_fn_t<kBGRX, 1>(px, reuse);
+    case kBGR * 2 + 0: return wave_fn_t<kBGR, 0>(px, reuse);
+    default: return wave_fn_t<kBGR, 1>(px, reuse);
+    }
+}
+
+// Workgroups of `fn` (256 threads, `lds` bytes of dynamic LDS) resident per CU: registers and LDS both
+// count. Cached per (kernel, LDS size): the query runs once per shape, not per call.
+int resident_per_cu(const void* fn, int lds) {
+    static std::mutex mu;
+    static std::map<std::pair<const void*, int>, int> cache;
+    std::lock_guard<std::mutex> lock(mu);
+    auto it = cache.find({fn, lds});
+    if (it != cache.end()) return it->second;
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, kThreads, (size_t)lds) != hipSuccess || n <= 0)
+        n = std::max(1, std::min(8, (160 * 1024) / std::max(lds, 1)));
+    cache[{fn, lds}] = n;
+    return n;
+}
+
 // Wave-row kernel plan for a uniform-geometry group: pixels per lane PX (the widest whose staging
 // fits the LDS budget and divides DW), the exact per-tile footprint from the host tables, REUSE when
 // consecutive output rows share source rows, and a tile height that gives every CU enough workgroups.
@@ -2112,6 +2200,12 @@ bool plan_wave(int f, const Geom& g, int DW, int DH, int count, int out_dtype, i
     const int budget = kn.wave_lds;
     const int want_px = kn.px;
     if (!x0_mask) x0_mask = 1u << (g.x0 & 31);
+    reuse = false;
+    for (int Y = 0; Y + 1 < DH; Y++) {
+        const bool pad0 = (yt[Y].b0 | yt[Y].b1) == 0, pad1 = (yt[Y + 1].b0 | yt[Y + 1].b1) == 0;
+        if (!pad0 && !pad1 && yt[Y + 1].r0 <= yt[Y].r1) { reuse = true; break; }
+    }
+    if (kn.reuse == 0) reuse = false;
     px = 0;
     for (int cand : {4, 2, 1}) {
         if (want_px && cand != want_px) continue;
@@ -2132,17 +2226,16 @@ bool plan_wave(int f, const Geom& g, int DW, int DH, int count, int out_dtype, i
         break;
     }
     if (!px) return false;
-    reuse = false;
-    for (int Y = 0; Y + 1 < DH; Y++) {
-        const bool pad0 = (yt[Y].b0 | yt[Y].b1) == 0, pad1 = (yt[Y + 1].b0 | yt[Y + 1].b1) == 0;
-        if (!pad0 && !pad1 && yt[Y + 1].r0 <= yt[Y].r1) { reuse = true; break; }
-    }
-    if (kn.reuse == 0) reuse = false;
     w.DW = DW; w.DH = DH;
     w.tiles_x = (DW + 64 * px - 1) / (64 * px);
-    const int per_cu = std::max(1, std::min(8, (160 * 1024) / std::max(lds, 1)));
+    // Rows per wave: enough that the whole grid is resident at once (one round: a second round repeats
+    // every workgroup's prologue latency at the tail), counting at most 4 resident workgroups per CU —
+    // longer per-wave row runs amortise the prologue better than more waves hide latency. C1: 16-row
+    // tiles at the 5 workgroups per CU its registers allow ran 1.6 rounds, 31.9 us; 28-row tiles (one
+    // round at 5 per CU) 31.6 us; 32-row tiles (one round at 4 per CU) 29.6 us (profiles/r03_c1_sweep.txt).
+    const int per_cu = std::min(4, resident_per_cu(wave_fn(f, out_dtype, px, reuse), lds));
     const int64_t slots = (int64_t)n_cu * per_cu;
-    int64_t rpw = ((int64_t)count * w.tiles_x * DH) / (4 * slots);
+    int64_t rpw = ((int64_t)count * w.tiles_x * DH + 4 * slots - 1) / (4 * slots);
     rpw = std::max<int64_t>(2, std::min<int64_t>(32, rpw));
     w.TH = std::max(1, std::min(std::min(DH, 4 * 64), kn.wth > 0 ? kn.wth : (int)(4 * rpw)));  // <= 64 rows per wave
     w.tiles_per_item = w.tiles_x * ((DH + w.TH - 1) / w.TH);
@@ -2598,13 +2691,16 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
         tab_off[f] = nbytes;
         nbytes += sizeof(XTab) * (size_t)DW + sizeof(YTab) * (size_t)DH;
     }
-    // ROI groups: [per ROI group: RoiRec x count], in a pinned zero-copy slot (PinRing).
+    // ROI groups: [per ROI group: RoiRec x count], in a pinned zero-copy slot (PinRing); RoiRecC (16 B)
+    // with the frames in the kernel arguments when they fit there (n_srcs <= kArgItems).
+    const bool compact = kn.roi_compact && n_srcs <= kArgItems;
+    const size_t rec_size = compact ? sizeof(RoiRecC) : sizeof(RoiRec);
     size_t rec_off[4] = {0, 0, 0, 0}, dyn_bytes = 0;
     if (any_roi) {
         for (int f = 0; f < 4; f++) {
             if (path[f] != kPathRoi) continue;
             rec_off[f] = dyn_bytes;
-            dyn_bytes += sizeof(RoiRec) * (size_t)count[f];
+            dyn_bytes += rec_size * (size_t)count[f];
         }
     }
     h->h_block.resize(nbytes);
@@ -2686,6 +2782,19 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
                     ord[p] = q[x][head[x]++];
                 }
             }
+            if (compact) {
+                RoiRecC* rc = reinterpret_cast<RoiRecC*>(dyn + rec_off[f]);
+                for (size_t p = 0; p < ord.size(); p++) {
+                    const int i = ord[p];
+                    const Geom& g = geo[i];  // clipped crop (pass 1); every value < 32768
+                    rc[p].x0 = (uint16_t)g.x0; rc[p].y0 = (uint16_t)g.y0;
+                    rc[p].cw = (uint16_t)g.cw; rc[p].ch = (uint16_t)g.ch;
+                    rc[p].frame = (uint16_t)(items ? items[i].src_index : i);
+                    rc[p].pad = 0;
+                    rc[p].item = i;
+                }
+                continue;
+            }
             for (size_t p = 0; p < ord.size(); p++) {
                 const int i = ord[p];
                 RoiRec& r = rr[p];
@@ -2722,8 +2831,19 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
     for (int f = 0; f < 4; f++) {
         if (path[f] == kPathNone) continue;
         if (path[f] == kPathRoi) {
-            QParams q = qp[f];
-            q.recs = reinterpret_cast<const RoiRec*>(d_dyn + rec_off[f]);
+            QParams& q = qp[f];
+            q.recs = d_dyn + rec_off[f];
+            q.nframes = 0;
+            if (compact) {
+                q.nframes = n_srcs;
+                for (int k = 0; k < n_srcs; k++) {
+                    FrameArg& fa = q.frames[k];
+                    for (int pl = 0; pl < 3; pl++) { fa.plane[pl] = srcs[k].planes[pl]; fa.pitch[pl] = srcs[k].pitch[pl]; }
+                    fa.width = srcs[k].width;
+                    fa.height = srcs[k].height;
+                    fa.pad = 0;
+                }
+            }
             q.lut = lut_d;
             q.dst = dst->data;
             q.mode = cfg->resize_mode;
@@ -2776,15 +2896,24 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
                     continue;
                 }
             }
-            const double ratio = (double)g0.cw / g0.rw;
-            int nsegx = kn.staged ? staged_nsegx(f, ratio, 2, kSlot) : 0;
+            // Tile width: the widest of 256 / 128 / 64 columns whose staged row segment (the exact widest
+            // footprint of any tile and crop origin of this group) fits the kernel's slot: 2 KB at 256
+            // columns (two DMA instructions per segment above 1 KB), 1 KB below.
+            const XTab* hx = reinterpret_cast<const XTab*>(h->h_block.data() + tab_off[f]);
+            auto seg_bytes = [&](int tw) {
+                int mY = 0, mC = 0;
+                wave_segments(f, g0.ox, g0.rw, DW, hx, x0_mask[f], tw, mY, mC);
+                return 16 * std::max(1, std::max(mY, mC));
+            };
+            int nsegx = 0;
+            if (kn.staged)
+                for (int n : {4, 2}) {  // (64 columns would need R % 4 == 0: the row kernel serves those)
+                    if (seg_bytes(64 * n) <= (n == 4 && kn.wide_slot ? 2 * kSlot : kSlot)) { nsegx = n; break; }
+                }
             if (nsegx && kn.nsegx > 0 && kn.nsegx < nsegx && 2 % (4 / kn.nsegx) == 0) nsegx = kn.nsegx;
             // Full-width tiles (512 columns, 2 KB row slots, one row per group): whole source rows per DMA
             // and whole output rows per store sweep (EVAM_PP_NSEGX=8).
-            if (nsegx == 4 && kn.nsegx == 8 && DW > 256) {
-                const int span = (int)std::ceil(511 * ratio) + 3;  // source columns of a 512-column tile row
-                if (span * fmt_bpp(f) + 32 <= 2 * kSlot) nsegx = 8;
-            }
+            if (nsegx == 4 && kn.nsegx == 8 && DW > 256 && seg_bytes(512) <= 2 * kSlot) nsegx = 8;
             if (nsegx) {
                 // Pipeline shape: R output rows per group, NBUF staging buffers (NBUF - 1 groups of DMA in
                 // flight).
@@ -2817,12 +2946,7 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
                 sp.tiles_per_item = sp.tiles_x * ((DH + sp.TH - 1) / sp.TH);
                 const int np = f == kI420 ? 3 : (f == kNV12 ? 2 : 1);
                 sp.offBuf = cfg->out_dtype == EVAM_DTYPE_F32 ? kLutBytes : 0;
-                {   // staged row segment: the widest footprint of any tile and crop origin of this group
-                    const XTab* hx = reinterpret_cast<const XTab*>(h->h_block.data() + tab_off[f]);
-                    int mY = 0, mC = 0;
-                    wave_segments(f, g0.ox, g0.rw, DW, hx, x0_mask[f], tw, mY, mC);
-                    sp.slot_bytes = std::min(nsegx > 4 ? 2 * kSlot : kSlot, 16 * std::max(1, std::max(mY, mC)));
-                }
+                sp.slot_bytes = seg_bytes(tw);  // <= the kernel's SLOT_MAX (tile choice above)
                 sp.buf_bytes = 2 * R * np * sp.slot_bytes;
                 sp.color_rgb = color_rgb;
                 sp.fill = fill;

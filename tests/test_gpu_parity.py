@@ -517,3 +517,30 @@ def test_many_items_chunked_launches(evam, O, coracle, gpu):
     for i in range(n):
         assert_same(got[i], ref1[i % 7], f"item {i}")
     pp.close()
+
+
+@pytest.mark.parametrize("fmt", ["NV12", "I420", "BGRX"])
+@pytest.mark.parametrize("n_frames", [64, 70])
+def test_roi_records_compact_and_full(evam, O, coracle, gpu, fmt, n_frames):
+    """ROI batches over <= 64 frames carry 16-byte records with the frames in the kernel arguments; more
+    frames fall back to self-contained 64-byte records. Both forms give the same, oracle-exact result,
+    including ROIs on the last frame slot and partially outside rects."""
+    import torch
+
+    rng = np.random.default_rng(zlib.crc32(f"rec{fmt}{n_frames}".encode()))
+    W, H = 96, 64
+    frames = [O.random_frame(rng, fc(O, fmt), W, H, pattern="gradient" if i % 3 else "uniform")
+              for i in range(n_frames)]
+    rois = []
+    for k in range(90):
+        si = n_frames - 1 if k % 9 == 0 else int(rng.integers(0, n_frames))
+        w, h = int(rng.integers(2, 90)), int(rng.integers(2, 60))
+        x, y = int(rng.integers(-8, W - 2)), int(rng.integers(-8, H - 2))
+        rois.append((si, x, y, max(w, 2 - x), max(h, 2 - y)))
+    info = evam.PreProcInfo(resize="aspect-ratio", placement="center", fill=(5, 6, 7),
+                            range=(0.0, 1.0), mean=(0.1, 0.2, 0.3), std=(0.3, 0.2, 0.1))
+    shape = (len(rois), 3, 32, 48)
+    got, _ = run_hip(evam, torch, upload(evam, frames, gpu), shape, torch.float32, info,
+                     rois=[evam.Roi(*r) for r in rois])
+    ref, _ = run_oracle(O, coracle, frames, shape, "f32", info, rois=rois)
+    assert_same(got, ref, f"roi records {fmt} frames={n_frames}")
