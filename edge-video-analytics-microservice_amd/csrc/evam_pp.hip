@@ -1448,35 +1448,20 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_wave(const WParams P) {
 
 static_assert(sizeof(evam_roi) == 20, "evam_roi layout");
 
-// One ROI in launch order, self-contained: its source frame's planes and size next to the caller's
-// rect and the item index (output slot), so a workgroup needs one 64-byte scalar load (one round
-// trip over PCIe from the pinned descriptor slot) before it can resolve the geometry.
+// One ROI tile in launch order, self-contained: its source frame's planes and size next to the caller's
+// rect, the item index (output slot) and the output rows the tile covers, so a workgroup needs one
+// 64-byte scalar load (one round trip over PCIe from the pinned descriptor slot) before it can resolve
+// the geometry. (A 16-byte record with the frames in the kernel arguments measured slower: the frame
+// lookup is a second dependent load, profiles/r03_c3_records.txt.)
 struct alignas(64) RoiRec {  // 64 B
     const uint8_t* plane[3];
     int32_t pitch[3];
-    int32_t width, height;
-    int32_t x, y, w, h;
+    uint16_t width, height;   // source frame (<= 32768, validated)
+    int32_t x, y, w, h;       // the caller's rect
     int32_t item;
+    uint16_t row0, row1;      // output rows [row0, row1) of this tile (DH <= 65535 for split tiles)
 };
 static_assert(sizeof(RoiRec) == 64, "RoiRec layout");
-
-// Compact form used when the call's frames fit the kernel arguments (n_srcs <= kArgItems): the frame
-// (planes, pitches, size) is a FrameArg in the launch's kernel arguments and the record carries only
-// the host-clipped crop, the frame index and the item index. The records are read over PCIe from the
-// pinned slot, one per workgroup at its start: 16 instead of 64 bytes each cuts that read from ~6 us
-// to ~3 us of the C3 launch (1,600 records; EVAM_PP_ABLATE=64 profile).
-struct alignas(16) RoiRecC {  // 16 B
-    uint16_t x0, y0, cw, ch;  // clipped crop (roi_clip of the caller's rect): re-clipping is the identity
-    uint16_t frame, pad;
-    int32_t item;
-};
-static_assert(sizeof(RoiRecC) == 16, "RoiRecC layout");
-struct FrameArg {  // 48 B
-    const uint8_t* plane[3];
-    int32_t pitch[3];
-    int32_t width, height, pad;
-};
-static_assert(sizeof(FrameArg) == 48, "FrameArg layout");
 
 #ifndef EVAM_PP_ROI_K
 #define EVAM_PP_ROI_K 6
@@ -1484,13 +1469,11 @@ static_assert(sizeof(FrameArg) == 48, "FrameArg layout");
 constexpr int kRoiK = EVAM_PP_ROI_K;  // max pixels per lane per row group in the ROI kernel
 
 struct QParams {
-    FrameArg frames[kArgItems];  // nframes > 0: the call's frames (records are RoiRecC)
-    int nframes;
-    const void* recs;         // this launch's ROIs in launch order (largest work first): RoiRec / RoiRecC
+    const RoiRec* recs;       // this launch's ROI tiles in launch order (largest work first)
     const float* lut;         // [3][256]
     void* dst;
     int DW, DH;
-    int TH, tiles_per_item;   // a tile is all DW columns x TH rows of one item
+    int TH;                   // most output rows of one tile (the LDS row table's size)
     int mode, placement;      // evam_resize_mode, evam_placement
     int slot_offset, slot_stride;
     int offXT, offYT, offBuf; // LDS carve: [LUT][XTab x DW][YTab x TH][buf0][buf1]
@@ -1500,6 +1483,29 @@ struct QParams {
     int ablate;               // diagnostics only (EVAM_PP_ABLATE bits): 2 no pixel math, 4 no stores, 16 no DMA,
                               // 32 stop after setup, 64 stop after geometry, 128 return at entry
 };
+
+// Diagnostic builds only (-DEVAM_PP_TRACE, tools/roi_timeline.py): per-workgroup timestamps of the
+// 100 MHz constant clock at entry / after the record and geometry / after the setup / at the end,
+// written by lane 0 with a vector store. Product builds compile no stamp.
+#ifdef EVAM_PP_TRACE
+constexpr int kTraceWGs = 16384, kTraceSlots = 8;
+__device__ unsigned long long g_evam_trace[kTraceWGs * kTraceSlots];
+#define EVAM_STAMP(k)                                                                                  \
+    do {                                                                                               \
+        unsigned long long t_;                                                                         \
+        __builtin_amdgcn_sched_barrier(0);                                                             \
+        asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");               \
+        __builtin_amdgcn_sched_barrier(0);                                                             \
+        if (threadIdx.x == 0 && blockIdx.x < kTraceWGs) g_evam_trace[blockIdx.x * kTraceSlots + (k)] = t_; \
+    } while (0)
+#define EVAM_TRACE_VAL(k, v)                                                                           \
+    do {                                                                                               \
+        if (threadIdx.x == 0 && blockIdx.x < kTraceWGs) g_evam_trace[blockIdx.x * kTraceSlots + (k)] = (v); \
+    } while (0)
+#else
+#define EVAM_STAMP(k) do { } while (0)
+#define EVAM_TRACE_VAL(k, v) do { } while (0)
+#endif
 
 template <int N>
 __device__ __forceinline__ void wait_vmcnt_stores(int nk) {
@@ -1529,8 +1535,11 @@ __device__ __forceinline__ void wait_vmcnt_stores(int nk) {
 //    are packed back to back in LDS and arrive by LDS-DMA while the previous group is converted;
 //  * the group's R x DW output pixels are packed densely onto the lanes (pixel p = tid + 256 k), so a
 //    72-wide classifier row keeps every lane busy and every store is row-contiguous.
+// 7 resident workgroups per CU need <= 96 SGPRs (800 / (96 + 16)); the occupancy API does not count
+// SGPRs (MI355X_MICROARCH.md, Residency): uncapped, the kernel's ~106 allowed only 6 and a 1,600-ROI
+// batch ran a second round (profiles/r03_c3_roi_timeline_before.json).
 template <int FMT, int OUT, int PX>
-__global__ EVAM_KERNEL_BOUNDS void evam_pp_roi(const QParams P) {
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(96))) void evam_pp_roi(const QParams P) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     using T = FmtTraits<FMT>;
     constexpr bool kYUV = FMT == kNV12 || FMT == kI420;
@@ -1540,30 +1549,23 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_roi(const QParams P) {
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     if (P.ablate & 128) return;  // diagnostics: launch cost only
-    const int t = blockIdx.x;
-    const int li = t / P.tiles_per_item;
-    const int ty = t - li * P.tiles_per_item;
-    int item, fw, fh, rx, ry, rwd, rht, pitch0, pitch1, pitch2;
-    const uint8_t *p0, *p1, *p2;
-    if (P.nframes > 0) {
-        const __attribute__((address_space(4))) RoiRecC* rc = (const __attribute__((address_space(4))) RoiRecC*)(P.recs) + li;
-        const uint32_t xy = *(const __attribute__((address_space(4))) uint32_t*)&rc->x0;
-        const uint32_t wh = *(const __attribute__((address_space(4))) uint32_t*)&rc->cw;
-        const int fi = rc->frame;
-        item = rc->item;
-        rx = xy & 0xFFFF; ry = xy >> 16; rwd = wh & 0xFFFF; rht = wh >> 16;
-        const FrameArg& fa = P.frames[fi];
-        p0 = fa.plane[0]; p1 = fa.plane[1]; p2 = fa.plane[2];
-        pitch0 = fa.pitch[0]; pitch1 = fa.pitch[1]; pitch2 = fa.pitch[2];
-        fw = fa.width; fh = fa.height;
-    } else {
-        const __attribute__((address_space(4))) RoiRec* roi = (const __attribute__((address_space(4))) RoiRec*)(P.recs) + li;
-        item = roi->item;
-        rx = roi->x; ry = roi->y; rwd = roi->w; rht = roi->h;
-        p0 = roi->plane[0]; p1 = roi->plane[1]; p2 = roi->plane[2];
-        pitch0 = roi->pitch[0]; pitch1 = roi->pitch[1]; pitch2 = roi->pitch[2];
-        fw = roi->width; fh = roi->height;
+    EVAM_STAMP(0);
+    // The LUT is loaded once per workgroup, whatever number of units it processes.
+    float* lut_s = reinterpret_cast<float*>(smem);
+    if constexpr (OUT == 1) {
+#pragma unroll
+        for (int k = 0; k < 3; k++) lut_s[tid + k * kThreads] = P.lut[tid + k * kThreads];  // 768 = 3 x kThreads
     }
+    const __attribute__((address_space(4))) RoiRec* roi = (const __attribute__((address_space(4))) RoiRec*)(P.recs) + blockIdx.x;
+    const int item = roi->item;
+    const uint32_t wh = *(const __attribute__((address_space(4))) uint32_t*)&roi->width;
+    const uint32_t rr01 = *(const __attribute__((address_space(4))) uint32_t*)&roi->row0;
+    const int fw = wh & 0xFFFF, fh = wh >> 16;
+    const int rx = roi->x, ry = roi->y, rwd = roi->w, rht = roi->h;
+    const uint8_t* p0 = roi->plane[0];
+    const uint8_t* p1 = roi->plane[1];
+    const uint8_t* p2 = roi->plane[2];
+    const int pitch0 = roi->pitch[0], pitch1 = roi->pitch[1], pitch2 = roi->pitch[2];
     Geom g;
     roi_geometry(FMT, fw, fh, true, rx, ry, rwd, rht, P.mode, P.placement, P.DW, P.DH,
                  g);  // never empty: the host validated every item
@@ -1571,6 +1573,7 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_roi(const QParams P) {
     const int cw = __builtin_amdgcn_readfirstlane(g.cw), ch = __builtin_amdgcn_readfirstlane(g.ch);
     const int rw = __builtin_amdgcn_readfirstlane(g.rw), rh = __builtin_amdgcn_readfirstlane(g.rh);
     const int ox = __builtin_amdgcn_readfirstlane(g.ox), oy = __builtin_amdgcn_readfirstlane(g.oy);
+    EVAM_STAMP(1);
     // diagnostics: stop after the geometry (64) / after the per-lane setup (32)
     if ((P.ablate & 64) && rw != -7) return;
     const double scx = 1. / ((double)rw / cw), scy = 1. / ((double)rh / ch);
@@ -1587,19 +1590,14 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_roi(const QParams P) {
     const __amdgpu_buffer_rsrc_t rsD1 = __builtin_amdgcn_make_buffer_rsrc((void*)d1, (short)0, 0x7FFFFFFF, 0x00020000);
     const __amdgpu_buffer_rsrc_t rsD2 = __builtin_amdgcn_make_buffer_rsrc((void*)d2, (short)0, 0x7FFFFFFF, 0x00020000);
 
-    // Prologue order: the LUT loads go out first; the row table is built while they are in flight;
-    // group 0's DMA (it needs only the row table and the analytic footprint) goes out before the column
-    // table and the per-lane setup are built, so its latency overlaps them.
-    float* lut_s = reinterpret_cast<float*>(smem);
-    float lutv[3] = {0.f, 0.f, 0.f};
-    if constexpr (OUT == 1) {
-#pragma unroll
-        for (int k = 0; k < 3; k++) lutv[k] = P.lut[tid + k * kThreads];  // 768 = 3 x kThreads
-    }
+    // Prologue order: the row table is built first; group 0's DMA (it needs only the row table and the
+    // analytic footprint) goes out before the column table and the per-lane setup are built, so its
+    // latency overlaps them.
     XTab* xt = reinterpret_cast<XTab*>(smem + P.offXT);
     YTab* yt = reinterpret_cast<YTab*>(smem + P.offYT);
     const int DW = P.DW;
-    const int Y0 = ty * P.TH, Y1 = min(Y0 + P.TH, P.DH), rows = Y1 - Y0;
+    const int Y0 = __builtin_amdgcn_readfirstlane(rr01 & 0xFFFF), Y1 = __builtin_amdgcn_readfirstlane(rr01 >> 16);
+    const int rows = Y1 - Y0;
     for (int ly = tid; ly < rows; ly += kThreads) {
         YTab e;
         e.r0 = 0; e.r1 = 0; e.b0 = 0; e.b1 = 0;
@@ -1643,11 +1641,7 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_roi(const QParams P) {
     // q / n for q < 2^16 by one mul_hi: m = ceil(2^32 / n) is exact there (n = 1: the identity).
     const uint32_t mY = nY > 1 ? (uint32_t)((0x100000000ull + nY - 1) / nY) : 0u;
     const uint32_t mC = nC > 1 ? (uint32_t)((0x100000000ull + nC - 1) / nC) : 0u;
-    if constexpr (OUT == 1) {
-#pragma unroll
-        for (int k = 0; k < 3; k++) lut_s[tid + k * kThreads] = lutv[k];
-    }
-    __syncthreads();  // row table visible to the DMA issue
+    __syncthreads();  // row table (and on the first unit the LUT) visible
     // One plane region of group grp: chunk q -> (segment, chunk) -> (row, tap) -> source offset.
     auto issue_plane = [&](int grp, uint8_t* base, int nr, int n, uint32_t m, int pl) {
         const int nq = 2 * nr * n;
@@ -1725,6 +1719,17 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_roi(const QParams P) {
         }
     }
     const int ngroups = (rows + R - 1) / R;
+#ifdef EVAM_PP_TRACE
+    {
+        EVAM_STAMP(2);
+        unsigned xcc, hw;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        EVAM_TRACE_VAL(4, (unsigned long long)cw | ((unsigned long long)ch << 32));
+        EVAM_TRACE_VAL(5, (unsigned long long)ngroups | ((unsigned long long)R << 32));
+        EVAM_TRACE_VAL(6, (unsigned long long)xcc | ((unsigned long long)hw << 32));
+    }
+#endif
     if ((P.ablate & 32) && ngroups != -7) {
         asm volatile("" :: "v"(lY[0][0]), "v"(lC[0][0]), "v"(wa[0][0]), "v"(rr[0]), "s"(mY), "s"(mC));
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // group 0's DMA lands before the LDS is released
@@ -1841,6 +1846,7 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_roi(const QParams P) {
         compute(grp, (grp & 1) ? buf1 : buf0);
         asm volatile("" ::: "memory");
     }
+    EVAM_STAMP(3);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1920,7 +1926,7 @@ struct Knobs {
     int stage_r = -1, stage_nbuf = -1;             // staged pipeline: rows per group, staging buffers
     int wth = -1, px = 0, reuse = 1, wave_lds = 40 * 1024;
     int roi_th = -1, roi_buf = -1, roi_px = 1, roi_sort = 1, roi_xcd = 0;  // roi_buf -1: sized for one round
-    int roi_compact = 1;                           // 16-byte ROI records + frames in the kernel arguments
+    int roi_unit = 0;                              // ROI work-unit size in row groups (0: one unit per base tile)
     int ablate = 0;                                // stage-removal diagnostics (results invalid)
     void read() {
         staged = env_int("EVAM_PP_STAGED", staged); wave = env_int("EVAM_PP_WAVE", wave);
@@ -1932,7 +1938,7 @@ struct Knobs {
         reuse = env_int("EVAM_PP_REUSE", reuse); wave_lds = env_int("EVAM_PP_WAVE_LDS", wave_lds);
         roi_th = env_int("EVAM_PP_ROI_TH", roi_th); roi_buf = env_int("EVAM_PP_ROI_BUF", roi_buf);
         roi_px = env_int("EVAM_PP_ROI_PX", roi_px); roi_sort = env_int("EVAM_PP_ROI_SORT", roi_sort);
-        roi_xcd = env_int("EVAM_PP_ROI_XCD", roi_xcd); roi_compact = env_int("EVAM_PP_ROI_COMPACT", roi_compact);
+        roi_xcd = env_int("EVAM_PP_ROI_XCD", roi_xcd); roi_unit = env_int("EVAM_PP_ROI_UNIT", roi_unit);
         ablate = env_int("EVAM_PP_ABLATE", ablate);
     }
 };
@@ -2245,35 +2251,62 @@ bool plan_wave(int f, const Geom& g, int DW, int DH, int count, int out_dtype, i
     return true;
 }
 
+template <int FMT, int OUT>
+const void* roi_fn_t(int px) {
+    return px == 4 ? (const void*)evam_pp_roi<FMT, OUT, 4> : (const void*)evam_pp_roi<FMT, OUT, 1>;
+}
+const void* roi_fn(int f, int out, int px) {
+    switch (f * 2 + out) {
+    case kNV12 * 2 + 0: return roi_fn_t<kNV12, 0>(px);
+    case kNV12 * 2 + 1: return roi_fn_t<kNV12, 1>(px);
+    case kI420 * 2 + 0: return roi_fn_t<kI420, 0>(px);
+    case kI420 * 2 + 1: return roi_fn_t<kI420, 1>(px);
+    case kBGRX * 2 + 0: return roi_fn_t<kBGRX, 0>(px);
+    case kBGRX * 2 + 1: return roi_fn_t<kBGRX, 1>(px);
+    case kBGR * 2 + 0: return roi_fn_t<kBGR, 0>(px);
+    default: return roi_fn_t<kBGR, 1>(px);
+    }
+}
+
 // ROI-kernel plan for one format group with per-item geometry: the tile height, the LDS carve and the
 // staging buffer size, sized for the widest crop of the group (max_row_bytes = row_bytes_bound of it).
-// Returns false when the group needs the generic kernel (outputs wider than kRoiK x 256 pixels, or a
-// crop so wide that one output row's segments overflow the LDS budget).
+// Returns false when the group needs the generic kernel (outputs wider than kRoiK x 256 pixels, taller
+// than 65535 rows, or a crop so wide that one output row's segments overflow the LDS budget).
 // The staging buffers are sized so that the whole grid fits on the chip in one round when it can: a ROI
-// batch is about one workgroup per CU slot (C3: 1,600 ROIs), and a second round would pay every
-// workgroup's setup latency (record, geometry, tables) again at the tail. Occupancy is capped by the
-// kernel's registers (kRoiWavesPerSimd), so the buffers take what that occupancy leaves of the LDS,
-// between the widest crop's row and 12 KB (EVAM_PP_ROI_BUF fixes it).
+// batch is about one workgroup per CU slot (C3: 1,600 ROIs), and a second round starts its workgroups
+// only when first-round ones finish, paying record, geometry and setup latency again at the tail
+// (C3 with 6 instead of 7 resident per CU: the 64 smallest ROIs started at ~32 us and ended the launch,
+// profiles/r03_c3_roi_timeline_before.json). Occupancy is capped by the kernel's registers
+// (kRoiWavesPerSimd); the buffers take what that occupancy leaves of the LDS (allocated in 1 KB
+// granules, checked against the runtime's occupancy calculator), between the widest crop's row and
+// 12 KB (EVAM_PP_ROI_BUF fixes it). `slots`: workgroups resident at once with that carve.
 constexpr int kRoiWavesPerSimd = 7;  // evam_pp_roi<*, *, 1> at kRoiK = 6: <= 72 VGPRs
-bool plan_roi(int DW, int DH, int out_dtype, int max_row_bytes, int count, int n_cu, const Knobs& kn, QParams& q,
-              int& lds) {
-    if (DW > kRoiK * kThreads) return false;
+bool plan_roi(int f, int DW, int DH, int out_dtype, int px, int max_row_bytes, int count, int n_cu, const Knobs& kn,
+              QParams& q, int& base_tiles, int& lds, int64_t& slots) {
+    if (DW > kRoiK * kThreads || DH > 65535) return false;
     q.DW = DW; q.DH = DH;
     q.TH = (int64_t)DW * DH <= 32768 ? DH : std::max(8, std::min(DH, 16384 / DW));
     if (kn.roi_th > 0) q.TH = std::max(1, std::min(DH, kn.roi_th));
-    q.tiles_per_item = (DH + q.TH - 1) / q.TH;
+    base_tiles = (DH + q.TH - 1) / q.TH;
     q.offXT = out_dtype == EVAM_DTYPE_F32 ? kLutBytes : 0;
     q.offYT = q.offXT + (int)sizeof(XTab) * DW;
     q.offBuf = q.offYT + (int)sizeof(YTab) * q.TH;
+    const int64_t grid = (int64_t)count * base_tiles;
+    const int per_cu = (int)std::max<int64_t>(1, std::min<int64_t>(kRoiWavesPerSimd, (grid + n_cu - 1) / n_cu));
     int buf = kn.roi_buf;
-    if (buf <= 0) {
-        const int64_t grid = (int64_t)count * q.tiles_per_item;
-        const int per_cu = (int)std::max<int64_t>(1, std::min<int64_t>(kRoiWavesPerSimd, (grid + n_cu - 1) / n_cu));
-        buf = std::min(12 * 1024, ((160 * 1024 / per_cu - q.offBuf) / 2) & ~15);
-    }
+    if (buf <= 0) buf = std::min(12 * 1024, ((((160 * 1024) / per_cu) & ~1023) - q.offBuf) / 2 & ~15);
     q.buf_bytes = (std::max(buf, max_row_bytes) + 15) & ~15;
     lds = q.offBuf + 2 * q.buf_bytes;
-    return q.buf_bytes <= 32 * 1024 && lds <= 160 * 1024;
+    if (q.buf_bytes > 32 * 1024 || lds > 160 * 1024) return false;
+    const void* fn = roi_fn(f, out_dtype, px == 4 && DW % 4 == 0 ? 4 : 1);
+    int res = resident_per_cu(fn, lds);
+    while (kn.roi_buf <= 0 && res < per_cu && q.buf_bytes - 512 >= max_row_bytes) {
+        q.buf_bytes -= 512;
+        lds -= 1024;
+        res = resident_per_cu(fn, lds);
+    }
+    slots = (int64_t)n_cu * res;
+    return true;
 }
 
 // Descriptor upload ring. The per-call descriptor block ([LUT][ItemDesc x n][tables]) changes with
@@ -2333,6 +2366,7 @@ struct evam_pp {
     std::vector<int> sc_order;
     std::vector<int> sc_members;   // item indices grouped by source format
     std::vector<Geom> sc_geo;
+    std::vector<int> sc_units;     // ROI work units: (item, row0, row1, cost)
 };
 
 namespace {
@@ -2444,6 +2478,26 @@ int ring_upload(evam_pp* h, const uint8_t** out) {
 extern "C" {
 
 int evam_pp_abi_version(void) { return EVAM_PP_ABI_VERSION; }
+
+#ifdef EVAM_PP_TRACE
+// Diagnostic builds: copy the first n_wg workgroups' trace records (kTraceSlots x u64 each) of the last
+// traced launch.
+// host == NULL: clear the trace buffer (before the launch to trace).
+int evam_pp_debug_trace(unsigned long long* host, int n_wg) {
+    if (!host) {
+        void* a = nullptr;
+        HIP_TRY(hipDeviceSynchronize());
+        HIP_TRY(hipGetSymbolAddress(&a, HIP_SYMBOL(g_evam_trace)));
+        HIP_TRY(hipMemset(a, 0, sizeof(g_evam_trace)));
+        return EVAM_PP_OK;
+    }
+    if (n_wg <= 0 || n_wg > kTraceWGs) return EVAM_PP_ERR_INVALID_ARG;
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpyFromSymbol(host, HIP_SYMBOL(g_evam_trace),
+                                sizeof(unsigned long long) * kTraceSlots * (size_t)n_wg));
+    return EVAM_PP_OK;
+}
+#endif
 
 const char* evam_pp_last_error(void) { return g_last_error.c_str(); }
 
@@ -2641,13 +2695,15 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
     enum { kPathNone, kPathUniform, kPathRoi, kPathGeneric };
     int path[4];
     QParams qp[4];
-    int qlds[4] = {0, 0, 0, 0};
+    int qlds[4] = {0, 0, 0, 0}, qbase[4] = {1, 1, 1, 1}, qrec[4] = {0, 0, 0, 0};
+    int64_t qslots[4] = {0, 0, 0, 0};
     bool any_generic = false, any_roi = false;
     for (int f = 0; f < 4; f++) {
         path[f] = kPathNone;
         if (!count[f]) continue;
         if (uniform[f] && kn.rows) path[f] = kPathUniform;
-        else if (kn.roi && plan_roi(DW, DH, cfg->out_dtype, row_bytes_bound(f, max_cw[f]), count[f], h->n_cu, kn, qp[f], qlds[f])) path[f] = kPathRoi;
+        else if (kn.roi && plan_roi(f, DW, DH, cfg->out_dtype, kn.roi_px, row_bytes_bound(f, max_cw[f]), count[f], h->n_cu,
+                                    kn, qp[f], qbase[f], qlds[f], qslots[f])) path[f] = kPathRoi;
         else path[f] = kPathGeneric;
         any_generic |= path[f] == kPathGeneric;
         any_roi |= path[f] == kPathRoi;
@@ -2691,16 +2747,17 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
         tab_off[f] = nbytes;
         nbytes += sizeof(XTab) * (size_t)DW + sizeof(YTab) * (size_t)DH;
     }
-    // ROI groups: [per ROI group: RoiRec x count], in a pinned zero-copy slot (PinRing); RoiRecC (16 B)
-    // with the frames in the kernel arguments when they fit there (n_srcs <= kArgItems).
-    const bool compact = kn.roi_compact && n_srcs <= kArgItems;
-    const size_t rec_size = compact ? sizeof(RoiRecC) : sizeof(RoiRec);
+    // ROI groups: [per ROI group: RoiRec x tiles], in a pinned zero-copy slot (PinRing). A group has
+    // count x base tiles, plus up to one extra tile per ROI when its longest crops are split in two.
     size_t rec_off[4] = {0, 0, 0, 0}, dyn_bytes = 0;
     if (any_roi) {
         for (int f = 0; f < 4; f++) {
             if (path[f] != kPathRoi) continue;
             rec_off[f] = dyn_bytes;
-            dyn_bytes += rec_size * (size_t)count[f];
+            // at most ceil(groups / roi_unit) <= DH units per ROI when base tiles are split
+            const int64_t per = qbase[f] == 1 && kn.roi_unit > 0
+                                    ? std::min<int64_t>(DH, (DH + kn.roi_unit - 1) / kn.roi_unit) : qbase[f];
+            dyn_bytes += sizeof(RoiRec) * (size_t)count[f] * (size_t)per;
         }
     }
     h->h_block.resize(nbytes);
@@ -2782,30 +2839,53 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
                     ord[p] = q[x][head[x]++];
                 }
             }
-            if (compact) {
-                RoiRecC* rc = reinterpret_cast<RoiRecC*>(dyn + rec_off[f]);
-                for (size_t p = 0; p < ord.size(); p++) {
-                    const int i = ord[p];
-                    const Geom& g = geo[i];  // clipped crop (pass 1); every value < 32768
-                    rc[p].x0 = (uint16_t)g.x0; rc[p].y0 = (uint16_t)g.y0;
-                    rc[p].cw = (uint16_t)g.cw; rc[p].ch = (uint16_t)g.ch;
-                    rc[p].frame = (uint16_t)(items ? items[i].src_index : i);
-                    rc[p].pad = 0;
-                    rc[p].item = i;
-                }
-                continue;
-            }
+            // Work units (one workgroup each): row tiles of each ROI of about kn.roi_unit row groups (a
+            // group is one DMA round trip: the per-workgroup critical path), so the widest crops no
+            // longer bound the launch. Units launch largest first; beyond the resident workgroups the
+            // dispatcher starts each remaining unit as a slot frees up.
+            const QParams& q = qp[f];
+            const int base = qbase[f];
+            const int pxr = kn.roi_px == 4 && DW % 4 == 0 ? 4 : 1;
+            const int rcap = std::max(1, ((kRoiK / pxr) * kThreads) / (DW / pxr));
+            const int gt = kn.roi_unit;
+            std::vector<int>& un = h->sc_units;  // (item, row0, row1, cost) per unit
+            un.clear();
+            int maxcost = 1;
             for (size_t p = 0; p < ord.size(); p++) {
                 const int i = ord[p];
-                RoiRec& r = rr[p];
+                const int R = std::max(1, std::min(std::min(q.buf_bytes / row_bytes_bound(f, geo[i].cw), rcap), DH));
+                int nt = base;
+                if (base == 1 && gt > 0) nt = std::max(1, std::min(DH, ((DH + R - 1) / R + gt - 1) / gt));
+                for (int t = 0; t < nt; t++) {
+                    const int y0 = base > 1 ? t * q.TH : (int)((int64_t)DH * t / nt);
+                    const int y1 = base > 1 ? std::min(DH, (t + 1) * q.TH) : (int)((int64_t)DH * (t + 1) / nt);
+                    const int cost = (y1 - y0 + R - 1) / R;
+                    maxcost = std::max(maxcost, cost);
+                    un.insert(un.end(), {i, y0, y1, cost});
+                }
+            }
+            // stable counting sort of the units by cost, largest first
+            const int nu = (int)(un.size() / 4);
+            std::vector<int> start(maxcost + 2, 0);
+            for (int u = 0; u < nu; u++) start[maxcost - un[4 * u + 3] + 1]++;
+            for (int c = 0; c <= maxcost; c++) start[c + 1] += start[c];
+            std::vector<int> slot(nu);
+            for (int u = 0; u < nu; u++) slot[u] = start[maxcost - un[4 * u + 3]]++;
+            for (int u = 0; u < nu; u++) {
+                const int i = un[4 * u];
                 const evam_image& sim = srcs[items ? items[i].src_index : i];
+                RoiRec& r = rr[slot[u]];
                 r.plane[0] = sim.planes[0]; r.plane[1] = sim.planes[1]; r.plane[2] = sim.planes[2];
                 r.pitch[0] = sim.pitch[0]; r.pitch[1] = sim.pitch[1]; r.pitch[2] = sim.pitch[2];
-                r.width = sim.width; r.height = sim.height;
+                r.width = (uint16_t)sim.width; r.height = (uint16_t)sim.height;
                 if (items) { r.x = items[i].x; r.y = items[i].y; r.w = items[i].w; r.h = items[i].h; }
                 else { r.x = r.y = r.w = r.h = 0; }  // w <= 0: the full frame
                 r.item = i;
+                r.row0 = (uint16_t)un[4 * u + 1];
+                r.row1 = (uint16_t)un[4 * u + 2];
             }
+            const int nrec = nu;
+            qrec[f] = nrec;
         }
     }
     const uint8_t* d_block = nullptr;
@@ -2832,18 +2912,7 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
         if (path[f] == kPathNone) continue;
         if (path[f] == kPathRoi) {
             QParams& q = qp[f];
-            q.recs = d_dyn + rec_off[f];
-            q.nframes = 0;
-            if (compact) {
-                q.nframes = n_srcs;
-                for (int k = 0; k < n_srcs; k++) {
-                    FrameArg& fa = q.frames[k];
-                    for (int pl = 0; pl < 3; pl++) { fa.plane[pl] = srcs[k].planes[pl]; fa.pitch[pl] = srcs[k].pitch[pl]; }
-                    fa.width = srcs[k].width;
-                    fa.height = srcs[k].height;
-                    fa.pad = 0;
-                }
-            }
+            q.recs = reinterpret_cast<const RoiRec*>(d_dyn + rec_off[f]);
             q.lut = lut_d;
             q.dst = dst->data;
             q.mode = cfg->resize_mode;
@@ -2853,7 +2922,7 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
             q.color_rgb = color_rgb;
             q.fill = fill;
             q.ablate = kn.ablate;
-            const int64_t grid = (int64_t)count[f] * q.tiles_per_item;
+            const int64_t grid = qrec[f];
             if (grid > 0x7FFFFFFF) return fail(EVAM_PP_ERR_INVALID_ARG, "evam_pp_run: too many tiles");
             hipError_t e = launch_roi(f, cfg->out_dtype, kn.roi_px, q, (int)grid, qlds[f], h->stream);
             if (e != hipSuccess) return fail(EVAM_PP_ERR_HIP, "kernel launch failed: %s", hipGetErrorString(e));

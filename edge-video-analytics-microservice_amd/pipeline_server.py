@@ -488,7 +488,7 @@ class DetectStage(_InferenceStage):
         """One launch over the frames of every request (hub thread)."""
         run = [it for r in reqs for it in r.items]
         out = self._tensor(len(run))
-        xfs = pp.convert([img for _, img, _ in run], out, self.info, want_transform=True)
+        xfs = pp.convert([img for _, img, _ in run], out, self.info, want_transform="lazy")
         raw = self.model.fn(out)
         raw = raw.detach().float().cpu().numpy() if hasattr(raw, "detach") else raw
         W, H = self.model.input_size

@@ -521,10 +521,9 @@ def test_many_items_chunked_launches(evam, O, coracle, gpu):
 
 @pytest.mark.parametrize("fmt", ["NV12", "I420", "BGRX"])
 @pytest.mark.parametrize("n_frames", [64, 70])
-def test_roi_records_compact_and_full(evam, O, coracle, gpu, fmt, n_frames):
-    """ROI batches over <= 64 frames carry 16-byte records with the frames in the kernel arguments; more
-    frames fall back to self-contained 64-byte records. Both forms give the same, oracle-exact result,
-    including ROIs on the last frame slot and partially outside rects."""
+def test_roi_batches_many_frames(evam, O, coracle, gpu, fmt, n_frames):
+    """ROI batches over many frames (self-contained records per ROI tile, the widest crops split into two
+    row tiles): oracle-exact, including ROIs on the last frame and partially outside rects."""
     import torch
 
     rng = np.random.default_rng(zlib.crc32(f"rec{fmt}{n_frames}".encode()))
