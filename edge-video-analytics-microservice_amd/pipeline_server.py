@@ -348,6 +348,7 @@ class BatchHub:
         self.max_wait_s = float(max_wait_s)
         self.target = int(target) if target else None
         self._pending: dict = {}
+        self._units: dict = {}          # pending units per key
         self._cv = threading.Condition()
         self._stop = False
         self._pp = None
@@ -367,11 +368,18 @@ class BatchHub:
         if units <= 0:
             return
         req = _Request(stage, items, units)
+        key = stage.hub_key()
         with self._cv:
             if self._stop:
                 raise RuntimeError("batch hub is closed")
-            self._pending.setdefault(stage.hub_key(), []).append(req)
-            self._cv.notify_all()
+            q = self._pending.setdefault(key, [])
+            q.append(req)
+            n = self._units.get(key, 0) + units
+            self._units[key] = n
+            # wake the hub only when it has something new to decide: a first request (its deadline
+            # starts) or a full batch; other submits would wake it just to go back to sleep
+            if len(q) == 1 or n >= (self.target or self.max_batch):
+                self._cv.notify()
         req.done.wait()
         if req.error is not None:
             raise req.error
@@ -380,14 +388,16 @@ class BatchHub:
         """(key, requests) to run now, or (None, wait seconds)."""
         wait = None
         for key, reqs in self._pending.items():
-            units = sum(r.units for r in reqs)
+            units = self._units[key]
             if units >= (self.target or self.max_batch) or now - reqs[0].t0 >= self.max_wait_s:
                 take, n = [], 0
                 while reqs and (not take or n + reqs[0].units <= self.max_batch):
                     n += reqs[0].units
                     take.append(reqs.pop(0))
+                self._units[key] = units - n
                 if not reqs:
                     del self._pending[key]
+                    del self._units[key]
                 return key, take
             left = self.max_wait_s - (now - reqs[0].t0)
             wait = left if wait is None else min(wait, left)

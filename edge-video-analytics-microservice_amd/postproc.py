@@ -51,7 +51,7 @@ class Region:
     tensors: list = field(default_factory=list)
 
 
-@dataclass
+@dataclass(slots=True)
 class FrameResult:
     width: int
     height: int
