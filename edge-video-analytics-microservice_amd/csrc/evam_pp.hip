@@ -1452,7 +1452,7 @@ static_assert(sizeof(evam_roi) == 20, "evam_roi layout");
 // rect, the item index (output slot) and the output rows the tile covers, so a workgroup needs one
 // 64-byte scalar load (one round trip over PCIe from the pinned descriptor slot) before it can resolve
 // the geometry. (A 16-byte record with the frames in the kernel arguments measured slower: the frame
-// lookup is a second dependent load, profiles/r03_c3_records.txt.)
+// lookup is a second dependent load, profiles/r02r_c3_records.txt.)
 struct alignas(64) RoiRec {  // 64 B
     const uint8_t* plane[3];
     int32_t pitch[3];
@@ -1537,7 +1537,7 @@ __device__ __forceinline__ void wait_vmcnt_stores(int nk) {
 //    72-wide classifier row keeps every lane busy and every store is row-contiguous.
 // 7 resident workgroups per CU need <= 96 SGPRs (800 / (96 + 16)); the occupancy API does not count
 // SGPRs (MI355X_MICROARCH.md, Residency): uncapped, the kernel's ~106 allowed only 6 and a 1,600-ROI
-// batch ran a second round (profiles/r03_c3_roi_timeline_before.json).
+// batch ran a second round (profiles/r02r_c3_roi_timeline_before.json).
 template <int FMT, int OUT, int PX>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(96))) void evam_pp_roi(const QParams P) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -2238,7 +2238,7 @@ bool plan_wave(int f, const Geom& g, int DW, int DH, int count, int out_dtype, i
     // every workgroup's prologue latency at the tail), counting at most 4 resident workgroups per CU —
     // longer per-wave row runs amortise the prologue better than more waves hide latency. C1: 16-row
     // tiles at the 5 workgroups per CU its registers allow ran 1.6 rounds, 31.9 us; 28-row tiles (one
-    // round at 5 per CU) 31.6 us; 32-row tiles (one round at 4 per CU) 29.6 us (profiles/r03_c1_sweep.txt).
+    // round at 5 per CU) 31.6 us; 32-row tiles (one round at 4 per CU) 29.6 us (profiles/r02r_c1_sweep.txt).
     const int per_cu = std::min(4, resident_per_cu(wave_fn(f, out_dtype, px, reuse), lds));
     const int64_t slots = (int64_t)n_cu * per_cu;
     int64_t rpw = ((int64_t)count * w.tiles_x * DH + 4 * slots - 1) / (4 * slots);
@@ -2276,7 +2276,7 @@ const void* roi_fn(int f, int out, int px) {
 // batch is about one workgroup per CU slot (C3: 1,600 ROIs), and a second round starts its workgroups
 // only when first-round ones finish, paying record, geometry and setup latency again at the tail
 // (C3 with 6 instead of 7 resident per CU: the 64 smallest ROIs started at ~32 us and ended the launch,
-// profiles/r03_c3_roi_timeline_before.json). Occupancy is capped by the kernel's registers
+// profiles/r02r_c3_roi_timeline_before.json). Occupancy is capped by the kernel's registers
 // (kRoiWavesPerSimd); the buffers take what that occupancy leaves of the LDS (allocated in 1 KB
 // granules, checked against the runtime's occupancy calculator), between the widest crop's row and
 // 12 KB (EVAM_PP_ROI_BUF fixes it). `slots`: workgroups resident at once with that carve.
