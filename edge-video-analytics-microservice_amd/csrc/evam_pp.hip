@@ -58,6 +58,16 @@ constexpr int kThreads = 256;
 #define EVAM_KERNEL_BOUNDS __launch_bounds__(kThreads)
 #endif
 constexpr int kLutBytes = 3 * 256 * 4;
+// Cache-policy bits of the output stores: 2 = nt (non-temporal). The outputs are written once and
+// read by nobody in the launch; streaming them past the caches measured 1.5-3 % faster on C2/C3/C4
+// and 10 % on C5 (profiles/r02r_store_policy.txt). EVAM_PP_LOAD_AUX: the same bits for the LDS-DMA
+// source reads (A/B builds).
+#ifndef EVAM_PP_STORE_AUX
+#define EVAM_PP_STORE_AUX 2
+#endif
+#ifndef EVAM_PP_LOAD_AUX
+#define EVAM_PP_LOAD_AUX 0
+#endif
 
 // OpenCV color_yuv.simd.hpp ITUR_BT_601_*; the -128 chroma bias is folded into the constants.
 constexpr int kCY = 1220542, kCUB = 2116026, kCUG = -409993, kCVG = -852492, kCVR = 1673527;
@@ -682,13 +692,13 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_rows(const RParams P) {
                         if (P.color_rgb) { const int tmp = v[0]; v[0] = v[2]; v[2] = tmp; }
                         const uint32_t vo = xo[j] * (uint32_t)esz;
                         if constexpr (OUT == 1) {
-                            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lut_s[v[0]]), rsD0, vo, sO, 0);
-                            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lut_s[256 + v[1]]), rsD1, vo, sO, 0);
-                            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lut_s[512 + v[2]]), rsD2, vo, sO, 0);
+                            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lut_s[v[0]]), rsD0, vo, sO, EVAM_PP_STORE_AUX);
+                            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lut_s[256 + v[1]]), rsD1, vo, sO, EVAM_PP_STORE_AUX);
+                            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lut_s[512 + v[2]]), rsD2, vo, sO, EVAM_PP_STORE_AUX);
                         } else {
-                            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v[0], rsD0, vo, sO, 0);
-                            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v[1], rsD1, vo, sO, 0);
-                            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v[2], rsD2, vo, sO, 0);
+                            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v[0], rsD0, vo, sO, EVAM_PP_STORE_AUX);
+                            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v[1], rsD1, vo, sO, EVAM_PP_STORE_AUX);
+                            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v[2], rsD2, vo, sO, EVAM_PP_STORE_AUX);
                         }
                     }
                 }
@@ -850,7 +860,7 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_staged(const SParams P) {
                 if (lane + c0 < nY)
                     __builtin_amdgcn_raw_ptr_buffer_load_lds(
                         rsY, (__attribute__((address_space(3))) void*)(buf + wave * SLOT + c0 * 16), 16, (lane + c0) * 16,
-                        yr * pitch0 + fsY, 0, 0);
+                        yr * pitch0 + fsY, EVAM_PP_LOAD_AUX, 0);
                 n++;
             }
             if constexpr (NP >= 2) {
@@ -861,11 +871,11 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_staged(const SParams P) {
                     if (lane + c0 < nC) {
                         __builtin_amdgcn_raw_ptr_buffer_load_lds(
                             rsC, (__attribute__((address_space(3))) void*)(buf + (2 * R + wave) * SLOT + c0 * 16), 16,
-                            (lane + c0) * 16, (yr >> 1) * pitch1 + fsC, 0, 0);
+                            (lane + c0) * 16, (yr >> 1) * pitch1 + fsC, EVAM_PP_LOAD_AUX, 0);
                         if constexpr (NP >= 3)
                             __builtin_amdgcn_raw_ptr_buffer_load_lds(
                                 rsV, (__attribute__((address_space(3))) void*)(buf + (4 * R + wave) * SLOT + c0 * 16), 16,
-                                (lane + c0) * 16, (yr >> 1) * pitch2 + fsC, 0, 0);
+                                (lane + c0) * 16, (yr >> 1) * pitch2 + fsC, EVAM_PP_LOAD_AUX, 0);
                     }
                     n += NP - 1;
                 }
@@ -894,11 +904,11 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_staged(const SParams P) {
                     if (lane + c0 < nck) {
                         const int co = (lane + c0) * 16;
                         if (pl == 0)
-                            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsY, dstl, 16, co, yr * pitch0 + fsY, 0, 0);
+                            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsY, dstl, 16, co, yr * pitch0 + fsY, EVAM_PP_LOAD_AUX, 0);
                         else if (pl == 1)
-                            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsC, dstl, 16, co, (yr >> 1) * pitch1 + fsC, 0, 0);
+                            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsC, dstl, 16, co, (yr >> 1) * pitch1 + fsC, EVAM_PP_LOAD_AUX, 0);
                         else
-                            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsV, dstl, 16, co, (yr >> 1) * pitch2 + fsC, 0, 0);
+                            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsV, dstl, 16, co, (yr >> 1) * pitch2 + fsC, EVAM_PP_LOAD_AUX, 0);
                     }
                     n++;
                 }
@@ -933,13 +943,13 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_staged(const SParams P) {
                 if (!xin[j]) return;  // lane 0 is in: the wave still issues all three stores
                 if constexpr (OUT == 1) {
                     const uint8_t* lb = reinterpret_cast<const uint8_t*>(lut_s);
-                    __builtin_amdgcn_raw_buffer_store_b32(*reinterpret_cast<const uint32_t*>(lb + v[0]), rsD0, xo[j], sO, 0);
-                    __builtin_amdgcn_raw_buffer_store_b32(*reinterpret_cast<const uint32_t*>(lb + 1024 + v[1]), rsD1, xo[j], sO, 0);
-                    __builtin_amdgcn_raw_buffer_store_b32(*reinterpret_cast<const uint32_t*>(lb + 2048 + v[2]), rsD2, xo[j], sO, 0);
+                    __builtin_amdgcn_raw_buffer_store_b32(*reinterpret_cast<const uint32_t*>(lb + v[0]), rsD0, xo[j], sO, EVAM_PP_STORE_AUX);
+                    __builtin_amdgcn_raw_buffer_store_b32(*reinterpret_cast<const uint32_t*>(lb + 1024 + v[1]), rsD1, xo[j], sO, EVAM_PP_STORE_AUX);
+                    __builtin_amdgcn_raw_buffer_store_b32(*reinterpret_cast<const uint32_t*>(lb + 2048 + v[2]), rsD2, xo[j], sO, EVAM_PP_STORE_AUX);
                 } else {
-                    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v[0], rsD0, xo[j], sO, 0);
-                    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v[1], rsD1, xo[j], sO, 0);
-                    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v[2], rsD2, xo[j], sO, 0);
+                    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v[0], rsD0, xo[j], sO, EVAM_PP_STORE_AUX);
+                    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v[1], rsD1, xo[j], sO, EVAM_PP_STORE_AUX);
+                    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v[2], rsD2, xo[j], sO, EVAM_PP_STORE_AUX);
                 }
             };
             if ((b0 | b1) == 0 || (P.ablate & 2)) {  // padding row (wave-uniform)
@@ -1119,21 +1129,21 @@ __device__ __forceinline__ void store_vec(const __amdgpu_buffer_rsrc_t rs, uint3
         if constexpr (PX == 4) {
             evam_v4i q = {(int)__float_as_uint(lut[v[0]]), (int)__float_as_uint(lut[v[1]]),
                           (int)__float_as_uint(lut[v[2]]), (int)__float_as_uint(lut[v[3]])};
-            __builtin_amdgcn_raw_buffer_store_b128(q, rs, vo, so, 0);
+            __builtin_amdgcn_raw_buffer_store_b128(q, rs, vo, so, EVAM_PP_STORE_AUX);
         } else if constexpr (PX == 2) {
             evam_v2i q = {(int)__float_as_uint(lut[v[0]]), (int)__float_as_uint(lut[v[1]])};
-            __builtin_amdgcn_raw_buffer_store_b64(q, rs, vo, so, 0);
+            __builtin_amdgcn_raw_buffer_store_b64(q, rs, vo, so, EVAM_PP_STORE_AUX);
         } else {
-            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lut[v[0]]), rs, vo, so, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lut[v[0]]), rs, vo, so, EVAM_PP_STORE_AUX);
         }
     } else {
         if constexpr (PX == 4)
             __builtin_amdgcn_raw_buffer_store_b32((uint32_t)v[0] | ((uint32_t)v[1] << 8) | ((uint32_t)v[2] << 16) |
-                                                      ((uint32_t)v[3] << 24), rs, vo, so, 0);
+                                                      ((uint32_t)v[3] << 24), rs, vo, so, EVAM_PP_STORE_AUX);
         else if constexpr (PX == 2)
-            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(v[0] | (v[1] << 8)), rs, vo, so, 0);
+            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(v[0] | (v[1] << 8)), rs, vo, so, EVAM_PP_STORE_AUX);
         else
-            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v[0], rs, vo, so, 0);
+            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v[0], rs, vo, so, EVAM_PP_STORE_AUX);
     }
 }
 
@@ -1258,7 +1268,7 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_wave(const WParams P) {
         for (int c = 0; c < nck; c += 64) {
             if (lane + c < nck)
                 __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(dst + c * 16), 16,
-                                                         (lane + c) * 16, soff, 0, 0);
+                                                         (lane + c) * 16, soff, EVAM_PP_LOAD_AUX, 0);
         }
     };
     auto issue = [&](const Plan& q, uint8_t* buf) {
@@ -1658,11 +1668,11 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(96))) void
             if (on) {
                 const int yr = tap ? yb : ya;
                 if (pl == 0)
-                    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsY, dstl, 16, yr * pitch0 + fsY + c * 16, 0, 0, 0);
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsY, dstl, 16, yr * pitch0 + fsY + c * 16, 0, EVAM_PP_LOAD_AUX, 0);
                 else if (pl == 1)
-                    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsC, dstl, 16, (yr >> 1) * pitch1 + fsC + c * 16, 0, 0, 0);
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsC, dstl, 16, (yr >> 1) * pitch1 + fsC + c * 16, 0, EVAM_PP_LOAD_AUX, 0);
                 else
-                    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsV, dstl, 16, (yr >> 1) * pitch2 + fsC + c * 16, 0, 0, 0);
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsV, dstl, 16, (yr >> 1) * pitch2 + fsC + c * 16, 0, EVAM_PP_LOAD_AUX, 0);
             }
         }
     };
