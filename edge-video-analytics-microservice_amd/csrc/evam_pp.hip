@@ -1076,12 +1076,27 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_staged(const SParams P) {
         asm volatile("" :: "v"(lY0[0]), "v"(lC0[0]), "v"(wa[0]), "v"(lY1[0]), "v"(lC1[0]));
         return;
     }
+    // Stores this wave issues for a full group (3 per owned row; the padding select is branchless).
+    int st_full = 0;
+#pragma unroll
+    for (int j = 0; j < SPW; j++) st_full += wave_stores[j] ? 3 * RPW : 0;
+    st_full = __builtin_amdgcn_readfirstlane(st_full);
     for (int g = 0; g < ngroups; g++) {
         // This wave's share of group g's DMA landed; everything issued after it (later groups' DMA, the
         // previous groups' stores) may stay in flight. The first iteration also covers the prologue's
         // global loads (LUT, column table), which were issued after the DMA.
-        if (g == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        else vmcnt_at_most(issued - q[0]);
+        if (g == 0) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        } else if constexpr (NBUF == 2) {
+            // Two buffers: only the stores of group g - 1 (a full group: group g exists) were issued
+            // after group g's DMA, and their count is a per-wave constant, so the wait is one
+            // immediate, not the counted ladder (scalar instructions are shared by the CU's waves).
+            if (st_full == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            else if (SPW == 1 || st_full == 3 * RPW) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(3 * RPW) : "memory");
+            else asm volatile("s_waitcnt vmcnt(%0)" :: "n"(6 * RPW) : "memory");
+        } else {
+            vmcnt_at_most(issued - q[0]);
+        }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();  // every wave's DMA for g landed; every wave done reading g-1
 #pragma unroll
