@@ -168,7 +168,11 @@ struct SParams {
     uint32_t fill;
     int ablate;
     int xcd_remap;       // 1: consecutive tiles land on one XCD (shared halo rows stay in one L2)
+    int ntcol;           // tiles_x when <= kTCols (tcol valid), else 0 (the kernel reads xtab)
+    int2 tcol[16];       // per tile column: crop-relative source columns of its first / last visible
+                         // output column's taps, or (-1, -1) for a tile of padding columns only
 };
+constexpr int kTCols = 16;
 
 // Workgroups are dispatched round-robin over the 8 XCDs (block b runs on XCD b % 8). Remap so each
 // XCD walks a contiguous run of tiles: neighbouring tiles of one frame share source rows at their
@@ -774,12 +778,21 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_staged(const SParams P) {
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    if (P.ablate & 128) return;  // diagnostics: launch cost only
+    // Prologue critical path: the launch parameters, then (in parallel) the item's arguments, the tile's
+    // row table and its column footprint (from the parameters when tiles_x <= kTCols), then the first
+    // DMA. Nothing waits on a load it does not need.
     const int t = P.xcd_remap ? xcd_tile(blockIdx.x, gridDim.x) : (int)blockIdx.x;
     const int item = t / P.tiles_per_item;
     const int tile = t - item * P.tiles_per_item;
     const int ty = tile / P.tiles_x;
     const int tx = tile - ty * P.tiles_x;
+    const int Y0 = ty * P.TH, Y1 = min(Y0 + P.TH, P.DH);
+    const int rows = Y1 - Y0;
+    // The tile's row table (<= 64 rows, host-checked), one row per lane in every wave: per-group lookups
+    // are v_readlane instead of dependent scalar loads from L2 (~1 us per group in the loop's critical
+    // path when the frames stream from HBM, profiles/r02_skeleton.txt).
+    LaneRows lr;
+    lr.load(P.ytab, Y0, rows, lane);
     const ItemArg& it = P.items[item];
     const __attribute__((address_space(4))) XTab* xtab_s = (const __attribute__((address_space(4))) XTab*)(P.xtab);
     const uint8_t* p0 = it.plane[0];
@@ -806,15 +819,19 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_staged(const SParams P) {
     const uint32_t fsh = OUT == 1 ? 2 : 0;
     const uint32_t fillv[3] = {(P.color_rgb ? fq2 : fq0) << fsh, fq1 << fsh, (P.color_rgb ? fq0 : fq2) << fsh};
 
-    const int X0 = tx * TW, Y0 = ty * P.TH, Y1 = min(Y0 + P.TH, P.DH);
+    const int X0 = tx * TW;
     const int rph = NSEGX >= 4 ? 0 : wave / NSEGX;
     // visible (non-padding) columns of the tile -> source footprint (wave-uniform)
     const int Xv0 = max(X0, ox), Xv1 = min(min(X0 + TW, P.DW), ox + rw) - 1;
     const bool cols = Xv0 <= Xv1;
     int fsY = 0, nY = 0, fsC = 0, nC = 0;
     if (cols) {
-        footprint_chunks(FMT, T::bpp, x0 + xtab_s[Xv0].s0, x0 + xtab_s[Xv1].s1, fsY, nY, fsC, nC);
+        int s0, s1;
+        if (tx < P.ntcol) { s0 = P.tcol[tx].x; s1 = P.tcol[tx].y; }
+        else { s0 = xtab_s[Xv0].s0; s1 = xtab_s[Xv1].s1; }
+        footprint_chunks(FMT, T::bpp, x0 + s0, x0 + s1, fsY, nY, fsC, nC);
     }
+    if (P.ablate & 128) return;  // diagnostics: prologue parameters only
     // per-lane column state for each of this wave's SPW 64-column segments (seg = wave + 4 j, or
     // wave % NSEGX for narrow tiles), filled once the first DMA is in flight: LDS byte offsets of the taps
     // inside a slot, weights
@@ -830,13 +847,7 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_staged(const SParams P) {
         xo[j] = (uint32_t)(xin[j] ? X[j] : 0) * (uint32_t)esz;
         lY0[j] = lY1[j] = lC0[j] = lC1[j] = wa[j] = wp[j] = 0;
     }
-    const int rows = Y1 - Y0;
     const int ngroups = (rows + R - 1) / R;
-    // The tile's row table (<= 64 rows, host-checked), one row per lane in every wave: per-group lookups
-    // are v_readlane instead of dependent scalar loads from L2 (~1 us per group in the loop's critical
-    // path when the frames stream from HBM, profiles/r02_skeleton.txt).
-    LaneRows lr;
-    lr.load(P.ytab, Y0, rows, lane);
 
     // ---- LDS-DMA of group g into buffer `buf` (slot s = plane * 2R + 2 * row + tap) ----
     // Returns the number of VMEM instructions this wave issued (wave-uniform; nY, nC >= 1 whenever
@@ -3042,6 +3053,11 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
                 sp.offBuf = cfg->out_dtype == EVAM_DTYPE_F32 ? kLutBytes : 0;
                 sp.slot_bytes = seg_bytes(tw);  // <= the kernel's SLOT_MAX (tile choice above)
                 sp.buf_bytes = 2 * R * np * sp.slot_bytes;
+                sp.ntcol = sp.tiles_x <= kTCols ? sp.tiles_x : 0;
+                for (int c = 0; c < sp.ntcol; c++) {
+                    const int Xv0 = std::max(c * tw, g0.ox), Xv1 = std::min(std::min(c * tw + tw, DW), g0.ox + g0.rw) - 1;
+                    sp.tcol[c] = Xv0 <= Xv1 ? int2{hx[Xv0].s0, hx[Xv1].s1} : int2{-1, -1};
+                }
                 sp.color_rgb = color_rgb;
                 sp.fill = fill;
                 sp.ablate = kn.ablate;

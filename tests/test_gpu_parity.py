@@ -362,7 +362,7 @@ def test_stats_and_timing(evam, O, gpu):
     ((480, 270), (224, 224), "aspect-crop"),        # C5 shape: central crop
 ])
 @pytest.mark.parametrize("variant", ["auto", "wave", "px1", "px2", "noreuse", "staged", "staged_xcd", "staged_r1",
-                                     "staged_wide", "staged_b3"])
+                                     "staged_wide", "staged_b3", "staged_slot2k"])
 def test_wave_kernel_variants(evam, O, coracle, gpu, fmt, src, dst, resize, variant, monkeypatch):
     """Uniform-geometry batches through the default kernel choice, the wave-row kernel forced
     (EVAM_PP_WAVE=2; every PX / REUSE choice) and the staged kernel (EVAM_PP_WAVE=0; with the
@@ -375,7 +375,8 @@ def test_wave_kernel_variants(evam, O, coracle, gpu, fmt, src, dst, resize, vari
            "staged": {"EVAM_PP_WAVE": "0"}, "staged_xcd": {"EVAM_PP_WAVE": "0", "EVAM_PP_XCD": "1"},
            "staged_r1": {"EVAM_PP_WAVE": "0", "EVAM_PP_STAGE_R": "1"},
            "staged_wide": {"EVAM_PP_WAVE": "0", "EVAM_PP_NSEGX": "8"},
-           "staged_b3": {"EVAM_PP_WAVE": "0", "EVAM_PP_STAGE_NBUF": "3"}}.get(variant, {})
+           "staged_b3": {"EVAM_PP_WAVE": "0", "EVAM_PP_STAGE_NBUF": "3"},
+           "staged_slot2k": {"EVAM_PP_WAVE": "0", "EVAM_PP_WIDE_SLOT": "1"}}.get(variant, {})
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     if variant == "px2" and dst[0] % 2:
@@ -543,3 +544,40 @@ def test_roi_batches_many_frames(evam, O, coracle, gpu, fmt, n_frames):
                      rois=[evam.Roi(*r) for r in rois])
     ref, _ = run_oracle(O, coracle, frames, shape, "f32", info, rois=rois)
     assert_same(got, ref, f"roi records {fmt} frames={n_frames}")
+
+
+@pytest.mark.parametrize("fmt", ["NV12", "I420", "BGR"])
+def test_staged_many_tile_columns(evam, O, coracle, gpu, fmt, monkeypatch):
+    """A staged launch with more tile columns than the kernel-argument footprint table holds (tiles_x >
+    16: each tile's footprint comes from the column table in device memory instead)."""
+    import torch
+
+    monkeypatch.setenv("EVAM_PP_WAVE", "0")
+    monkeypatch.setenv("EVAM_PP_NSEGX", "2")  # 128-column tiles: 2200 / 128 -> 18 tile columns
+    rng = np.random.default_rng(zlib.crc32(f"tcol{fmt}".encode()))
+    frames = [O.random_frame(rng, fc(O, fmt), 2400, 64, pattern=p) for p in ("uniform", "gradient")]
+    info = evam.PreProcInfo(resize="aspect-ratio", placement="center", fill=(3, 4, 5))
+    shape = (2, 3, 40, 2200)
+    got, _ = run_hip(evam, torch, upload(evam, frames, gpu), shape, torch.uint8, info)
+    ref, _ = run_oracle(O, coracle, frames, shape, "u8", info)
+    assert_same(got, ref, f"staged >16 tile columns {fmt}")
+
+
+@pytest.mark.parametrize("unit", ["2", "4"])
+def test_roi_work_units(evam, O, coracle, gpu, unit, monkeypatch):
+    """ROI batches with the crops split into row tiles of a few row groups each (EVAM_PP_ROI_UNIT): every
+    tile of a ROI lands in its own rows of the ROI's slot."""
+    import torch
+
+    monkeypatch.setenv("EVAM_PP_ROI_UNIT", unit)
+    rng = np.random.default_rng(zlib.crc32(f"unit{unit}".encode()))
+    W, H = 640, 360
+    frames = [O.random_frame(rng, O.NV12, W, H, pattern="gradient" if i else "uniform") for i in range(2)]
+    rois = [(int(rng.integers(0, 2)), int(rng.integers(0, W - 8)), int(rng.integers(0, H - 8)),
+             int(rng.integers(8, 400)), int(rng.integers(8, 300))) for _ in range(40)]
+    info = evam.PreProcInfo(range=(0.0, 1.0), mean=(0.1, 0.2, 0.3), std=(0.3, 0.2, 0.1))
+    shape = (len(rois), 3, 72, 72)
+    got, _ = run_hip(evam, torch, upload(evam, frames, gpu), shape, torch.float32, info,
+                     rois=[evam.Roi(*r) for r in rois])
+    ref, _ = run_oracle(O, coracle, frames, shape, "f32", info, rois=rois)
+    assert_same(got, ref, f"roi units {unit}")
