@@ -279,6 +279,10 @@ class COracle:
         L.orc_preprocess_item.restype = ctypes.c_int
         L.orc_num_threads.restype = ctypes.c_int
         L.orc_set_num_threads.argtypes = [ctypes.c_int]
+        L.orc_fast_batch.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                     ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                     ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+        L.orc_fast_batch.restype = ctypes.c_int
 
     @staticmethod
     def _ptr(a, t=ctypes.c_uint8):
@@ -341,3 +345,43 @@ class COracle:
         if rc != 0:
             raise ValueError(f"oracle rejected item (rc={rc})")
         return tuple(int(v) for v in geom)
+
+
+class OrcFrame(ctypes.Structure):
+    """orc_frame of oracle/evam_cpu_fast.c."""
+
+    _fields_ = [("planes", ctypes.c_void_p * 3), ("pitch", ctypes.c_int32 * 3), ("fourcc", ctypes.c_int32),
+                ("width", ctypes.c_int32), ("height", ctypes.c_int32), ("pad_", ctypes.c_int32)]
+
+
+class FastBatch:
+    """The CPU baseline (oracle/evam_cpu_fast.c, same arithmetic as the oracle, OpenCV-style organisation):
+    a whole batch of items in one call. The frames and ROI array are marshalled once, so a timed loop
+    measures the C code, not ctypes."""
+
+    def __init__(self, coracle: "COracle", frames, rois=None):
+        self.lib = coracle.lib
+        self.planes = [[np.ascontiguousarray(p) for p in f.planes] for f in frames]
+        self.frames = (OrcFrame * len(frames))()
+        for k, (f, pl) in enumerate(zip(frames, self.planes)):
+            for i, p in enumerate(pl):
+                self.frames[k].planes[i] = p.ctypes.data
+                self.frames[k].pitch[i] = p.shape[1]
+            self.frames[k].fourcc, self.frames[k].width, self.frames[k].height = f.fourcc, f.width, f.height
+        items = rois if rois is not None else [(i, 0, 0, 0, 0) for i in range(len(frames))]
+        self.items = np.ascontiguousarray(np.asarray(items, np.int32).reshape(-1, 5))
+
+    def run(self, out: np.ndarray, mode=0, placement=0, color_rgb=False, lut=None, fill=(0, 0, 0), slot_offset=0,
+            slot_stride=1):
+        out_f32 = out.dtype == np.float32
+        if out_f32:
+            self._lut = np.ascontiguousarray(lut if lut is not None else np_norm_lut(0), np.float32)
+        self._fill = np.asarray(fill, np.uint8)
+        DH, DW = out.shape[2], out.shape[3]
+        rc = self.lib.orc_fast_batch(len(self.items), ctypes.addressof(self.frames), self.items.ctypes.data, mode,
+                                     placement, int(color_rgb), int(out_f32),
+                                     self._lut.ctypes.data if out_f32 else None, self._fill.ctypes.data,
+                                     out.ctypes.data, slot_offset, slot_stride, DW, DH)
+        if rc != 0:
+            raise ValueError(f"CPU baseline rejected the batch (rc={rc})")
+

@@ -184,3 +184,37 @@ def test_saturating_clamp_identity():
     mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)
     assert mod.check() == 0
+
+
+@pytest.mark.parametrize("fmt", ["NV12", "I420", "BGRX", "BGR"])
+@pytest.mark.parametrize("mode,placement,rgb,dst,dtype", [
+    (0, 0, False, (72, 72), "f32"), (1, 1, True, (96, 64), "u8"), (2, 0, False, (40, 56), "f32"),
+    (1, 0, False, (33, 17), "u8"), (0, 0, True, (300, 170), "f32")])
+def test_cpu_fast_matches_oracle(O, coracle, fmt, mode, placement, rgb, dst, dtype):
+    """The bench's CPU baseline (oracle/evam_cpu_fast.c: batch-parallel, row-cached, vectorised) is
+    byte-identical to the oracle on ROI batches with edge, odd, partly outside and full-frame items,
+    up- and downscales, letterbox / central crop, RGB order and clip-ring slot strides."""
+    f = {"NV12": O.NV12, "I420": O.I420, "BGRX": O.BGRX, "BGR": O.BGR}[fmt]
+    rng = np.random.default_rng(hash((fmt, mode, dst)) & 0xFFFF)
+    frames = [O.random_frame(rng, f, 160, 90, pattern=p) for p in ("uniform", "gradient", "uniform")]
+    rois = [(0, 0, 0, 0, 0), (1, 0, 0, 0, 0), (2, -5, -3, 40, 30), (1, 151, 81, 20, 20), (0, 3, 5, 1, 1),
+            (2, 17, 9, 131, 77), (1, 60, 40, 7, 45)]
+    for _ in range(13):  # clipped rects stay non-empty (the oracle rejects an empty crop)
+        x, y = int(rng.integers(-10, 150)), int(rng.integers(-10, 80))
+        rois.append((int(rng.integers(0, 3)), x, y, int(rng.integers(1, 170)) + max(0, -x),
+                     int(rng.integers(1, 100)) + max(0, -y)))
+    lut = O.np_norm_lut(3, (0.0, 1.0), (0.1, 0.2, 0.3), (0.3, 0.2, 0.1)) if dtype == "f32" else None
+    npd = np.float32 if dtype == "f32" else np.uint8
+    stride = 2 if dst == (33, 17) else 1
+    shape = (len(rois) * stride + 1, 3, dst[1], dst[0])
+    ref = np.full(shape, 7, npd)
+    for i, r in enumerate(rois):
+        coracle.preprocess_item(frames[r[0]], r[1:], ref, 1 + i * stride, mode=mode, placement=placement,
+                                color_rgb=rgb, lut=lut, fill=(4, 5, 6))
+    got = np.full(shape, 7, npd)
+    O.FastBatch(coracle, frames, rois).run(got, mode=mode, placement=placement, color_rgb=rgb, lut=lut,
+                                           fill=(4, 5, 6), slot_offset=1, slot_stride=stride)
+    if dtype == "f32":
+        assert (got.view(np.uint32) == ref.view(np.uint32)).all()
+    else:
+        assert (got == ref).all()
