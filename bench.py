@@ -211,9 +211,12 @@ def via_pipeline(args, evam, torch, wl, device_index):
     S, F = args.streams, args.frames_per_stream
     ps.PipelineServer.start({"pipeline_dir": os.path.join(tmp, "pipelines"), "model_dir": os.path.join(tmp, "models"),
                              "device": device_index, "batch_max": args.hub_batch, "batch_wait_ms": 1.0,
-                             "batch_target": args.hub_batch})
+                             "batch_target": args.hub_batch, "runner": args.runner})
     ps.PipelineServer.register_model("bench_detector/1", ps.InferenceModel(detector, (DW, DH), name="bench"))
-    pool = device_frames(evam, torch, wl, 2 * S, torch.device(f"cuda:{device_index}"), seed=99)
+    # distinct frames: at least 2 per stream and >= 3x the Infinity Cache, as the direct leg's pool
+    W, H = wl["src"]
+    n_pool = max(2 * S, -(-3 * MALL_BYTES // (W * H * 3 // 2)))
+    pool = device_frames(evam, torch, wl, n_pool, torch.device(f"cuda:{device_index}"), seed=99)
 
     def run(frames_per_stream):
         qs, pipes = [], []
@@ -242,7 +245,8 @@ def via_pipeline(args, evam, torch, wl, device_index):
     sizes = [b[1] for b in ps.PipelineServer.hub().batches]
     ps.PipelineServer.stop()
     return {"value": round(S * F / el, 1), "elapsed_s": round(el, 4), "streams": S, "frames_per_stream": F,
-            "stream_batch_size": args.stream_batch, "hub_launches": len(sizes),
+            "stream_batch_size": args.stream_batch, "runner": args.runner, "pool_frames": n_pool,
+            "hub_launches": len(sizes),
             "mean_frames_per_launch": round(float(np.mean(sizes)), 2) if sizes else 0.0}
 
 
@@ -283,6 +287,8 @@ def main():
     ap.add_argument("--frames-per-stream", type=int, default=1024, help="--via pipeline: frames per stream")
     ap.add_argument("--stream-batch", type=int, default=16, help="--via pipeline: gvadetect batch-size per stream")
     ap.add_argument("--hub-batch", type=int, default=256, help="--via pipeline: max frames per hub launch")
+    ap.add_argument("--runner", choices=["device", "threads"], default="device",
+                    help="--via pipeline: one runner thread per device (default) or one thread per pipeline")
     args = ap.parse_args()
 
     import torch
@@ -317,8 +323,11 @@ def main():
             "n_gpus": 1, "higher_is_better": True, "dtype": "u8" if wl["dtype"] == "u8" else "u8->f32",
             "data": "synthetic device-resident frames through application sources; null detector",
             "config": {"workload": wl["desc"], **r,
-                       "path": "Pipeline thread per stream -> gvadetect stage -> per-device BatchHub -> one "
-                               "evam_pp_run per tick -> model -> per-frame results"}}), flush=True)
+                       "path": ("one runner thread per device: bulk ingest of every stream's queue -> gvadetect "
+                                "stage -> one evam_pp_run per tick over all streams -> model -> per-frame results"
+                                if args.runner == "device" else
+                                "Pipeline thread per stream -> gvadetect stage -> per-device BatchHub -> one "
+                                "evam_pp_run per tick -> model -> per-frame results")}}), flush=True)
         return
     n = args.frames or wl["frames"]
     strong = args.config == "c4" and world > 1 and not args.frames

@@ -37,6 +37,7 @@ device ``Image``s, or host planes uploaded on arrival.
 """
 from __future__ import annotations
 
+import gc
 import json
 import os
 import queue
@@ -319,12 +320,12 @@ class _Request:
 
     __slots__ = ("stage", "items", "units", "t0", "done", "error")
 
-    def __init__(self, stage, items, units):
+    def __init__(self, stage, items, units, event=True):
         self.stage = stage
         self.items = items
         self.units = units
         self.t0 = time.perf_counter()
-        self.done = threading.Event()
+        self.done = threading.Event() if event else None
         self.error = None
 
 
@@ -434,6 +435,136 @@ class BatchHub:
             self._pp = None
 
 
+class DeviceRunner:
+    """Per-device pipeline runner (the default; server option ``runner``: ``"device"`` | ``"threads"``).
+
+    One thread services every pipeline the device owns, the way one GStreamer main loop serves many
+    pipelines in native code: it drains each application source in bulk, and once the ready frames of
+    all pipelines reach the hub's ``target`` (or the oldest has waited ``max_wait_s``) it runs one tick —
+    stage by stage, ONE ``evam_pp_run`` and one model call per interchangeable stage over every pipeline's
+    frames (chunks of at most ``max_batch`` units), then each pipeline's per-stream bookkeeping and its
+    destination. With one Python thread per stream instead (``"threads"``: 32 pipeline threads handing
+    requests to the :class:`BatchHub` thread) the GIL hand-offs and per-frame queue calls bounded the
+    pipeline layer at ~28 % of the kernel rate (``profiles/r02r_bench_via_pipeline*.json``).
+    """
+
+    def __init__(self, hub: "BatchHub"):
+        self.hub = hub
+        self._pipes: list = []
+        self._cv = threading.Condition()
+        self._stop = False
+        self._thread = threading.Thread(target=self._loop, name=f"evam-runner-{hub.device}", daemon=True)
+        self._thread.start()
+
+    def add(self, pipe):
+        with self._cv:
+            if self._stop:
+                raise RuntimeError("device runner is closed")
+            self._pipes.append(pipe)
+            self._cv.notify()
+
+    def close(self):
+        with self._cv:
+            self._stop = True
+            self._cv.notify_all()
+        self._thread.join(10)
+
+    def _loop(self):
+        hub = self.hub
+        idle = 0.0005
+        while True:
+            with self._cv:
+                while not self._pipes and not self._stop:
+                    self._cv.wait()
+                if self._stop and not self._pipes:
+                    return
+                pipes = list(self._pipes)
+            ready, oldest, total, done = [], None, 0, []
+            for p in pipes:
+                try:
+                    p._ingest()
+                except Exception as e:  # noqa: BLE001 — reported through status(), as the reference does
+                    p._fail(e)
+                    done.append(p)
+                    continue
+                n = len(p._pend)
+                if p._stop.is_set() or (p._eos and not n):
+                    p._end()
+                    done.append(p)
+                elif n >= p._batch or p._eos:
+                    ready.append(p)
+                    total += n
+                    oldest = p._pend_t0 if oldest is None else min(oldest, p._pend_t0)
+            if done:
+                with self._cv:
+                    self._pipes = [p for p in self._pipes if p not in done]
+            if not ready:
+                time.sleep(idle)
+                continue
+            if total < (hub.target or 1) and time.perf_counter() - oldest < hub.max_wait_s:
+                time.sleep(idle)
+                continue
+            # about max_batch frames per tick, in whole batch-size multiples per pipeline
+            share = max(1, hub.max_batch // len(ready))
+            work = []
+            for p in ready:
+                k = max(p._batch, share // p._batch * p._batch)
+                if not p._eos:
+                    k = min(k, len(p._pend) // p._batch * p._batch)
+                work.append((p, p._pend[:k]))
+                del p._pend[:k]
+                p._pend_t0 = time.perf_counter()
+            self._tick(work)
+
+    def _tick(self, work):
+        """Run the stage chains of `work` [(pipeline, frames)] stage by stage, batched across pipelines."""
+        hub = self.hub
+        failed = set()
+        depth = max(len(p.stages) for p, _ in work)
+        for k in range(depth):
+            groups: dict = {}
+            for p, items in work:
+                if p in failed or k >= len(p.stages) or not items:
+                    continue
+                st = p.stages[k]
+                try:
+                    if not st.batchable:
+                        st.process(items)
+                        continue
+                    w, units = st.prepare(items)
+                except Exception as e:  # noqa: BLE001
+                    p._fail(e)
+                    failed.add(p)
+                    continue
+                if units > 0:
+                    groups.setdefault(st.hub_key(), []).append((p, _Request(st, w, units, event=False)))
+            for key, reqs in groups.items():
+                i = 0
+                while i < len(reqs):  # chunks of at most max_batch units (at least one request)
+                    j, n = i, 0
+                    while j < len(reqs) and (j == i or n + reqs[j][1].units <= hub.max_batch):
+                        n += reqs[j][1].units
+                        j += 1
+                    chunk = reqs[i:j]
+                    i = j
+                    try:
+                        chunk[0][1].stage.run_batch([r for _, r in chunk], hub.pp())
+                        hub.batches.append((key, n, len(chunk)))
+                        if len(hub.batches) > 4096:
+                            del hub.batches[:2048]
+                    except Exception as e:  # noqa: BLE001 — delivered to every pipeline of the batch
+                        for p, _ in chunk:
+                            p._fail(e)
+                            failed.add(p)
+                        continue
+                    for p, r in chunk:
+                        if p not in failed:
+                            r.stage.finish(r.items)
+        for p, items in work:
+            if p not in failed:
+                p._emit_all(items)
+
+
 class _InferenceStage:
     """Common part of gvadetect / gvaclassify: interval gating, model lookup, HIP pre-processing.
 
@@ -464,6 +595,22 @@ class _InferenceStage:
     def out_dtype(self) -> int:
         return N.DTYPE_F32 if self.model.out_dtype == "f32" else N.DTYPE_U8
 
+    # A stage's work for one stream: prepare (gating / selection, on the caller's thread) -> run_batch over the
+    # requests of every interchangeable stage (one launch) -> finish (per-stream bookkeeping).
+    batchable = True
+
+    def prepare(self, items):
+        raise NotImplementedError
+
+    def finish(self, work):
+        pass
+
+    def process(self, items):
+        """Thread runner: gate, hand the work to the device's BatchHub (blocks until its batch ran), finish."""
+        work, units = self.prepare(items)
+        self.server.hub().submit(self, work, units)
+        self.finish(work)
+
     def hub_key(self):
         """Stages with equal keys are interchangeable: their requests run as one batch."""
         return (self.el.factory, id(self.model), self.info.cache_key(self.out_dtype()), self.threshold)
@@ -489,10 +636,10 @@ class _InferenceStage:
 
 
 class DetectStage(_InferenceStage):
-    def process(self, items):
-        """items: list of (frame_index, Image, FrameResult). Appends regions to each FrameResult."""
-        run = [it for it in items if it[0] % self.interval == 0]
-        self.server.hub().submit(self, run, len(run))
+    def prepare(self, items):
+        """items: list of (frame_index, Image, FrameResult) -> (the frames to infer, units)."""
+        run = [it for it in items if it[0] % self.interval == 0] if self.interval > 1 else items
+        return run, len(run)
 
     def run_batch(self, reqs, pp):
         """One launch over the frames of every request (hub thread)."""
@@ -532,7 +679,7 @@ class ClassifyStage(_InferenceStage):
         oc = tuple(sorted(self.object_class)) if self.object_class else None
         return super().hub_key() + (oc,)
 
-    def process(self, items):
+    def prepare(self, items):
         work = []          # (frame_index, Image, [regions to classify])
         for fi, img, fr in items:
             if fi % self.interval:
@@ -551,7 +698,9 @@ class ClassifyStage(_InferenceStage):
                 todo.append(r)
             if todo:
                 work.append((fi, img, todo))
-        self.server.hub().submit(self, work, sum(len(t) for _, _, t in work))
+        return work, sum(len(t) for _, _, t in work)
+
+    def finish(self, work):
         if self.reclassify > 1:
             for fi, _, todo in work:
                 for r in todo:
@@ -600,6 +749,7 @@ class ActionRecognitionStage(_InferenceStage):
     """
 
     CLIP = 16
+    batchable = False
 
     def __init__(self, el, server, device):
         super().__init__(el, server, device)
@@ -674,6 +824,13 @@ class Pipeline:
         self.end_time = None
         self._thread = None
         self._stop = threading.Event()
+        # device-runner state (DeviceRunner): frames ingested and not yet run, end of stream, completion
+        self._pend: list = []
+        self._pend_t0 = 0.0
+        self._eos = False
+        self._batch = 1
+        self._done = threading.Event()
+        self._runner = False
 
     # -- construction ------------------------------------------------------------------------
     def build(self, source=None, parameters=None):
@@ -708,9 +865,86 @@ class Pipeline:
         self.destination = destination or {}
         self.state = self.RUNNING
         self.start_time = time.time()
-        self._thread = threading.Thread(target=self._run, name=f"pipeline-{self.id}", daemon=True)
-        self._thread.start()
+        if self.server.options.get("runner", "device") == "threads":
+            self._thread = threading.Thread(target=self._run, name=f"pipeline-{self.id}", daemon=True)
+            self._thread.start()
+        else:
+            self._runner = True
+            self._batch = max([getattr(s, "batch_size", 1) for s in self.stages] + [1])
+            self._pend_t0 = time.perf_counter()
+            self.server.runner().add(self)
         return self.id
+
+    # -- device-runner side (called on the DeviceRunner thread only) ----------------------------------
+    def _ingest(self):
+        """Move whatever the source holds now into ``_pend`` as (frame_index, Image, FrameResult), without
+        blocking: an application queue is drained in one step under its lock, not item by item."""
+        if self._eos:
+            return
+        src = self.source
+        kind = src.get("type")
+        if kind == "application":
+            q = src.get("input")
+            if isinstance(q, queue.Queue):
+                with q.mutex:
+                    got = list(q.queue)
+                    q.queue.clear()
+                    q.not_full.notify_all()
+            else:
+                got = []
+                while True:
+                    try:
+                        got.append(q.get_nowait())
+                    except queue.Empty:
+                        break
+        elif kind == "frames":
+            got = list(src.get("frames", [])) + [None]
+        else:
+            raise PreProcError(N.ERR_UNSUPPORTED, f"source type {kind!r}: decode is upstream of this build; use an "
+                                                  "'application' source of decoded frames")
+        if not got:
+            return
+        if any(x is None for x in got):     # end of stream
+            got = got[:next(i for i, x in enumerate(got) if x is None)]
+            self._eos = True
+        if not got:
+            return
+        if not self._pend:
+            self._pend_t0 = time.perf_counter()
+        base, uri, FR = self.frames, self.source.get("uri"), P.FrameResult
+        if all(type(x) is Image for x in got):
+            self._pend.extend([(base + k, im, FR(im.width, im.height, base + k, uri)) for k, im in enumerate(got)])
+        else:
+            for k, item in enumerate(got):
+                img = self._as_image(item)
+                ts = int(item.get("timestamp", 0)) if isinstance(item, dict) else base + k
+                self._pend.append((base + k, img, FR(img.width, img.height, timestamp=ts, source=uri)))
+        self.frames += len(got)
+
+    def _emit_all(self, items):
+        dst = self.destination.get("metadata", self.destination)
+        if dst.get("output") is None:
+            return
+        for _, img, fr in items:
+            self._emit(fr, img)
+
+    def _fail(self, e):
+        self.error = f"{type(e).__name__}: {e}"
+        self.state = self.ERROR
+        self._end()
+
+    def _end(self):
+        if self._done.is_set():
+            return
+        if self.state == self.RUNNING:
+            self.state = self.ABORTED if self._stop.is_set() else self.COMPLETED
+        for st in self.stages:
+            st.close()
+        self.end_time = time.time()
+        dst = self.destination.get("metadata", self.destination)
+        if dst.get("output") is not None:
+            dst["output"].put(None)
+        self._done.set()
 
     def _frames(self):
         src = self.source
@@ -799,7 +1033,9 @@ class Pipeline:
         return self.status()
 
     def wait(self, timeout=None):
-        if self._thread is not None:
+        if self._runner:
+            self._done.wait(timeout)
+        elif self._thread is not None:
             self._thread.join(timeout)
         return self.status()
 
@@ -821,6 +1057,7 @@ class _Server:
         self.started = False
         self.device = 0
         self._hub = None
+        self._runner = None
         self._hub_lock = threading.Lock()
 
     def hub(self) -> BatchHub:
@@ -834,8 +1071,24 @@ class _Server:
                                      target=o.get("batch_target"))
             return self._hub
 
+    def runner(self) -> DeviceRunner:
+        """The device's pipeline runner (created on first use; it batches through the hub's limits)."""
+        hub = self.hub()
+        with self._hub_lock:
+            if self._runner is None:
+                if self.options.get("gc_freeze", True):
+                    # The heap built so far (torch, models, templates) leaves the collector's generations:
+                    # the runner makes a few short-lived objects per frame, and every young collection that
+                    # escalated would otherwise rescan it (2x the per-frame cost at 32 streams).
+                    gc.freeze()
+                self._runner = DeviceRunner(hub)
+            return self._runner
+
     def close_hub(self):
         with self._hub_lock:
+            if self._runner is not None:
+                self._runner.close()
+                self._runner = None
             if self._hub is not None:
                 self._hub.close()
                 self._hub = None

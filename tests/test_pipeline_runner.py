@@ -1,0 +1,159 @@
+"""The per-device pipeline runner (pipeline_server.DeviceRunner) on CPU: the HIP pre-processor is replaced by
+a recording stub (the kernels are covered by the GPU suites), so these tests check the runner's own logic —
+bulk ingest of application queues, batch-size gating and end of stream, one launch per interchangeable
+stage across pipelines bounded by batch_max, per-stream stage order, destinations, errors, stop — in the
+`"device"` runner and, for the same scenario, the `"threads"` runner (per-pipeline threads + BatchHub)."""
+import json
+import queue
+
+import pytest
+import torch
+
+from test_pipeline_server import PIPES, make_model_tree
+
+
+class StubPP:
+    """Records every convert call; returns lazily built identity transforms like HipPreProcessor."""
+
+    calls = []
+
+    def __init__(self, device=0, stream=None):
+        pass
+
+    def convert(self, srcs, out, info=None, rois=None, slot_offset=0, slot_stride=1, want_transform=False):
+        n_src = len(srcs)
+        n_roi = None if rois is None else len(rois)
+        StubPP.calls.append((n_src, n_roi, tuple(out.shape)))
+        if want_transform:
+            return [None] * n_src
+
+    def close(self):
+        pass
+
+
+@pytest.fixture
+def stubbed(evam, monkeypatch, tmp_path):
+    ps = evam.pipeline_server
+    pre = evam.preproc
+    monkeypatch.setattr(pre, "HipPreProcessor", StubPP)
+    monkeypatch.setattr(ps._InferenceStage, "_tensor",
+                        lambda self, n: torch.zeros((n, 3, self.model.input_size[1], self.model.input_size[0])))
+    StubPP.calls = []
+    mdir = make_model_tree(str(tmp_path / "models"), {
+        "det_alias": {"det_ver": (64, 64, {"input_preproc": [], "output_postproc": [{"labels": ["bg", "car"]}]})},
+        "cls_alias": {"cls_ver": (24, 24, {"input_preproc": [],
+                                           "output_postproc": [{"layer_name": "color", "attribute_name": "color",
+                                                                "labels": ["dark", "light"], "method": "max"}]})}})
+    yield ps, pre, mdir
+    ps.PipelineServer.stop()
+
+
+def frames(pre, n, w=64, h=48):
+    planes = [torch.zeros((h, w), dtype=torch.uint8), torch.zeros((h // 2, w), dtype=torch.uint8)]
+    return [pre.Image(pre.FOURCC_BY_NAME["NV12"], w, h, planes) for _ in range(n)]
+
+
+def register(ps, det_every=2, fail=False):
+    def detector(t):
+        if fail:
+            raise RuntimeError("model failed")
+        n = t.shape[0]
+        out = torch.full((n, 1, 7), -1.0)
+        out[::det_every, 0] = torch.tensor([0, 1, 0.9, 0.25, 0.25, 0.5, 0.75])   # a car on every det_every-th
+        return out
+
+    ps.PipelineServer.register_model("det_alias/det_ver", ps.InferenceModel(detector, (64, 64), name="det"))
+    ps.PipelineServer.register_model("cls_alias/cls_ver", ps.InferenceModel(
+        lambda t: {"color": torch.stack([torch.zeros(t.shape[0]), torch.ones(t.shape[0])], 1)}, (24, 24),
+        name="cls"))
+
+
+@pytest.mark.parametrize("runner", ["device", "threads"])
+def test_runner_batches_across_pipelines(stubbed, runner):
+    ps, pre, mdir = stubbed
+    ps.PipelineServer.start({"pipeline_dir": PIPES, "model_dir": mdir, "runner": runner, "batch_max": 8,
+                             "batch_wait_ms": 200, "batch_target": 8})
+    register(ps)
+    counts = [5, 3, 7, 1]  # frames per stream; batch-size 2 leaves a remainder flushed at end of stream
+    pipes, outs = [], []
+    for k, n in enumerate(counts):
+        qin, qout = queue.Queue(), queue.Queue()
+        for im in frames(pre, n):
+            qin.put(im)
+        qin.put(None)
+        p = ps.PipelineServer.pipeline("detect_classify", "hip")
+        p.start(source={"type": "application", "input": qin},
+                destination={"metadata": {"type": "application", "output": qout, "mode": "json"}},
+                parameters={"detection-properties": {"batch-size": 2}})
+        pipes.append(p)
+        outs.append(qout)
+    for p in pipes:
+        st = p.wait(60)
+        assert st["state"] == "COMPLETED", st
+    n_objects = 0
+    for n, q in zip(counts, outs):
+        lines = []
+        while (x := q.get(timeout=5)) is not None:
+            lines.append(json.loads(x))
+        assert len(lines) == n
+        for i, d in enumerate(lines):
+            objs = d.get("objects", [])
+            # frame i of a batch of 2 gets a car when its index in the launch is even; every car is classified
+            assert all("color" in o and o["color"]["label"] == "light" for o in objs)
+            n_objects += len(objs)
+    det = [c for c in StubPP.calls if c[1] is None]
+    cls = [c for c in StubPP.calls if c[1] is not None]
+    assert sum(c[0] for c in det) == sum(counts)           # every frame pre-processed exactly once
+    assert all(c[0] <= 8 for c in det)                       # batch_max frames per launch
+    assert len(det) < sum(counts)                            # frames of several streams share launches
+    assert n_objects > 0 and sum(c[1] for c in cls) == n_objects  # every car classified once
+    hub = ps.PipelineServer.hub()
+    assert any(b[2] > 1 for b in hub.batches)                # a launch served more than one pipeline
+
+
+def test_runner_model_error_marks_pipelines(stubbed):
+    ps, pre, mdir = stubbed
+    ps.PipelineServer.start({"pipeline_dir": PIPES, "model_dir": mdir})
+    register(ps, fail=True)
+    qin = queue.Queue()
+    for im in frames(pre, 3):
+        qin.put(im)
+    qin.put(None)
+    p = ps.PipelineServer.pipeline("detect_classify", "hip")
+    p.start(source={"type": "application", "input": qin}, destination={})
+    st = p.wait(60)
+    assert st["state"] == "ERROR" and "model failed" in st["message"]
+
+
+def test_runner_stop_and_frames_source(stubbed):
+    ps, pre, mdir = stubbed
+    ps.PipelineServer.start({"pipeline_dir": PIPES, "model_dir": mdir})
+    register(ps, det_every=1)
+    # a "frames" source: the list is the whole stream
+    qout = queue.Queue()
+    p = ps.PipelineServer.pipeline("detect_classify", "hip")
+    p.start(source={"type": "frames", "frames": frames(pre, 4)},
+            destination={"metadata": {"output": qout, "mode": "frames"}})
+    assert p.wait(60)["state"] == "COMPLETED"
+    got = []
+    while (x := qout.get(timeout=5)) is not None:
+        got.append(x)
+    assert len(got) == 4 and all(len(fr.regions) == 1 for _, fr in got)
+    # an application source that never ends: stop() aborts it
+    qin = queue.Queue()
+    for im in frames(pre, 2):
+        qin.put(im)
+    p2 = ps.PipelineServer.pipeline("detect_classify", "hip")
+    p2.start(source={"type": "application", "input": qin}, destination={})
+    p2.stop()
+    assert p2.wait(30)["state"] == "ABORTED"
+    assert p2.status()["elapsed_time"] >= 0
+
+
+def test_frame_result_lists_are_lazy(evam):
+    P = evam.postproc
+    fr = P.FrameResult(10, 20)
+    assert fr._regions is None and fr.regions == [] and fr._regions == []
+    fr.tensors.append(1)
+    assert fr.tensors == [1] and P.FrameResult(1, 2, regions=[5]).regions == [5]
+    assert json.loads(P.gvametaconvert_json(P.FrameResult(4, 4, timestamp=7)))["timestamp"] == 7
