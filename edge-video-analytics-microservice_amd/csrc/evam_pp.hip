@@ -1173,6 +1173,33 @@ __device__ __forceinline__ void store_vec(const __amdgpu_buffer_rsrc_t rs, uint3
     }
 }
 
+// Same, with the fp32 values given as byte offsets into an LDS LUT section `lb` (vfinal<1>): the LUT
+// read needs no address arithmetic (section base 0, 1024, 2048 is the instruction's immediate offset).
+template <int OUT, int PX>
+__device__ __forceinline__ void store_off(const __amdgpu_buffer_rsrc_t rs, uint32_t vo, const uint8_t* lb,
+                                          const uint32_t (&v)[PX]) {
+    if constexpr (OUT == 1) {
+        auto L = [&](uint32_t o) { return (int)*reinterpret_cast<const uint32_t*>(lb + o); };
+        if constexpr (PX == 4) {
+            evam_v4i q = {L(v[0]), L(v[1]), L(v[2]), L(v[3])};
+            __builtin_amdgcn_raw_buffer_store_b128(q, rs, vo, 0, EVAM_PP_STORE_AUX);
+        } else if constexpr (PX == 2) {
+            evam_v2i q = {L(v[0]), L(v[1])};
+            __builtin_amdgcn_raw_buffer_store_b64(q, rs, vo, 0, EVAM_PP_STORE_AUX);
+        } else {
+            __builtin_amdgcn_raw_buffer_store_b32((uint32_t)L(v[0]), rs, vo, 0, EVAM_PP_STORE_AUX);
+        }
+    } else {
+        if constexpr (PX == 4)
+            __builtin_amdgcn_raw_buffer_store_b32(v[0] | (v[1] << 8) | (v[2] << 16) | (v[3] << 24), rs, vo, 0,
+                                                  EVAM_PP_STORE_AUX);
+        else if constexpr (PX == 2)
+            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(v[0] | (v[1] << 8)), rs, vo, 0, EVAM_PP_STORE_AUX);
+        else
+            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v[0], rs, vo, 0, EVAM_PP_STORE_AUX);
+    }
+}
+
 // Uniform-geometry kernel built around independent waves. A workgroup owns a 64·PX-column x TH-row
 // tile of one item; each of its four waves owns a contiguous quarter of the tile's rows and walks it
 // one output row at a time, every lane producing PX adjacent pixels:
@@ -1590,7 +1617,12 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(96))) void
     float* lut_s = reinterpret_cast<float*>(smem);
     if constexpr (OUT == 1) {
 #pragma unroll
-        for (int k = 0; k < 3; k++) lut_s[tid + k * kThreads] = P.lut[tid + k * kThreads];  // 768 = 3 x kThreads
+        // sections in source channel order (B, G, R): RGB output swaps the B / R output planes instead
+        // of the values (see rsD0 / rsD2), so the per-pixel path carries no swap
+        for (int k = 0; k < 3; k++) {  // 768 = 3 x kThreads
+            const int i = tid + k * kThreads;
+            lut_s[i] = P.lut[P.color_rgb ? 512 - (i & ~255) + (i & 255) : i];
+        }
     }
     const __attribute__((address_space(4))) RoiRec* roi = (const __attribute__((address_space(4))) RoiRec*)(P.recs) + blockIdx.x;
     const int item = roi->item;
@@ -1622,9 +1654,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(96))) void
     const __amdgpu_buffer_rsrc_t rsY = __builtin_amdgcn_make_buffer_rsrc((void*)p0, (short)0, 0x7FFFFFFF, 0x00020000);
     const __amdgpu_buffer_rsrc_t rsC = __builtin_amdgcn_make_buffer_rsrc((void*)(p1 ? p1 : p0), (short)0, 0x7FFFFFFF, 0x00020000);
     const __amdgpu_buffer_rsrc_t rsV = __builtin_amdgcn_make_buffer_rsrc((void*)(p2 ? p2 : p0), (short)0, 0x7FFFFFFF, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rsD0 = __builtin_amdgcn_make_buffer_rsrc((void*)d0, (short)0, 0x7FFFFFFF, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsD0 = __builtin_amdgcn_make_buffer_rsrc((void*)(P.color_rgb ? d2 : d0), (short)0, 0x7FFFFFFF, 0x00020000);
     const __amdgpu_buffer_rsrc_t rsD1 = __builtin_amdgcn_make_buffer_rsrc((void*)d1, (short)0, 0x7FFFFFFF, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rsD2 = __builtin_amdgcn_make_buffer_rsrc((void*)d2, (short)0, 0x7FFFFFFF, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsD2 = __builtin_amdgcn_make_buffer_rsrc((void*)(P.color_rgb ? d0 : d2), (short)0, 0x7FFFFFFF, 0x00020000);
 
     // Prologue order: the row table is built first; group 0's DMA (it needs only the row table and the
     // analytic footprint) goes out before the column table and the per-lane setup are built, so its
@@ -1727,7 +1759,10 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(96))) void
         xt[X] = e;
     }
     __syncthreads();  // column table visible to the per-lane setup
-    const int f0 = P.fill & 0xFF, f1 = (P.fill >> 8) & 0xFF, f2 = (P.fill >> 16) & 0xFF;
+    // fill in source channel order (P.fill is in output plane order); fp32: LUT byte offsets
+    const uint32_t fsh = OUT == 1 ? 2 : 0;
+    const uint32_t fq0 = P.fill & 0xFF, fq1 = (P.fill >> 8) & 0xFF, fq2 = (P.fill >> 16) & 0xFF;
+    const uint32_t f0 = (P.color_rgb ? fq2 : fq0) << fsh, f1 = fq1 << fsh, f2 = (P.color_rgb ? fq0 : fq2) << fsh;
     // Per-lane state for quad steps k < K, identical for every group: row of the quad inside the
     // group; per pixel packed LDS tap offsets (tap 0 low, tap 1 high half) and horizontal weights.
     uint32_t lY[KQ][PX], lC[KQ][PX], wa[KQ][PX];
@@ -1790,7 +1825,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(96))) void
                 sc1 = (ya >> 1) == (yb >> 1) ? sc0 : sc0 + segC;
             }
             const uint32_t wb0 = (uint32_t)e.b0, wb1 = (uint32_t)e.b1;
-            int v[3][PX];
+            uint32_t v[3][PX];  // source channel c (B, G, R); fp32: 4 x value, the LUT byte offset
 #pragma unroll
             for (int j = 0; j < PX; j++) {
                 if (padrow || wa[k][j] == 0) {  // padding row / column
@@ -1810,8 +1845,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(96))) void
                     hrow_sat(sy0[tY0], sy0[tY1], uv_terms_sat(sc0[tC0], sv0[tC0]), uv_terms_sat(sc0[tC1], sv0[tC1]), wp, H0);
                     hrow_sat(sy1[tY0], sy1[tY1], uv_terms_sat(sc1[tC0], sv1[tC0]), uv_terms_sat(sc1[tC1], sv1[tC1]), wp, H1);
 #pragma unroll
-                    for (int ch3 = 0; ch3 < 3; ch3++) v[ch3][j] = vresize(H0[ch3], H1[ch3], wb0, wb1);
-                    if (P.color_rgb) { const int tmp = v[0][j]; v[0][j] = v[2][j]; v[2][j] = tmp; }
+                    for (int ch3 = 0; ch3 < 3; ch3++) v[ch3][j] = vfinal<OUT>(H0[ch3], H1[ch3], wb0, wb1);
                     continue;
                 }
 #endif
@@ -1851,9 +1885,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(96))) void
                 for (int ch3 = 0; ch3 < 3; ch3++) {
                     const uint32_t D0 = __umul24(c[0][ch3], a0) + __umul24(c[1][ch3], a1);
                     const uint32_t D1 = __umul24(c[2][ch3], a0) + __umul24(c[3][ch3], a1);
-                    v[ch3][j] = vresize(D0, D1, wb0, wb1);
+                    v[ch3][j] = vfinal<OUT>(D0, D1, wb0, wb1);
                 }
-                if (P.color_rgb) { const int tmp = v[0][j]; v[0][j] = v[2][j]; v[2][j] = tmp; }
             }
             // soffset 0: the row offset is in voffset (a > 8-byte store with an SGPR soffset misses
             // the compiler's store-data hazard wait on gfx950, see evam_pp_wave)
@@ -1862,9 +1895,10 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(96))) void
                 asm volatile("" :: "v"(v[0][0]), "v"(v[1][0]), "v"(v[2][0]));
                 continue;
             }
-            store_vec<OUT, PX>(rsD0, vo, 0, lut_s, v[0]);
-            store_vec<OUT, PX>(rsD1, vo, 0, lut_s + 256, v[1]);
-            store_vec<OUT, PX>(rsD2, vo, 0, lut_s + 512, v[2]);
+            const uint8_t* lb = reinterpret_cast<const uint8_t*>(lut_s);
+            store_off<OUT, PX>(rsD0, vo, lb, v[0]);
+            store_off<OUT, PX>(rsD1, vo, lb + 1024, v[1]);
+            store_off<OUT, PX>(rsD2, vo, lb + 2048, v[2]);
         }
     };
 
