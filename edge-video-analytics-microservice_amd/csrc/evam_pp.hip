@@ -848,6 +848,8 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_staged(const SParams P) {
         lY0[j] = lY1[j] = lC0[j] = lC1[j] = wa[j] = wp[j] = 0;
     }
     const int ngroups = (rows + R - 1) / R;
+    // letterbox padding columns anywhere in this tile (the per-pixel fill select is skipped otherwise)
+    const bool anypadc = Xv0 > X0 || Xv1 < min(X0 + TW, P.DW) - 1;
 
     // ---- LDS-DMA of group g into buffer `buf` (slot s = plane * 2R + 2 * row + tap) ----
     // Returns the number of VMEM instructions this wave issued (wave-uniform; nY, nC >= 1 whenever
@@ -985,20 +987,32 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_staged(const SParams P) {
                 const uint8_t* sv1 = FMT == kNV12 ? sc1 + 1 : sc1 + 2 * R * SLOT;
                 const UVs tA = uv_terms_sat(sc0[lC0j], sv0[lC0j]);
                 const UVs tB = uv_terms_sat(sc0[lC1j], sv0[lC1j]);
-                // both vertical taps in one chroma row (wave-uniform, ~half the rows of a 2:1 chroma
-                // downscale): its terms are reused instead of read and converted again
-                UVs tC = tA, tD = tB;
-                if (!share) {
-                    tC = uv_terms_sat(sc1[lC0j], sv1[lC0j]);
-                    tD = uv_terms_sat(sc1[lC1j], sv1[lC1j]);
-                }
                 const uint32_t yA = luma_term(sy0[lY0j]), yB = luma_term(sy0[lY1j]);
                 const uint32_t yC = luma_term(sy1[lY0j]), yD = luma_term(sy1[lY1j]);
-                v[0] = vfinal<OUT>(hpass_sat(yA, tA.b, yB, tB.b, wpj), hpass_sat(yC, tC.b, yD, tD.b, wpj), wb0, wb1);
-                v[1] = vfinal<OUT>(hpass_sat(yA, tA.g, yB, tB.g, wpj), hpass_sat(yC, tC.g, yD, tD.g, wpj), wb0, wb1);
-                v[2] = vfinal<OUT>(hpass_sat(yA, tA.r, yB, tB.r, wpj), hpass_sat(yC, tC.r, yD, tD.r, wpj), wb0, wb1);
+                const uint32_t h0[3] = {hpass_sat(yA, tA.b, yB, tB.b, wpj), hpass_sat(yA, tA.g, yB, tB.g, wpj),
+                                        hpass_sat(yA, tA.r, yB, tB.r, wpj)};
+                uint32_t h1[3];
+                // both vertical taps in one chroma row (wave-uniform, ~half the rows of a 2:1 chroma
+                // downscale): its terms are reused instead of read and converted again. The second row's
+                // horizontal pass is written out in both branches, so the shared path carries no copies of
+                // the chroma terms.
+                if (share) {
+                    h1[0] = hpass_sat(yC, tA.b, yD, tB.b, wpj);
+                    h1[1] = hpass_sat(yC, tA.g, yD, tB.g, wpj);
+                    h1[2] = hpass_sat(yC, tA.r, yD, tB.r, wpj);
+                } else {
+                    const UVs tC = uv_terms_sat(sc1[lC0j], sv1[lC0j]);
+                    const UVs tD = uv_terms_sat(sc1[lC1j], sv1[lC1j]);
+                    h1[0] = hpass_sat(yC, tC.b, yD, tD.b, wpj);
+                    h1[1] = hpass_sat(yC, tC.g, yD, tD.g, wpj);
+                    h1[2] = hpass_sat(yC, tC.r, yD, tD.r, wpj);
+                }
 #pragma unroll
-                for (int c = 0; c < 3; c++) v[c] = padc ? fillv[c] : v[c];
+                for (int c = 0; c < 3; c++) v[c] = vfinal<OUT>(h0[c], h1[c], wb0, wb1);
+                if (anypadc) {  // wave-uniform: most launches have no padding column at all (C2, C4, C5)
+#pragma unroll
+                    for (int c = 0; c < 3; c++) v[c] = padc ? fillv[c] : v[c];
+                }
                 put(v);
                 continue;
             }

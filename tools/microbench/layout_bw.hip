@@ -82,7 +82,7 @@ __global__ __launch_bounds__(256) void layout(const uint8_t* __restrict__ src, f
 // rows; it reads the band's touched source row segments (WCOLS * 3.75 bytes each, 16 B per lane), then
 // writes BAND x WCOLS x 3 planes with dword stores (lane = pixel). Loads land in LDS (nothing waits on
 // them), so loads and stores overlap freely: this is the access shape alone.
-template <int WCOLS, int BAND, int MODE>  // MODE 0: loads + stores, 1: loads only, 2: stores only, 3: per-row interleaved
+template <int WCOLS, int BAND, int MODE>  // MODE 0: loads + stores, 1: loads only, 2: stores only, 3: per-row interleaved (4-8: below)
 __global__ __launch_bounds__(256) void shape(const uint8_t* __restrict__ src, float* __restrict__ dst) {
     __shared__ uint4 stage[4][128];
     constexpr int tiles_x = 512 / WCOLS, bands = 512 / BAND, seg = WCOLS * 15 / 4;  // bytes per source segment
@@ -141,6 +141,45 @@ __global__ __launch_bounds__(256) void shape(const uint8_t* __restrict__ src, fl
         }
         return;
     }
+    if (MODE >= 6 && MODE <= 8) {
+        // MODE 5's double-buffered row loop with the staged kernel's two memory choices: 6 = LDS-DMA loads
+        // (buffer_load ... lds, 16 B per lane), 7 = non-temporal stores, 8 = both
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)src, (short)0, 0x7FFFFFFF, 0x00020000);
+        auto loads_dma = [&](int r) {
+            const int oy = band * BAND + r;
+            const int sy = (int)((oy + 0.5) * (1080.0 / 512) - 0.5);
+            if (wave < 3) {
+                const size_t base = (size_t)frame * kFrame +
+                                    (wave < 2 ? (size_t)min(max(sy + wave, 0), kH - 1) * kW
+                                              : (size_t)kW * kH + (size_t)(min(max(sy, 0), kH - 1) >> 1) * kW) +
+                                    (size_t)tx * seg;
+                for (int c0 = 0; c0 < chunks; c0 += 64)
+                    if (c0 + lane < chunks)
+                        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                            rs, (__attribute__((address_space(3))) void*)&stage[wave][c0 & 127], 16, (c0 + lane) * 16,
+                            (int)base, 0, 0);
+            }
+        };
+        auto stores_nt = [&](int r, uint32_t v) {
+            const int oy = band * BAND + r;
+            float* o = dst + (size_t)frame * kDW * kDH * 3 + (size_t)oy * kDW + tx * WCOLS;
+            for (int x = tid; x < WCOLS; x += 256)
+                for (int pl = 0; pl < 3; pl++) {
+                    if (MODE == 6) o[(size_t)pl * kDW * kDH + x] = (float)(v + pl);
+                    else __builtin_nontemporal_store((float)(v + pl), &o[(size_t)pl * kDW * kDH + x]);
+                }
+        };
+        if (MODE == 7) loads(0); else loads_dma(0);
+        for (int r = 0; r < BAND; r++) {
+            if (MODE != 7) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            const uint32_t v = stage[tid >> 6][tid & 63].x;
+            __syncthreads();
+            if (r + 1 < BAND) { if (MODE == 7) loads(r + 1); else loads_dma(r + 1); }
+            stores_nt(r, v);
+        }
+        return;
+    }
     if (MODE != 2) for (int r = 0; r < BAND; r++) loads(r);
     if (MODE != 1) for (int r = 0; r < BAND; r++) stores(r);
 }
@@ -196,5 +235,7 @@ int main() {
     SHAPE(512, 4, 0, alg) SHAPE(512, 4, 1, 96.1e6) SHAPE(512, 4, 2, 100.66e6) SHAPE(512, 4, 3, alg)
     SHAPE(512, 2, 0, alg) SHAPE(512, 2, 3, alg)
     SHAPE(256, 16, 4, alg) SHAPE(256, 16, 5, alg) SHAPE(512, 8, 4, alg) SHAPE(512, 8, 5, alg)
+    SHAPE(256, 16, 6, alg) SHAPE(256, 16, 7, alg) SHAPE(256, 16, 8, alg) SHAPE(256, 16, 5, alg)
+    SHAPE(256, 16, 6, alg) SHAPE(256, 16, 7, alg) SHAPE(256, 16, 8, alg)
     return 0;
 }
