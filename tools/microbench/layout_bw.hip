@@ -141,7 +141,9 @@ __global__ __launch_bounds__(256) void shape(const uint8_t* __restrict__ src, fl
         }
         return;
     }
-    if (MODE >= 6 && MODE <= 8) {
+    if (MODE >= 6 && MODE <= 11) {
+        // 9 / 10 / 11: MODE 8 plus a dependent integer chain of 32 / 64 / 112 VALU per pixel between the
+        // staged value and its stores (the conversion arithmetic's issue slots and latency, no extra bytes)
         // MODE 5's double-buffered row loop with the staged kernel's two memory choices: 6 = LDS-DMA loads
         // (buffer_load ... lds, 16 B per lane), 7 = non-temporal stores, 8 = both
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)src, (short)0, 0x7FFFFFFF, 0x00020000);
@@ -166,16 +168,23 @@ __global__ __launch_bounds__(256) void shape(const uint8_t* __restrict__ src, fl
             for (int x = tid; x < WCOLS; x += 256)
                 for (int pl = 0; pl < 3; pl++) {
                     if (MODE == 6) o[(size_t)pl * kDW * kDH + x] = (float)(v + pl);
+                    else if (MODE >= 9) __builtin_nontemporal_store(__uint_as_float(v + pl), &o[(size_t)pl * kDW * kDH + x]);
                     else __builtin_nontemporal_store((float)(v + pl), &o[(size_t)pl * kDW * kDH + x]);
                 }
         };
+        constexpr int CHAIN = MODE == 9 ? 32 : (MODE == 10 ? 64 : (MODE == 11 ? 112 : 0));
         if (MODE == 7) loads(0); else loads_dma(0);
         for (int r = 0; r < BAND; r++) {
             if (MODE != 7) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
-            const uint32_t v = stage[tid >> 6][tid & 63].x;
+            uint32_t v = stage[tid >> 6][tid & 63].x;
             __syncthreads();
             if (r + 1 < BAND) { if (MODE == 7) loads(r + 1); else loads_dma(r + 1); }
+#pragma unroll
+            for (int k = 0; k < CHAIN; k++) {  // one v_mad_u32_u24 per step, each depending on the previous
+                v = __umul24(v, 0x9E37u) + (uint32_t)k;
+                asm volatile("" : "+v"(v));
+            }
             stores_nt(r, v);
         }
         return;
@@ -237,5 +246,13 @@ int main() {
     SHAPE(256, 16, 4, alg) SHAPE(256, 16, 5, alg) SHAPE(512, 8, 4, alg) SHAPE(512, 8, 5, alg)
     SHAPE(256, 16, 6, alg) SHAPE(256, 16, 7, alg) SHAPE(256, 16, 8, alg) SHAPE(256, 16, 5, alg)
     SHAPE(256, 16, 6, alg) SHAPE(256, 16, 7, alg) SHAPE(256, 16, 8, alg)
+    SHAPE(256, 16, 9, alg) SHAPE(256, 16, 10, alg) SHAPE(256, 16, 11, alg) SHAPE(256, 16, 8, alg)
+    SHAPE(256, 16, 9, alg) SHAPE(256, 16, 10, alg) SHAPE(256, 16, 11, alg)
+    // the same shapes held to 6 resident workgroups per CU (the staged kernel's SGPR-bound occupancy) by
+    // 16 KB of unused dynamic LDS (8 KB static + 16 KB = 24 KB: 160 / 24 -> 6)
+#define SHAPE6(WC, BD, M, B) run("shape " #WC " cols x " #BD " rows mode " #M " @6/CU", [&](int k) { \
+        hipLaunchKernelGGL((shape<WC, BD, M>), dim3(kN * (512 / WC) * (512 / BD)), dim3(256), 16384, 0, src[k], dst[k]); }, B);
+    SHAPE6(256, 16, 8, alg) SHAPE6(256, 16, 11, alg) SHAPE(256, 16, 8, alg) SHAPE(256, 16, 11, alg)
+    SHAPE6(256, 16, 8, alg) SHAPE6(256, 16, 11, alg)
     return 0;
 }
