@@ -57,6 +57,11 @@ constexpr int kThreads = 256;
 #else
 #define EVAM_KERNEL_BOUNDS __launch_bounds__(kThreads)
 #endif
+#ifdef EVAM_PP_STAGED_SGPR
+#define EVAM_STAGED_BOUNDS __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(EVAM_PP_STAGED_SGPR)))
+#else
+#define EVAM_STAGED_BOUNDS EVAM_KERNEL_BOUNDS
+#endif
 constexpr int kLutBytes = 3 * 256 * 4;
 // Cache-policy bits of the output stores: 2 = nt (non-temporal). The outputs are written once and
 // read by nobody in the launch; streaming them past the caches measured 1.5-3 % faster on C2/C3/C4
@@ -759,7 +764,7 @@ __device__ __forceinline__ void vmcnt_at_most(int n) {
 // exact) and waits for group g with vmcnt(operations issued after group g's DMA), so stores and later
 // groups' DMA stay in flight.
 template <int FMT, int OUT, int R, int NSEGX, int NBUF>
-__global__ EVAM_KERNEL_BOUNDS void evam_pp_staged(const SParams P) {
+__global__ EVAM_STAGED_BOUNDS void evam_pp_staged(const SParams P) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     using T = FmtTraits<FMT>;
     constexpr bool kYUV = FMT == kNV12 || FMT == kI420;
@@ -809,9 +814,16 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_staged(const SParams P) {
     const __amdgpu_buffer_rsrc_t rsC = __builtin_amdgcn_make_buffer_rsrc((void*)(p1 ? p1 : p0), (short)0, 0x7FFFFFFF, 0x00020000);
     const __amdgpu_buffer_rsrc_t rsV = __builtin_amdgcn_make_buffer_rsrc((void*)(p2 ? p2 : p0), (short)0, 0x7FFFFFFF, 0x00020000);
     // plane of source channel 0 / 2 (B / R): swapped for RGB order
+#ifdef EVAM_PP_ONE_DST
+    // one resource for the item's three output planes; the plane offset rides in soffset
+    const __amdgpu_buffer_rsrc_t rsD = __builtin_amdgcn_make_buffer_rsrc((void*)d0, (short)0, 0x7FFFFFFF, 0x00020000);
+    const int pbytes = (int)(plane * esz);
+    const int po0 = P.color_rgb ? 2 * pbytes : 0, po2 = P.color_rgb ? 0 : 2 * pbytes;
+#else
     const __amdgpu_buffer_rsrc_t rsD0 = __builtin_amdgcn_make_buffer_rsrc((void*)(P.color_rgb ? d2 : d0), (short)0, 0x7FFFFFFF, 0x00020000);
     const __amdgpu_buffer_rsrc_t rsD1 = __builtin_amdgcn_make_buffer_rsrc((void*)d1, (short)0, 0x7FFFFFFF, 0x00020000);
     const __amdgpu_buffer_rsrc_t rsD2 = __builtin_amdgcn_make_buffer_rsrc((void*)(P.color_rgb ? d0 : d2), (short)0, 0x7FFFFFFF, 0x00020000);
+#endif
 
     float* lut_s = reinterpret_cast<float*>(smem);
     // fill in source channel order (P.fill is in output plane order); fp32: LUT byte offsets
@@ -956,13 +968,25 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_staged(const SParams P) {
                 if (!xin[j]) return;  // lane 0 is in: the wave still issues all three stores
                 if constexpr (OUT == 1) {
                     const uint8_t* lb = reinterpret_cast<const uint8_t*>(lut_s);
+#ifdef EVAM_PP_ONE_DST
+                    __builtin_amdgcn_raw_buffer_store_b32(*reinterpret_cast<const uint32_t*>(lb + v[0]), rsD, xo[j], sO + po0, EVAM_PP_STORE_AUX);
+                    __builtin_amdgcn_raw_buffer_store_b32(*reinterpret_cast<const uint32_t*>(lb + 1024 + v[1]), rsD, xo[j], sO + pbytes, EVAM_PP_STORE_AUX);
+                    __builtin_amdgcn_raw_buffer_store_b32(*reinterpret_cast<const uint32_t*>(lb + 2048 + v[2]), rsD, xo[j], sO + po2, EVAM_PP_STORE_AUX);
+#else
                     __builtin_amdgcn_raw_buffer_store_b32(*reinterpret_cast<const uint32_t*>(lb + v[0]), rsD0, xo[j], sO, EVAM_PP_STORE_AUX);
                     __builtin_amdgcn_raw_buffer_store_b32(*reinterpret_cast<const uint32_t*>(lb + 1024 + v[1]), rsD1, xo[j], sO, EVAM_PP_STORE_AUX);
                     __builtin_amdgcn_raw_buffer_store_b32(*reinterpret_cast<const uint32_t*>(lb + 2048 + v[2]), rsD2, xo[j], sO, EVAM_PP_STORE_AUX);
+#endif
                 } else {
+#ifdef EVAM_PP_ONE_DST
+                    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v[0], rsD, xo[j], sO + po0, EVAM_PP_STORE_AUX);
+                    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v[1], rsD, xo[j], sO + pbytes, EVAM_PP_STORE_AUX);
+                    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v[2], rsD, xo[j], sO + po2, EVAM_PP_STORE_AUX);
+#else
                     __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v[0], rsD0, xo[j], sO, EVAM_PP_STORE_AUX);
                     __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v[1], rsD1, xo[j], sO, EVAM_PP_STORE_AUX);
                     __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v[2], rsD2, xo[j], sO, EVAM_PP_STORE_AUX);
+#endif
                 }
             };
             if ((b0 | b1) == 0 || (P.ablate & 2)) {  // padding row (wave-uniform)
@@ -1615,7 +1639,7 @@ __device__ __forceinline__ void wait_vmcnt_stores(int nk) {
 // 7 resident workgroups per CU need <= 96 SGPRs (800 / (96 + 16)); the occupancy API does not count
 // SGPRs (MI355X_MICROARCH.md, Residency): uncapped, the kernel's ~106 allowed only 6 and a 1,600-ROI
 // batch ran a second round (profiles/r02r_c3_roi_timeline_before.json).
-template <int FMT, int OUT, int PX>
+template <int FMT, int OUT, int PX, int NB>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(96))) void evam_pp_roi(const QParams P) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     using T = FmtTraits<FMT>;
@@ -1725,8 +1749,11 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(96))) void
     const uint32_t mC = nC > 1 ? (uint32_t)((0x100000000ull + nC - 1) / nC) : 0u;
     __syncthreads();  // row table (and on the first unit the LUT) visible
     // One plane region of group grp: chunk q -> (segment, chunk) -> (row, tap) -> source offset.
-    auto issue_plane = [&](int grp, uint8_t* base, int nr, int n, uint32_t m, int pl) {
+    // Returns the number of DMA instructions this wave issued (wave-uniform: an instruction with no active
+    // lane is skipped), for the counted waits of the three-buffer pipeline.
+    auto issue_plane = [&](int grp, uint8_t* base, int nr, int n, uint32_t m, int pl) -> int {
         const int nq = 2 * nr * n;
+        int cnt = 0;
         for (int q0 = wave * 64; q0 < nq; q0 += 4 * 64) {
             const int q = q0 + lane;
             const int seg = n > 1 ? (int)__umulhi((uint32_t)q, m) : q;
@@ -1737,6 +1764,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(96))) void
             bool on = q < nq && (e.b0 | e.b1) != 0;           // padding rows stage nothing
             if (pl > 0) on = on && !(tap && (ya >> 1) == (yb >> 1));  // chroma row shared by both taps
             __attribute__((address_space(3))) void* dstl = (__attribute__((address_space(3))) void*)(base + q0 * 16);
+            if constexpr (NB == 3) cnt += __builtin_amdgcn_ballot_w64(on) != 0 ? 1 : 0;
             if (on) {
                 const int yr = tap ? yb : ya;
                 if (pl == 0)
@@ -1747,16 +1775,19 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(96))) void
                     __builtin_amdgcn_raw_ptr_buffer_load_lds(rsV, dstl, 16, (yr >> 1) * pitch2 + fsC + c * 16, 0, EVAM_PP_LOAD_AUX, 0);
             }
         }
+        return cnt;
     };
-    auto issue = [&](int grp, uint8_t* buf) {
-        if (nY == 0 || (P.ablate & 16)) return;  // no visible columns: every pixel is fill
+    auto issue = [&](int grp, uint8_t* buf) -> int {
+        if (nY == 0 || (P.ablate & 16)) return 0;  // no visible columns: every pixel is fill
         const int nr = min(R, rows - grp * R);
-        issue_plane(grp, buf, nr, nY, mY, 0);
-        if constexpr (NP >= 2) issue_plane(grp, buf + offC, nr, nC, mC, 1);
-        if constexpr (NP >= 3) issue_plane(grp, buf + offC + 2 * R * segC, nr, nC, mC, 2);
+        int cnt = issue_plane(grp, buf, nr, nY, mY, 0);
+        if constexpr (NP >= 2) cnt += issue_plane(grp, buf + offC, nr, nC, mC, 1);
+        if constexpr (NP >= 3) cnt += issue_plane(grp, buf + offC + 2 * R * segC, nr, nC, mC, 2);
+        return __builtin_amdgcn_readfirstlane(cnt);
     };
     uint8_t* const buf0 = smem + P.offBuf;
     uint8_t* const buf1 = buf0 + P.buf_bytes;
+    uint8_t* const buf2 = buf1 + P.buf_bytes;  // NB == 3 only
     issue(0, buf0);
     for (int X = tid; X < DW; X += kThreads) {
         XTab e;
@@ -1917,6 +1948,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(96))) void
     };
 
 
+    if constexpr (NB == 2) {
     for (int grp = 0; grp < ngroups; grp++) {
         // Wait for this wave's share of group grp's DMA. Group grp-1 was full (only the last group can
         // be partial), so this wave issued at least 3 stores for each of its nk_w store steps after
@@ -1929,6 +1961,27 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(96))) void
         asm volatile("" ::: "memory");  // the next group's DMA stays ahead of this group's stores
         compute(grp, (grp & 1) ? buf1 : buf0);
         asm volatile("" ::: "memory");
+    }
+    } else {
+    // Three buffers: two groups of DMA in flight while one is converted (the widest crops walk ~15 groups
+    // of ~2.4 us DMA round trips under load with two buffers). In issue order, after group grp's DMA this
+    // wave issued: group grp-2's stores (grp >= 2), group grp+1's DMA (nd_ahead instructions), group
+    // grp-1's stores; groups before the last are full, so each store step counts 3.
+    int nd_ahead = ngroups > 1 ? issue(1, buf1) : 0;
+    uint8_t* bc = buf0;  // buffer of group grp
+    uint8_t* bn = buf2;  // buffer of group grp + 2
+    for (int grp = 0; grp < ngroups; grp++) {
+        vmcnt_at_most(nd_ahead + (grp >= 1 ? 3 * nk_w : 0) + (grp >= 2 ? 3 * nk_w : 0));
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();  // every wave's DMA for grp landed; every wave done reading grp-1
+        nd_ahead = grp + 2 < ngroups ? issue(grp + 2, bn) : 0;
+        asm volatile("" ::: "memory");  // later groups' DMA stays ahead of this group's stores
+        compute(grp, bc);
+        asm volatile("" ::: "memory");
+        uint8_t* const t = bc;  // rotate: grp+1 -> current, grp (read by now) -> grp+3's slot
+        bc = bc == buf0 ? buf1 : (bc == buf1 ? buf2 : buf0);
+        bn = t;
+    }
     }
     EVAM_STAMP(3);
 }
@@ -2011,6 +2064,7 @@ struct Knobs {
     int wth = -1, px = 0, reuse = 1, wave_lds = 40 * 1024;
     int roi_th = -1, roi_buf = -1, roi_px = 1, roi_sort = 1, roi_xcd = 0;  // roi_buf -1: sized for one round
     int roi_unit = 0;                              // ROI work-unit size in row groups (0: one unit per base tile)
+    int roi_nbuf = 2;                              // ROI staging buffers (3: two groups of DMA in flight)
     int ablate = 0;                                // stage-removal diagnostics (results invalid)
     void read() {
         staged = env_int("EVAM_PP_STAGED", staged); wave = env_int("EVAM_PP_WAVE", wave);
@@ -2023,6 +2077,7 @@ struct Knobs {
         roi_th = env_int("EVAM_PP_ROI_TH", roi_th); roi_buf = env_int("EVAM_PP_ROI_BUF", roi_buf);
         roi_px = env_int("EVAM_PP_ROI_PX", roi_px); roi_sort = env_int("EVAM_PP_ROI_SORT", roi_sort);
         roi_xcd = env_int("EVAM_PP_ROI_XCD", roi_xcd); roi_unit = env_int("EVAM_PP_ROI_UNIT", roi_unit);
+        roi_nbuf = env_int("EVAM_PP_ROI_NBUF", roi_nbuf);
         ablate = env_int("EVAM_PP_ABLATE", ablate);
     }
 };
@@ -2175,35 +2230,37 @@ hipError_t launch(int f, int out, const KParams& p, int grid, int lds, hipStream
     }
 }
 
-template <int FMT, int OUT, int PX>
+template <int FMT, int OUT, int PX, int NB>
 hipError_t launch_roi_px(const QParams& p, int grid, int lds, hipStream_t s) {
     if (lds > 64 * 1024) {
-        hipError_t e = hipFuncSetAttribute((const void*)evam_pp_roi<FMT, OUT, PX>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        hipError_t e = hipFuncSetAttribute((const void*)evam_pp_roi<FMT, OUT, PX, NB>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL((evam_pp_roi<FMT, OUT, PX>), dim3(grid), dim3(kThreads), lds, s, p);
+    hipLaunchKernelGGL((evam_pp_roi<FMT, OUT, PX, NB>), dim3(grid), dim3(kThreads), lds, s, p);
     return hipGetLastError();
 }
 
 // PX = 1 (adjacent lanes, adjacent pixels) by default. PX = 4 (one dwordx4 store per channel and
 // one row setup per 4 pixels; EVAM_PP_ROI_PX=4) measured 8 % slower on C3: lanes 4 pixels apart
 // spread their LDS tap reads over 4x more dwords, so the byte reads bank-conflict.
+// NB = 3 staging buffers (EVAM_PP_ROI_NBUF=3): two groups of DMA in flight, PX = 1 only.
 template <int FMT, int OUT>
-hipError_t launch_roi_t(int px, const QParams& p, int grid, int lds, hipStream_t s) {
-    if (px == 4 && p.DW % 4 == 0) return launch_roi_px<FMT, OUT, 4>(p, grid, lds, s);
-    return launch_roi_px<FMT, OUT, 1>(p, grid, lds, s);
+hipError_t launch_roi_t(int px, int nb, const QParams& p, int grid, int lds, hipStream_t s) {
+    if (px == 4 && p.DW % 4 == 0) return launch_roi_px<FMT, OUT, 4, 2>(p, grid, lds, s);
+    if (nb == 3) return launch_roi_px<FMT, OUT, 1, 3>(p, grid, lds, s);
+    return launch_roi_px<FMT, OUT, 1, 2>(p, grid, lds, s);
 }
 
-hipError_t launch_roi(int f, int out, int px, const QParams& p, int grid, int lds, hipStream_t s) {
+hipError_t launch_roi(int f, int out, int px, int nb, const QParams& p, int grid, int lds, hipStream_t s) {
     switch (f * 2 + out) {
-    case kNV12 * 2 + 0: return launch_roi_t<kNV12, 0>(px, p, grid, lds, s);
-    case kNV12 * 2 + 1: return launch_roi_t<kNV12, 1>(px, p, grid, lds, s);
-    case kI420 * 2 + 0: return launch_roi_t<kI420, 0>(px, p, grid, lds, s);
-    case kI420 * 2 + 1: return launch_roi_t<kI420, 1>(px, p, grid, lds, s);
-    case kBGRX * 2 + 0: return launch_roi_t<kBGRX, 0>(px, p, grid, lds, s);
-    case kBGRX * 2 + 1: return launch_roi_t<kBGRX, 1>(px, p, grid, lds, s);
-    case kBGR * 2 + 0: return launch_roi_t<kBGR, 0>(px, p, grid, lds, s);
-    default: return launch_roi_t<kBGR, 1>(px, p, grid, lds, s);
+    case kNV12 * 2 + 0: return launch_roi_t<kNV12, 0>(px, nb, p, grid, lds, s);
+    case kNV12 * 2 + 1: return launch_roi_t<kNV12, 1>(px, nb, p, grid, lds, s);
+    case kI420 * 2 + 0: return launch_roi_t<kI420, 0>(px, nb, p, grid, lds, s);
+    case kI420 * 2 + 1: return launch_roi_t<kI420, 1>(px, nb, p, grid, lds, s);
+    case kBGRX * 2 + 0: return launch_roi_t<kBGRX, 0>(px, nb, p, grid, lds, s);
+    case kBGRX * 2 + 1: return launch_roi_t<kBGRX, 1>(px, nb, p, grid, lds, s);
+    case kBGR * 2 + 0: return launch_roi_t<kBGR, 0>(px, nb, p, grid, lds, s);
+    default: return launch_roi_t<kBGR, 1>(px, nb, p, grid, lds, s);
     }
 }
 
@@ -2336,19 +2393,20 @@ bool plan_wave(int f, const Geom& g, int DW, int DH, int count, int out_dtype, i
 }
 
 template <int FMT, int OUT>
-const void* roi_fn_t(int px) {
-    return px == 4 ? (const void*)evam_pp_roi<FMT, OUT, 4> : (const void*)evam_pp_roi<FMT, OUT, 1>;
+const void* roi_fn_t(int px, int nb) {
+    return px == 4 ? (const void*)evam_pp_roi<FMT, OUT, 4, 2>
+                   : (nb == 3 ? (const void*)evam_pp_roi<FMT, OUT, 1, 3> : (const void*)evam_pp_roi<FMT, OUT, 1, 2>);
 }
-const void* roi_fn(int f, int out, int px) {
+const void* roi_fn(int f, int out, int px, int nb) {
     switch (f * 2 + out) {
-    case kNV12 * 2 + 0: return roi_fn_t<kNV12, 0>(px);
-    case kNV12 * 2 + 1: return roi_fn_t<kNV12, 1>(px);
-    case kI420 * 2 + 0: return roi_fn_t<kI420, 0>(px);
-    case kI420 * 2 + 1: return roi_fn_t<kI420, 1>(px);
-    case kBGRX * 2 + 0: return roi_fn_t<kBGRX, 0>(px);
-    case kBGRX * 2 + 1: return roi_fn_t<kBGRX, 1>(px);
-    case kBGR * 2 + 0: return roi_fn_t<kBGR, 0>(px);
-    default: return roi_fn_t<kBGR, 1>(px);
+    case kNV12 * 2 + 0: return roi_fn_t<kNV12, 0>(px, nb);
+    case kNV12 * 2 + 1: return roi_fn_t<kNV12, 1>(px, nb);
+    case kI420 * 2 + 0: return roi_fn_t<kI420, 0>(px, nb);
+    case kI420 * 2 + 1: return roi_fn_t<kI420, 1>(px, nb);
+    case kBGRX * 2 + 0: return roi_fn_t<kBGRX, 0>(px, nb);
+    case kBGRX * 2 + 1: return roi_fn_t<kBGRX, 1>(px, nb);
+    case kBGR * 2 + 0: return roi_fn_t<kBGR, 0>(px, nb);
+    default: return roi_fn_t<kBGR, 1>(px, nb);
     }
 }
 
@@ -2377,16 +2435,18 @@ bool plan_roi(int f, int DW, int DH, int out_dtype, int px, int max_row_bytes, i
     q.offBuf = q.offYT + (int)sizeof(YTab) * q.TH;
     const int64_t grid = (int64_t)count * base_tiles;
     const int per_cu = (int)std::max<int64_t>(1, std::min<int64_t>(kRoiWavesPerSimd, (grid + n_cu - 1) / n_cu));
+    const int pxv = px == 4 && DW % 4 == 0 ? 4 : 1;
+    const int nb = pxv == 1 && kn.roi_nbuf == 3 ? 3 : 2;
     int buf = kn.roi_buf;
-    if (buf <= 0) buf = std::min(12 * 1024, ((((160 * 1024) / per_cu) & ~1023) - q.offBuf) / 2 & ~15);
+    if (buf <= 0) buf = std::min(12 * 1024, ((((160 * 1024) / per_cu) & ~1023) - q.offBuf) / nb & ~15);
     q.buf_bytes = (std::max(buf, max_row_bytes) + 15) & ~15;
-    lds = q.offBuf + 2 * q.buf_bytes;
+    lds = q.offBuf + nb * q.buf_bytes;
     if (q.buf_bytes > 32 * 1024 || lds > 160 * 1024) return false;
-    const void* fn = roi_fn(f, out_dtype, px == 4 && DW % 4 == 0 ? 4 : 1);
+    const void* fn = roi_fn(f, out_dtype, pxv, nb);
     int res = resident_per_cu(fn, lds);
     while (kn.roi_buf <= 0 && res < per_cu && q.buf_bytes - 512 >= max_row_bytes) {
         q.buf_bytes -= 512;
-        lds -= 1024;
+        lds -= 512 * nb;
         res = resident_per_cu(fn, lds);
     }
     slots = (int64_t)n_cu * res;
@@ -3008,7 +3068,7 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
             q.ablate = kn.ablate;
             const int64_t grid = qrec[f];
             if (grid > 0x7FFFFFFF) return fail(EVAM_PP_ERR_INVALID_ARG, "evam_pp_run: too many tiles");
-            hipError_t e = launch_roi(f, cfg->out_dtype, kn.roi_px, q, (int)grid, qlds[f], h->stream);
+            hipError_t e = launch_roi(f, cfg->out_dtype, kn.roi_px, kn.roi_nbuf, q, (int)grid, qlds[f], h->stream);
             if (e != hipSuccess) return fail(EVAM_PP_ERR_HIP, "kernel launch failed: %s", hipGetErrorString(e));
             launches++;
             continue;

@@ -581,3 +581,29 @@ def test_roi_work_units(evam, O, coracle, gpu, unit, monkeypatch):
                      rois=[evam.Roi(*r) for r in rois])
     ref, _ = run_oracle(O, coracle, frames, shape, "f32", info, rois=rois)
     assert_same(got, ref, f"roi units {unit}")
+
+
+@pytest.mark.parametrize("fmt", FORMATS)
+@pytest.mark.parametrize("buf", ["0", "1024", "3072"])
+def test_roi_kernel_three_buffers(evam, O, coracle, gpu, fmt, buf, monkeypatch):
+    """ROI kernel with three staging buffers (EVAM_PP_ROI_NBUF=3: two groups of DMA in flight, counted
+    vmcnt waits). Small forced buffers (EVAM_PP_ROI_BUF) make every crop walk many row groups, so each
+    wait level of the pipeline (first group, second, steady state, last partial group) is exercised."""
+    import torch
+
+    monkeypatch.setenv("EVAM_PP_ROI_NBUF", "3")
+    if buf != "0":
+        monkeypatch.setenv("EVAM_PP_ROI_BUF", buf)
+    rng = np.random.default_rng(zlib.crc32(f"nb3{fmt}{buf}".encode()))
+    W, H = 400, 240
+    frames = [O.random_frame(rng, fc(O, fmt), W, H, pattern="gradient" if i else "uniform") for i in range(3)]
+    rois = [(int(rng.integers(0, 3)), int(rng.integers(-6, W - 8)), int(rng.integers(-6, H - 8)),
+             int(rng.integers(6, 390)), int(rng.integers(6, 230))) for _ in range(37)]
+    for dst, info in (((72, 72), evam.PreProcInfo(range=(0.0, 1.0), mean=(0.1, 0.2, 0.3), std=(0.3, 0.2, 0.1))),
+                      ((64, 40), evam.PreProcInfo(resize="aspect-ratio", placement="center", color_space="RGB",
+                                                  fill=(7, 8, 9), range=(0.0, 1.0)))):
+        shape = (len(rois), 3, dst[1], dst[0])
+        got, _ = run_hip(evam, torch, upload(evam, frames, gpu), shape, torch.float32, info,
+                         rois=[evam.Roi(*r) for r in rois])
+        ref, _ = run_oracle(O, coracle, frames, shape, "f32", info, rois=rois)
+        assert_same(got, ref, f"roi 3 buffers {fmt} buf={buf} dst={dst}")
