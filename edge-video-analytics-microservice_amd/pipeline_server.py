@@ -38,7 +38,9 @@ device ``Image``s, or host planes uploaded on arrival.
 from __future__ import annotations
 
 import gc
+import itertools
 import json
+import operator
 import os
 import queue
 import re
@@ -53,6 +55,7 @@ from . import postproc as P
 from ._native import PreProcError
 from .preproc import Image
 
+_WIDTH, _HEIGHT = operator.attrgetter("width"), operator.attrgetter("height")
 INFERENCE_ELEMENTS = ("gvadetect", "gvaclassify", "gvaactionrecognitionbin", "gvainference")
 HIP_BACKENDS = ("hip",)
 # backends DL Streamer 2022.1 accepts that only the reference implements
@@ -487,7 +490,7 @@ class DeviceRunner:
                     p._fail(e)
                     done.append(p)
                     continue
-                n = len(p._pend)
+                n = len(p._pend) - p._head
                 if p._stop.is_set() or (p._eos and not n):
                     p._end()
                     done.append(p)
@@ -508,11 +511,14 @@ class DeviceRunner:
             share = max(1, hub.max_batch // len(ready))
             work = []
             for p in ready:
+                n = len(p._pend) - p._head
                 k = max(p._batch, share // p._batch * p._batch)
-                if not p._eos:
-                    k = min(k, len(p._pend) // p._batch * p._batch)
-                work.append((p, p._pend[:k]))
-                del p._pend[:k]
+                k = min(k, n) if p._eos else min(k, n // p._batch * p._batch)
+                work.append((p, p._pend[p._head:p._head + k]))
+                p._head += k  # a read index, not del [:k]: a stream's backlog is taken in O(k) per tick
+                if p._head >= 4096 and 2 * p._head >= len(p._pend):
+                    del p._pend[:p._head]
+                    p._head = 0
                 p._pend_t0 = time.perf_counter()
             self._tick(work)
 
@@ -612,7 +618,14 @@ class _InferenceStage:
         self.finish(work)
 
     def hub_key(self):
-        """Stages with equal keys are interchangeable: their requests run as one batch."""
+        """Stages with equal keys are interchangeable: their requests run as one batch (computed once: the
+        element's model, pre-processing and properties are fixed for the pipeline's life)."""
+        k = self.__dict__.get("_hub_key")
+        if k is None:
+            k = self._hub_key = self._make_hub_key()
+        return k
+
+    def _make_hub_key(self):
         return (self.el.factory, id(self.model), self.info.cache_key(self.out_dtype()), self.threshold)
 
     def pp(self):
@@ -675,9 +688,9 @@ class ClassifyStage(_InferenceStage):
         self.reclassify = max(1, int(el.properties.get("reclassify-interval", 1)))
         self._cache: dict = {}   # object_id -> (frame index classified at, tensors)
 
-    def hub_key(self):
+    def _make_hub_key(self):
         oc = tuple(sorted(self.object_class)) if self.object_class else None
-        return super().hub_key() + (oc,)
+        return super()._make_hub_key() + (oc,)
 
     def prepare(self, items):
         work = []          # (frame_index, Image, [regions to classify])
@@ -826,6 +839,7 @@ class Pipeline:
         self._stop = threading.Event()
         # device-runner state (DeviceRunner): frames ingested and not yet run, end of stream, completion
         self._pend: list = []
+        self._head = 0  # frames before it are taken
         self._pend_t0 = 0.0
         self._eos = False
         self._batch = 1
@@ -904,16 +918,23 @@ class Pipeline:
                                                   "'application' source of decoded frames")
         if not got:
             return
-        if any(x is None for x in got):     # end of stream
+        types = set(map(type, got))  # C-level scan (Image.__eq__ would run per item for `None in got`)
+        if type(None) in types:      # end of stream
             got = got[:next(i for i, x in enumerate(got) if x is None)]
             self._eos = True
+            types = set(map(type, got))
         if not got:
             return
-        if not self._pend:
+        if len(self._pend) == self._head:
+            self._pend.clear()
+            self._head = 0
             self._pend_t0 = time.perf_counter()
         base, uri, FR = self.frames, self.source.get("uri"), P.FrameResult
-        if all(type(x) is Image for x in got):
-            self._pend.extend([(base + k, im, FR(im.width, im.height, base + k, uri)) for k, im in enumerate(got)])
+        if types == {Image}:
+            n = len(got)
+            idx = range(base, base + n)
+            frs = map(FR, map(_WIDTH, got), map(_HEIGHT, got), idx, itertools.repeat(uri, n))
+            self._pend.extend(zip(idx, got, frs))
         else:
             for k, item in enumerate(got):
                 img = self._as_image(item)
