@@ -284,7 +284,7 @@ def main():
                          "pipelines, one per stream, batched across streams by the per-device hub); reported "
                          "as its own line next to the direct kernel rate")
     ap.add_argument("--streams", type=int, default=32, help="--via pipeline: pipelines (streams)")
-    ap.add_argument("--frames-per-stream", type=int, default=8192, help="--via pipeline: frames per stream")
+    ap.add_argument("--frames-per-stream", type=int, default=16384, help="--via pipeline: frames per stream")
     ap.add_argument("--stream-batch", type=int, default=16, help="--via pipeline: gvadetect batch-size per stream")
     ap.add_argument("--hub-batch", type=int, default=256, help="--via pipeline: max frames per hub launch")
     ap.add_argument("--runner", choices=["device", "threads"], default="device",

@@ -822,6 +822,7 @@ class Pipeline:
     """One pipeline instance (``PipelineServer.pipeline(name, version)``)."""
 
     QUEUED, RUNNING, COMPLETED, ERROR, ABORTED = "QUEUED", "RUNNING", "COMPLETED", "ERROR", "ABORTED"
+    kIngest = 1024  # device runner: most frames of one stream ingested and not yet run
 
     def __init__(self, server: "_Server", definition: PipelineDefinition, instance_id: int):
         self.server = server
@@ -897,22 +898,36 @@ class Pipeline:
             return
         src = self.source
         kind = src.get("type")
+        # At most kIngest frames ahead of the runner per stream: the rest stays in the application's queue
+        # (bounded buffering; a backlog of hundreds of thousands of live records made the collector's
+        # full passes grow with it).
+        backlog = len(self._pend) - self._head
+        if backlog > self.kIngest // 4:  # refill in large steps, not a few frames per tick
+            return
+        room = self.kIngest - backlog
         if kind == "application":
             q = src.get("input")
             if isinstance(q, queue.Queue):
                 with q.mutex:
-                    got = list(q.queue)
-                    q.queue.clear()
+                    d = q.queue
+                    if len(d) <= room:
+                        got = list(d)
+                        d.clear()
+                    else:
+                        got = [d.popleft() for _ in range(room)]
                     q.not_full.notify_all()
             else:
                 got = []
-                while True:
+                while len(got) < room:
                     try:
                         got.append(q.get_nowait())
                     except queue.Empty:
                         break
         elif kind == "frames":
-            got = list(src.get("frames", [])) + [None]
+            frames = src.get("frames", [])
+            got = list(frames[self.frames:self.frames + room])
+            if self.frames + len(got) >= len(frames):
+                got.append(None)
         else:
             raise PreProcError(N.ERR_UNSUPPORTED, f"source type {kind!r}: decode is upstream of this build; use an "
                                                   "'application' source of decoded frames")
@@ -1102,6 +1117,11 @@ class _Server:
                     # the runner makes a few short-lived objects per frame, and every young collection that
                     # escalated would otherwise rescan it (2x the per-frame cost at 32 streams).
                     gc.freeze()
+                gct = self.options.get("gc_threshold", (20000, 100, 1000))
+                if gct:
+                    # Per-frame records die by reference count, never in cycles; collecting them every 700
+                    # allocations (the default) cost as much as the rest of the runner at 32 streams.
+                    gc.set_threshold(*gct)
                 self._runner = DeviceRunner(hub)
             return self._runner
 
