@@ -1568,6 +1568,11 @@ static_assert(sizeof(RoiRec) == 64, "RoiRec layout");
 #define EVAM_PP_ROI_K 6
 #endif
 constexpr int kRoiK = EVAM_PP_ROI_K;  // max pixels per lane per row group in the ROI kernel
+#ifdef EVAM_PP_ROI_ALU_NORM
+constexpr bool kRoiAluNorm = true;    // fp32 normalisation in the ALU (PX 1), no LDS LUT
+#else
+constexpr bool kRoiAluNorm = false;
+#endif
 
 struct QParams {
     const RoiRec* recs;       // this launch's ROI tiles in launch order (largest work first)
@@ -1583,6 +1588,10 @@ struct QParams {
     uint32_t fill;
     int ablate;               // diagnostics only (EVAM_PP_ABLATE bits): 2 no pixel math, 4 no stores, 16 no DMA,
                               // 32 stop after setup, 64 stop after geometry, 128 return at entry
+    // EVAM_PP_ROI_ALU_NORM builds: the normalisation in the reference operation order, per SOURCE channel
+    // (B, G, R; swapped for RGB like the planes), instead of the LDS LUT
+    float na, nb, nm[3], ns[3];
+    int nflags;
 };
 
 // Diagnostic builds only (-DEVAM_PP_TRACE, tools/roi_timeline.py): per-workgroup timestamps of the
@@ -1653,7 +1662,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(96))) void
     EVAM_STAMP(0);
     // The LUT is loaded once per workgroup, whatever number of units it processes.
     float* lut_s = reinterpret_cast<float*>(smem);
-    if constexpr (OUT == 1) {
+    if constexpr (OUT == 1 && !(kRoiAluNorm && PX == 1)) {
 #pragma unroll
         // sections in source channel order (B, G, R): RGB output swaps the B / R output planes instead
         // of the values (see rsD0 / rsD2), so the per-pixel path carries no swap
@@ -1938,6 +1947,18 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(96))) void
             const uint32_t vo = (gbase + (uint32_t)(tid + k * kThreads) * PX) * (uint32_t)esz;
             if (P.ablate & 4) {
                 asm volatile("" :: "v"(v[0][0]), "v"(v[1][0]), "v"(v[2][0]));
+                continue;
+            }
+            if constexpr (kRoiAluNorm && OUT == 1 && PX == 1) {  // (the PX 4 variant keeps the LUT)
+                auto nrm = [&](uint32_t v4, int c) -> uint32_t {
+                    float x = (float)(v4 >> 2);
+                    if (P.nflags & 1) { x = __fmul_rn(x, P.na); x = __fadd_rn(x, P.nb); }
+                    if (P.nflags & 2) { x = __fsub_rn(x, P.nm[c]); x = __fdiv_rn(x, P.ns[c]); }
+                    return __float_as_uint(x);
+                };
+                __builtin_amdgcn_raw_buffer_store_b32(nrm(v[0][0], 0), rsD0, vo, 0, EVAM_PP_STORE_AUX);
+                __builtin_amdgcn_raw_buffer_store_b32(nrm(v[1][0], 1), rsD1, vo, 0, EVAM_PP_STORE_AUX);
+                __builtin_amdgcn_raw_buffer_store_b32(nrm(v[2][0], 2), rsD2, vo, 0, EVAM_PP_STORE_AUX);
                 continue;
             }
             const uint8_t* lb = reinterpret_cast<const uint8_t*>(lut_s);
@@ -2430,7 +2451,7 @@ bool plan_roi(int f, int DW, int DH, int out_dtype, int px, int max_row_bytes, i
     q.TH = (int64_t)DW * DH <= 32768 ? DH : std::max(8, std::min(DH, 16384 / DW));
     if (kn.roi_th > 0) q.TH = std::max(1, std::min(DH, kn.roi_th));
     base_tiles = (DH + q.TH - 1) / q.TH;
-    q.offXT = out_dtype == EVAM_DTYPE_F32 ? kLutBytes : 0;
+    q.offXT = out_dtype == EVAM_DTYPE_F32 && !(kRoiAluNorm && !(px == 4 && DW % 4 == 0)) ? kLutBytes : 0;
     q.offYT = q.offXT + (int)sizeof(XTab) * DW;
     q.offBuf = q.offYT + (int)sizeof(YTab) * q.TH;
     const int64_t grid = (int64_t)count * base_tiles;
@@ -3066,6 +3087,14 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
             q.color_rgb = color_rgb;
             q.fill = fill;
             q.ablate = kn.ablate;
+            q.na = (float)(((double)cfg->range[1] - (double)cfg->range[0]) / 255.0);
+            q.nb = cfg->range[0];
+            for (int c = 0; c < 3; c++) {
+                const int oc = color_rgb ? 2 - c : c;  // source channel c lands in output plane oc
+                q.nm[c] = cfg->mean[oc];
+                q.ns[c] = cfg->std[oc];
+            }
+            q.nflags = cfg->norm_flags;
             const int64_t grid = qrec[f];
             if (grid > 0x7FFFFFFF) return fail(EVAM_PP_ERR_INVALID_ARG, "evam_pp_run: too many tiles");
             hipError_t e = launch_roi(f, cfg->out_dtype, kn.roi_px, kn.roi_nbuf, q, (int)grid, qlds[f], h->stream);
