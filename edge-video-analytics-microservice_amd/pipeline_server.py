@@ -1094,6 +1094,7 @@ class _Server:
         self.device = 0
         self._hub = None
         self._runner = None
+        self._gc_saved = None
         self._hub_lock = threading.Lock()
 
     def hub(self) -> BatchHub:
@@ -1112,11 +1113,13 @@ class _Server:
         hub = self.hub()
         with self._hub_lock:
             if self._runner is None:
+                self._gc_saved = (gc.get_threshold(), False)
                 if self.options.get("gc_freeze", True):
                     # The heap built so far (torch, models, templates) leaves the collector's generations:
                     # the runner makes a few short-lived objects per frame, and every young collection that
                     # escalated would otherwise rescan it (2x the per-frame cost at 32 streams).
                     gc.freeze()
+                    self._gc_saved = (self._gc_saved[0], True)
                 gct = self.options.get("gc_threshold", (20000, 100, 1000))
                 if gct:
                     # Per-frame records die by reference count, never in cycles; collecting them every 700
@@ -1130,6 +1133,12 @@ class _Server:
             if self._runner is not None:
                 self._runner.close()
                 self._runner = None
+                if self._gc_saved is not None:  # the process's collector settings, as before the runner
+                    thresholds, frozen = self._gc_saved
+                    gc.set_threshold(*thresholds)
+                    if frozen:
+                        gc.unfreeze()
+                    self._gc_saved = None
             if self._hub is not None:
                 self._hub.close()
                 self._hub = None

@@ -157,3 +157,24 @@ def test_frame_result_lists_are_lazy(evam):
     fr.tensors.append(1)
     assert fr.tensors == [1] and P.FrameResult(1, 2, regions=[5]).regions == [5]
     assert json.loads(P.gvametaconvert_json(P.FrameResult(4, 4, timestamp=7)))["timestamp"] == 7
+
+
+def test_runner_restores_collector_settings(stubbed):
+    """The device runner raises the collector thresholds and freezes the startup heap while it serves;
+    PipelineServer.stop() gives the process its own settings back."""
+    import gc
+
+    ps, pre, mdir = stubbed
+    before = gc.get_threshold()
+    ps.PipelineServer.start({"pipeline_dir": PIPES, "model_dir": mdir})
+    register(ps)
+    qin = queue.Queue()
+    for im in frames(pre, 2):
+        qin.put(im)
+    qin.put(None)
+    p = ps.PipelineServer.pipeline("detect_classify", "hip")
+    p.start(source={"type": "application", "input": qin}, destination={})
+    assert p.wait(30)["state"] == "COMPLETED"
+    assert gc.get_threshold() == (20000, 100, 1000) and gc.get_freeze_count() > 0
+    ps.PipelineServer.stop()
+    assert gc.get_threshold() == before and gc.get_freeze_count() == 0
