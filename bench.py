@@ -408,6 +408,7 @@ def main():
     e0.record(stream)
     for t in range(args.steps):
         step(t)
+    t_submit = time.perf_counter() - t0  # host time to enqueue the K steps (≈ wall when host-bound)
     e1.record(stream)
     torch.cuda.synchronize()
     if world > 1:
@@ -461,6 +462,7 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(wall_max / args.steps * 1e3, 4),
+            "host_submit_ms_per_step": round(t_submit / args.steps * 1e3, 4),
             "higher_is_better": True,
             "scaling": "strong" if strong else "weak",
             "vs_baseline": None,

@@ -246,10 +246,11 @@ inline void roi_largest_first(const int* idx, int n, const Geom* geo, int DH, bo
             maxw = std::max(maxw, (int64_t)geo[i].cw * std::min(geo[i].ch, 2 * DH));
         }
     int start[65] = {0};
+    const double to_bucket = 63.0 / (double)maxw;  // a multiply per ROI, not a 64-bit division
     for (int m = 0; m < n; m++) {
         const int i = idx[m];
         const int64_t w = (int64_t)geo[i].cw * std::min(geo[i].ch, 2 * DH);
-        bucket[i] = sort ? 63 - (int)(w * 63 / maxw) : 0;  // 0 = largest
+        bucket[i] = sort ? 63 - std::min(63, (int)((double)w * to_bucket)) : 0;  // 0 = largest
         start[bucket[i] + 1]++;
     }
     for (int b = 0; b < 64; b++) start[b + 1] += start[b];

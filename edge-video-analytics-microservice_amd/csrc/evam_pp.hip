@@ -2496,9 +2496,12 @@ struct DescRing {
 // Per-call ROI descriptors ([RoiRec x n], launch order) change with every
 // detection result. They are written into a slot of pinned, coherent (fine-grained) host memory that
 // the ROI kernel reads directly over PCIe: each workgroup fetches only its own ~70 bytes, so a call
-// costs one memcpy and no copy command. `used[k]` fences the reuse of slot k.
+// costs one memcpy and no copy command. Slots are used in order and fenced in runs of kFence: one event,
+// recorded after the call that used the run's last slot, covers the run (an event record per call adds
+// a packet the command processor serves between every two ROI launches).
 struct PinRing {
-    static constexpr int N = 4;
+    static constexpr int N = 16;
+    static constexpr int kFence = 4;
     uint8_t* host[N] = {};
     const uint8_t* dev[N] = {};  // device address of host[k]
     size_t cap[N] = {};
@@ -2508,6 +2511,18 @@ struct PinRing {
 };
 
 }  // namespace
+
+#ifdef EVAM_PP_HOST_PROF
+// Diagnostic build: cumulative host time from entry to each mark of evam_pp_run, printed at destroy.
+#include <chrono>
+static double g_hp[12];
+static long g_hp_n;
+#define HP_START const auto hp_t0 = std::chrono::steady_clock::now(); double hp_t[12] = {}
+#define HP(i) (hp_t[i] = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - hp_t0).count())
+#else
+#define HP_START (void)0
+#define HP(i) (void)0
+#endif
 
 struct evam_pp {
     int device = 0;
@@ -2567,8 +2582,9 @@ void pin_release(PinRing& r) {
 int pin_acquire(evam_pp* h, size_t n, uint8_t** host, const uint8_t** dev) {
     PinRing& r = h->pin;
     const int k = (r.cur + 1) % PinRing::N;
-    if (!r.used[k]) HIP_TRY(hipEventCreateWithFlags(&r.used[k], hipEventDisableTiming));
-    if (r.used_rec[k]) HIP_TRY(hipEventSynchronize(r.used[k]));
+    const int fk = k | (PinRing::kFence - 1);  // the run's fence: recorded after slot fk's previous use
+    if (!r.used[fk]) HIP_TRY(hipEventCreateWithFlags(&r.used[fk], hipEventDisableTiming));
+    if (r.used_rec[fk]) HIP_TRY(hipEventSynchronize(r.used[fk]));
     if (r.cap[k] < n) {
         if (r.host[k]) HIP_TRY(hipHostFree(r.host[k]));
         r.host[k] = nullptr;
@@ -2692,6 +2708,13 @@ int evam_pp_create(int hip_device, void* hip_stream, evam_pp** out) {
 
 void evam_pp_destroy(evam_pp* h) {
     if (!h) return;
+#ifdef EVAM_PP_HOST_PROF
+    if (g_hp_n) {
+        fprintf(stderr, "[host prof] %ld steady calls, mean us from entry at marks 1..10:", g_hp_n);
+        for (int i = 1; i <= 10; i++) fprintf(stderr, " %.2f", g_hp[i] / g_hp_n);
+        fprintf(stderr, "\n");
+    }
+#endif
     (void)hipSetDevice(h->device);
     if (h->ring.copy || h->pin.cur >= 0) {
         (void)hipStreamSynchronize(h->stream);
@@ -2763,6 +2786,7 @@ int evam_pp_linear_table(int src_size, int dst_size, int is_x, int32_t* ofs, int
 
 int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* items, int n_items,
                 const evam_preproc* cfg, const evam_tensor* dst, evam_transform* out_xform) {
+    HP_START;
     if (!h || !srcs || !cfg || !dst) return fail(EVAM_PP_ERR_INVALID_ARG, "evam_pp_run: NULL argument");
     if (n_srcs <= 0) return fail(EVAM_PP_ERR_INVALID_ARG, "evam_pp_run: n_srcs must be > 0");
     if (!items) n_items = n_srcs;
@@ -2811,6 +2835,7 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
         }
     }
 
+    HP(1);
     // ---- pass 1 (integer only): item -> source, format, clipped crop; validation ----
     std::vector<int>& fmt = h->sc_fmt;
     std::vector<Geom>& geo = h->sc_geo;
@@ -2843,6 +2868,7 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
         if (rep[f] < 0) rep[f] = i;
         else if (g.cw != geo[rep[f]].cw || g.ch != geo[rep[f]].ch) uniform[f] = false;  // geometry = f(cw, ch)
     }
+    HP(2);
     // item indices grouped by format, in call order within a format
     std::vector<int>& members = h->sc_members;
     members.resize(n_items);
@@ -2896,6 +2922,7 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
         if (h->opt_stats) src_bytes += item_src_bytes(f, g, DW, DH);
     }
 
+    HP(3);
     // ---- descriptor block (device-resident, re-uploaded only when its bytes change) ----
     // [LUT][ItemDesc x (items of generic groups)][per uniform group: XTab x DW, YTab x DH]
     // Everything in it is a function of the configuration and the geometry, not of the frames, so a new
@@ -2972,11 +2999,13 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
         }
     }
     (void)any_generic;
+    HP(4);
     HIP_TRY(hipSetDevice(h->device));
     uint8_t* dyn = nullptr;
     const uint8_t* d_dyn = nullptr;
     if (any_roi) {
         if (int rc = pin_acquire(h, dyn_bytes, &dyn, &d_dyn)) return rc;
+        HP(5);
         // Launch order: largest estimated work first (counting sort on 64 buckets of the staged
         // bytes, crop width x touched rows). Workgroups are dispatched in order as slots free, so
         // the long ROIs start first and the short ones fill the tail.
@@ -2989,6 +3018,7 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
             RoiRec* rr = reinterpret_cast<RoiRec*>(dyn + rec_off[f]);
             std::vector<int>& ord = h->sc_order;
             roi_largest_first(members.data() + mfirst[f], count[f], geo.data(), DH, sort, bucket.data(), ord);
+            HP(6);
             if (xcd_group) {
                 // Record p runs on XCD p % 8: deal each frame's ROIs (frame s -> XCD s % 8, largest
                 // first within the XCD) so overlapping crops of one frame share one L2.
@@ -3016,6 +3046,19 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
             std::vector<int>& un = h->sc_units;  // (item, row0, row1, cost) per unit
             un.clear();
             int maxcost = 1;
+            if (base == 1 && gt <= 0) {
+                // one unit per ROI (the default): no row split, no 64-bit divisions (this loop runs per ROI
+                // on the host for every call: 1,600 ROIs in C3)
+                un.resize(4 * ord.size());
+                int* u4 = un.data();
+                for (size_t p = 0; p < ord.size(); p++, u4 += 4) {
+                    const int i = ord[p];
+                    const int R = std::max(1, std::min(std::min(q.buf_bytes / row_bytes_bound(f, geo[i].cw), rcap), DH));
+                    const int cost = (DH + R - 1) / R;
+                    maxcost = std::max(maxcost, cost);
+                    u4[0] = i; u4[1] = 0; u4[2] = DH; u4[3] = cost;
+                }
+            } else
             for (size_t p = 0; p < ord.size(); p++) {
                 const int i = ord[p];
                 const int R = std::max(1, std::min(std::min(q.buf_bytes / row_bytes_bound(f, geo[i].cw), rcap), DH));
@@ -3029,6 +3072,7 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
                     un.insert(un.end(), {i, y0, y1, cost});
                 }
             }
+            HP(7);
             // stable counting sort of the units by cost, largest first
             const int nu = (int)(un.size() / 4);
             std::vector<int> start(maxcost + 2, 0);
@@ -3053,8 +3097,10 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
             qrec[f] = nrec;
         }
     }
+    HP(8);
     const uint8_t* d_block = nullptr;
     if (int rc = ring_upload(h, &d_block)) return rc;
+    HP(9);
 
     // ---- launches ----
     if (h->opt_timing) HIP_TRY(hipEventRecord(h->ev0, h->stream));
@@ -3279,12 +3325,20 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
         if (e != hipSuccess) return fail(EVAM_PP_ERR_HIP, "kernel launch failed: %s", hipGetErrorString(e));
         launches++;
     }
-    if (any_roi) {
+    if (any_roi && (h->pin.cur & (PinRing::kFence - 1)) == PinRing::kFence - 1) {
         HIP_TRY(hipEventRecord(h->pin.used[h->pin.cur], h->stream));
         h->pin.used_rec[h->pin.cur] = true;
     }
     if (h->opt_timing) HIP_TRY(hipEventRecord(h->ev1, h->stream));
     h->timed = h->opt_timing != 0;
+#ifdef EVAM_PP_HOST_PROF
+    HP(10);
+    static long hp_calls = 0;
+    if (++hp_calls > 200) {  // steady state: past warm-up, allocations and code-object loading
+        for (int i = 0; i < 12; i++) g_hp[i] += hp_t[i];
+        g_hp_n++;
+    }
+#endif
 
     h->stats.n_items = n_items;
     h->stats.n_launches = launches;

@@ -397,7 +397,7 @@ def test_wave_kernel_variants(evam, O, coracle, gpu, fmt, src, dst, resize, vari
 
 def test_stream_switch_and_descriptor_churn(evam, O, coracle, gpu):
     """Descriptor slots stay valid across torch stream switches and many changing ROI sets / geometries
-    (the upload ring and the pinned ROI ring wrap several times; slot fences follow the stream)."""
+    (the upload ring and the pinned ROI ring wrap; slot fences, one per run of ROI slots, follow the stream)."""
     import torch
 
     rng = np.random.default_rng(11)
@@ -406,7 +406,7 @@ def test_stream_switch_and_descriptor_churn(evam, O, coracle, gpu):
     pp = evam.HipPreProcessor(device=0)
     streams = [torch.cuda.Stream(device=gpu) for _ in range(3)]
     outs, refs = [], []
-    for it in range(12):
+    for it in range(40):  # 20 ROI calls: the 16-slot pinned ROI ring wraps
         s = streams[it % 3]
         with torch.cuda.stream(s):
             if it % 2:
