@@ -1660,6 +1660,11 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(96))) void
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     if (P.ablate & 128) return;  // diagnostics: launch cost only
     EVAM_STAMP(0);
+    // The whole 64-byte record in one scalar load, issued first: it is a PCIe read from pinned host
+    // memory (~1-2 us under load), and field-by-field loads became up to three dependent round trips
+    // per wave. Its latency overlaps the LUT load below.
+    typedef unsigned int u32x16 __attribute__((ext_vector_type(16)));
+    const u32x16 rec = *((const __attribute__((address_space(4))) u32x16*)(P.recs) + blockIdx.x);
     // The LUT is loaded once per workgroup, whatever number of units it processes.
     float* lut_s = reinterpret_cast<float*>(smem);
     if constexpr (OUT == 1 && !(kRoiAluNorm && PX == 1)) {
@@ -1671,16 +1676,22 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(96))) void
             lut_s[i] = P.lut[P.color_rgb ? 512 - (i & ~255) + (i & 255) : i];
         }
     }
-    const __attribute__((address_space(4))) RoiRec* roi = (const __attribute__((address_space(4))) RoiRec*)(P.recs) + blockIdx.x;
-    const int item = roi->item;
-    const uint32_t wh = *(const __attribute__((address_space(4))) uint32_t*)&roi->width;
-    const uint32_t rr01 = *(const __attribute__((address_space(4))) uint32_t*)&roi->row0;
+    // RoiRec as dwords: plane[0..2] 0-5, pitch[0..2] 6-8, width | height << 16 9, x y w h 10-13, item 14,
+    // row0 | row1 << 16 15
+    static_assert(offsetof(RoiRec, pitch) == 24 && offsetof(RoiRec, width) == 36 && offsetof(RoiRec, x) == 40 &&
+                  offsetof(RoiRec, item) == 56 && offsetof(RoiRec, row0) == 60, "RoiRec dword map");
+    auto ptr_of = [](unsigned lo, unsigned hi) {
+        return reinterpret_cast<const uint8_t*>(((uint64_t)hi << 32) | lo);
+    };
+    const int item = (int)rec[14];
+    const uint32_t wh = rec[9];
+    const uint32_t rr01 = rec[15];
     const int fw = wh & 0xFFFF, fh = wh >> 16;
-    const int rx = roi->x, ry = roi->y, rwd = roi->w, rht = roi->h;
-    const uint8_t* p0 = roi->plane[0];
-    const uint8_t* p1 = roi->plane[1];
-    const uint8_t* p2 = roi->plane[2];
-    const int pitch0 = roi->pitch[0], pitch1 = roi->pitch[1], pitch2 = roi->pitch[2];
+    const int rx = (int)rec[10], ry = (int)rec[11], rwd = (int)rec[12], rht = (int)rec[13];
+    const uint8_t* p0 = ptr_of(rec[0], rec[1]);
+    const uint8_t* p1 = ptr_of(rec[2], rec[3]);
+    const uint8_t* p2 = ptr_of(rec[4], rec[5]);
+    const int pitch0 = (int)rec[6], pitch1 = (int)rec[7], pitch2 = (int)rec[8];
     Geom g;
     roi_geometry(FMT, fw, fh, true, rx, ry, rwd, rht, P.mode, P.placement, P.DW, P.DH,
                  g);  // never empty: the host validated every item
