@@ -785,13 +785,22 @@ __global__ EVAM_STAGED_BOUNDS void evam_pp_staged(const SParams P) {
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     // Prologue critical path: the launch parameters, then (in parallel) the item's arguments, the tile's
     // row table and its column footprint (from the parameters when tiles_x <= kTCols), then the first
-    // DMA. Nothing waits on a load it does not need.
-    const int t = P.xcd_remap ? xcd_tile(blockIdx.x, gridDim.x) : (int)blockIdx.x;
-    const int item = t / P.tiles_per_item;
-    const int tile = t - item * P.tiles_per_item;
-    const int ty = tile / P.tiles_x;
-    const int tx = tile - ty * P.tiles_x;
-    const int Y0 = ty * P.TH, Y1 = min(Y0 + P.TH, P.DH);
+    // DMA. Two batches of scalar loads, one wait each: (1) the launch parameters, (2) the item's
+    // arguments and the tile column's footprint (the row table's vector load goes out between them).
+    // Without the empty asm uses, branches on parameters split the loads into ~6 dependent round trips
+    // before the first DMA (C2 +0.5 to +3 %, C5 +0.4 to +1.4 %: profiles/r02zz_prologue_batch_ab.txt).
+    const int p_xcd = P.xcd_remap, p_tpi = P.tiles_per_item, p_tx = P.tiles_x, p_TH = P.TH, p_DH = P.DH;
+    const int p_grid = gridDim.x;
+    asm volatile("" ::"s"(p_xcd), "s"(p_tpi), "s"(p_tx), "s"(p_TH), "s"(p_DH), "s"(p_grid), "s"(P.ytab), "s"(P.ox),
+                 "s"(P.rw), "s"(P.slot_bytes), "s"(P.ablate), "s"(P.offBuf), "s"(P.color_rgb), "s"(P.DW),
+                 "s"(P.ntcol));
+    const int t_x = xcd_tile(blockIdx.x, p_grid);
+    const int t = p_xcd ? t_x : (int)blockIdx.x;
+    const int item = t / p_tpi;
+    const int tile = t - item * p_tpi;
+    const int ty = tile / p_tx;
+    const int tx = tile - ty * p_tx;
+    const int Y0 = ty * p_TH, Y1 = min(Y0 + p_TH, p_DH);
     const int rows = Y1 - Y0;
     // The tile's row table (<= 64 rows, host-checked), one row per lane in every wave: per-group lookups
     // are v_readlane instead of dependent scalar loads from L2 (~1 us per group in the loop's critical
@@ -805,6 +814,10 @@ __global__ EVAM_STAGED_BOUNDS void evam_pp_staged(const SParams P) {
     const uint8_t* p2 = it.plane[2];
     const int pitch0 = it.pitch[0], pitch1 = it.pitch[1], pitch2 = it.pitch[2];
     const int x0 = it.x0, y0 = it.y0, ox = P.ox, rw = P.rw;
+    const int2 tc = P.tcol[min(tx, kTCols - 1)];
+    const int p_ntcol = P.ntcol, p_index = it.index;
+    asm volatile("" ::"s"(p0), "s"(p1), "s"(p2), "s"(pitch0), "s"(pitch1), "s"(pitch2), "s"(x0), "s"(y0),
+                 "s"(p_index), "s"(tc.x), "s"(tc.y), "s"(P.dst), "s"(P.slot_offset), "s"(P.slot_stride));
     const size_t plane = (size_t)P.DW * P.DH;
     const size_t esz = OUT == 1 ? 4 : 1;
     uint8_t* const d0 = reinterpret_cast<uint8_t*>(P.dst) + (size_t)(P.slot_offset + it.index * P.slot_stride) * 3 * plane * esz;
@@ -839,7 +852,7 @@ __global__ EVAM_STAGED_BOUNDS void evam_pp_staged(const SParams P) {
     int fsY = 0, nY = 0, fsC = 0, nC = 0;
     if (cols) {
         int s0, s1;
-        if (tx < P.ntcol) { s0 = P.tcol[tx].x; s1 = P.tcol[tx].y; }
+        if (tx < p_ntcol) { s0 = tc.x; s1 = tc.y; }
         else { s0 = xtab_s[Xv0].s0; s1 = xtab_s[Xv1].s1; }
         footprint_chunks(FMT, T::bpp, x0 + s0, x0 + s1, fsY, nY, fsC, nC);
     }
@@ -1260,6 +1273,10 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_wave(const WParams P) {
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int t = blockIdx.x;
+    // the launch parameters of the prologue in one batch of scalar loads (one wait): without the empty
+    // asm use, branches split them into dependent round trips ahead of the first DMA
+    asm volatile("" ::"s"(P.tiles_per_item), "s"(P.tiles_x), "s"(P.ytab), "s"(P.xtab), "s"(P.ablate), "s"(P.TH),
+                 "s"(P.DH), "s"(P.DW), "s"(P.ox), "s"(P.rw));
     const int item = t / P.tiles_per_item;
     const int tile = t - item * P.tiles_per_item;
     const int ty = tile / P.tiles_x;
@@ -1285,10 +1302,6 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_wave(const WParams P) {
     const __amdgpu_buffer_rsrc_t rsO2 = __builtin_amdgcn_make_buffer_rsrc((void*)(P.color_rgb ? d0 : d2), (short)0, 0x7FFFFFFF, 0x00020000);
 
     float* lut_s = reinterpret_cast<float*>(smem);
-    if constexpr (OUT == 1) {
-        for (int i = tid; i < 768; i += kThreads) lut_s[i] = P.lut[i];
-        __syncthreads();
-    }
     // fill values in output plane order (P.fill is already in output channel order)
     const int fo0 = P.fill & 0xFF, fo1 = (P.fill >> 8) & 0xFF, fo2 = (P.fill >> 16) & 0xFF;
     const int fb0 = P.color_rgb ? fo2 : fo0, fb2 = P.color_rgb ? fo0 : fo2;  // same, in BGR order
@@ -1298,33 +1311,22 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_wave(const WParams P) {
     const int Xv0 = max(X0, ox), Xv1 = min(min(X0 + TW, P.DW), ox + rw) - 1;
     const bool cols = Xv0 <= Xv1;
     int fsY = 0, nY = 0, fsC = 0, nC = 0;
-    if (cols) {
-        footprint_chunks(FMT, T::bpp, x0 + xtab_s[Xv0].s0, x0 + xtab_s[Xv1].s1, fsY, nY, fsC, nC);
-    }
-    // per-lane column state for the PX pixels of this lane
+    // both footprint taps in one batch of scalar loads (clamped indices: read even for padding tiles)
+    const int fs0 = xtab_s[max(min(Xv0, P.DW - 1), 0)].s0, fs1 = xtab_s[max(min(Xv1, P.DW - 1), 0)].s1;
+    if (cols) footprint_chunks(FMT, T::bpp, x0 + fs0, x0 + fs1, fsY, nY, fsC, nC);
+    // per-lane column state for the PX pixels of this lane: the PX table loads go out together here and
+    // are consumed after the first DMA is issued
     const int Xl = X0 + lane * PX;
     const bool xin = Xl < P.DW;  // DW % PX == 0: a lane's pixels are all in or all out
-    uint32_t lY[PX], lC[PX], wa[PX];
+    XTab xts[PX];
 #pragma unroll
-    for (int j = 0; j < PX; j++) {
-        const XTab xt = P.xtab[xin ? Xl + j : 0];
-        wa[j] = (uint32_t)xt.a0 | ((uint32_t)xt.a1 << 16);
-        lY[j] = lC[j] = 0;
-        if (xin && wa[j] != 0) {
-            const int ca = x0 + xt.s0, cb = x0 + xt.s1;
-            lY[j] = (uint32_t)(ca * T::bpp - fsY) | ((uint32_t)(cb * T::bpp - fsY) << 16);
-            if constexpr (FMT == kNV12)
-                lC[j] = (uint32_t)(2 * (ca >> 1) - fsC) | ((uint32_t)(2 * (cb >> 1) - fsC) << 16);
-            else if constexpr (FMT == kI420)
-                lC[j] = (uint32_t)((ca >> 1) - fsC) | ((uint32_t)((cb >> 1) - fsC) << 16);
-        }
-    }
+    for (int j = 0; j < PX; j++) xts[j] = P.xtab[xin ? Xl + j : 0];
+    uint32_t lY[PX], lC[PX], wa[PX];
     const uint32_t vo = (uint32_t)(xin ? Xl : 0) * (uint32_t)esz;
 
     // this wave's rows
     const int thw = (P.TH + 3) >> 2;
     const int Yw0 = Y0 + wave * thw, Yw1 = min(Yw0 + thw, Y1);
-    if (Yw0 >= Yw1) return;
     uint8_t* const wbuf = smem + P.offBuf + wave * P.wave_bytes;
     const int half = P.wave_bytes >> 1;
     const int segY = P.segY, segC = P.segC;
@@ -1333,6 +1335,7 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_wave(const WParams P) {
 
     LaneRows lr;  // this wave's rows (<= 64, host)
     lr.load(P.ytab, Yw0, Yw1 - Yw0, lane);
+
     // Staging decision for output row Y, given the source rows (pa, pb) whose H the wave holds.
     struct Plan {
         int ya, yb, b0, b1;
@@ -1479,8 +1482,32 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_wave(const WParams P) {
 #pragma unroll
         for (int ch = 0; ch < 3; ch++) HA[j][ch] = HB[j][ch] = 0;
     int pa = -1, pb = -1;
-    Plan cur = plan(Yw0, pa, pb);
-    issue(cur, wbuf);
+    // Prologue order: the first row's DMA needs only the item, the footprint and the row table, so it goes
+    // out before the LUT load, its barrier and the per-lane column math, whose latency it then covers.
+    Plan cur{};
+    if (Yw0 < Yw1) {
+        cur = plan(Yw0, pa, pb);
+        issue(cur, wbuf);
+    }
+    if constexpr (OUT == 1) {
+        for (int i = tid; i < 768; i += kThreads) lut_s[i] = P.lut[i];
+        __syncthreads();  // every wave, including those without rows
+    }
+    if (Yw0 >= Yw1) return;
+#pragma unroll
+    for (int j = 0; j < PX; j++) {
+        const XTab& xt = xts[j];
+        wa[j] = (uint32_t)xt.a0 | ((uint32_t)xt.a1 << 16);
+        lY[j] = lC[j] = 0;
+        if (xin && wa[j] != 0) {
+            const int ca = x0 + xt.s0, cb = x0 + xt.s1;
+            lY[j] = (uint32_t)(ca * T::bpp - fsY) | ((uint32_t)(cb * T::bpp - fsY) << 16);
+            if constexpr (FMT == kNV12)
+                lC[j] = (uint32_t)(2 * (ca >> 1) - fsC) | ((uint32_t)(2 * (cb >> 1) - fsC) << 16);
+            else if constexpr (FMT == kI420)
+                lC[j] = (uint32_t)((ca >> 1) - fsC) | ((uint32_t)((cb >> 1) - fsC) << 16);
+        }
+    }
     int i = 0;
     for (int Y = Yw0; Y < Yw1; Y++, i++) {
         // this row's DMA landed; the previous row's three stores may stay in flight
@@ -1658,6 +1685,10 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(96))) void
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    // the parameters of the prologue in one batch of scalar loads, so the record's PCIe read below is not
+    // queued behind a kernarg round trip for the diagnostics test
+    asm volatile("" ::"s"(P.ablate), "s"(P.recs), "s"(P.lut), "s"(P.color_rgb), "s"(P.mode), "s"(P.placement),
+                 "s"(P.DW), "s"(P.DH));
     if (P.ablate & 128) return;  // diagnostics: launch cost only
     EVAM_STAMP(0);
     // The whole 64-byte record in one scalar load, issued first: it is a PCIe read from pinned host
