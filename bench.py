@@ -446,7 +446,8 @@ def main():
                     "mean_launch_ms": round(res_ms, 5), "steps": args.resident_steps,
                     "set_bytes": in_bytes + out_n * 3 * DH * DW * esz}
     tot = evam.streams.reduce_run(wall, n * args.steps, alg_bytes * args.steps,
-                                  device=device if world > 1 and backend == "nccl" else None)
+                                  device=device if world > 1 and backend == "nccl" else None,
+                                  device_key=evam.streams.device_key(local))
     wall_max = tot.elapsed_max_s
     value = tot.frames / wall_max
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
@@ -458,7 +459,8 @@ def main():
                       + (" [host feed, PCIe-inclusive]" if feed is not None else ""),
             "value": round(value, 1),
             "unit": "frames/s",
-            "n_gpus": world,
+            "n_gpus": tot.devices,  # distinct GPUs (a gloo rehearsal may put several ranks on one)
+            "ranks": world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(wall_max / args.steps * 1e3, 4),

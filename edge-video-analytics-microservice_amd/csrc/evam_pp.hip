@@ -48,21 +48,15 @@ using namespace evam;
 // ------------------------------------------------------------------------------------------------
 constexpr int kThreads = 256;
 
-// Optional SGPR cap (diagnostics). A CU admits floor(800 / (ceil(sgpr/16)*16 + 16)) 256-thread
-// workgroups (MI355X_MICROARCH.md, Residency), so the staged kernel's ~102 SGPRs allow 6. Capping at
-// 80 (8 per CU; the excess spills to VGPR lanes) measured 2-8 % SLOWER on every config
-// (profiles/r01_sweeps.txt, r01t), so the default leaves the allocation to the compiler.
-#ifdef EVAM_PP_SGPR_CAP
-#define EVAM_KERNEL_BOUNDS __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(EVAM_PP_SGPR_CAP)))
-#else
-#define EVAM_KERNEL_BOUNDS __launch_bounds__(kThreads)
-#endif
-#ifdef EVAM_PP_STAGED_SGPR
-#define EVAM_STAGED_BOUNDS __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(EVAM_PP_STAGED_SGPR)))
-#else
-#define EVAM_STAGED_BOUNDS EVAM_KERNEL_BOUNDS
-#endif
 constexpr int kLutBytes = 3 * 256 * 4;
+// Stage-removal diagnostics (bits: 2 no pixel math, 4 no stores, 8 loads only, 16 no loads, 32/64/128 stop
+// early). Compile-time only: a product build is 0, every diagnostic branch folds away, and no environment
+// setting can change results. A build with -DEVAM_PP_ABLATE=bits computes INVALID tensors; evam_pp_create
+// refuses it unless EVAM_PP_DIAGNOSTIC_BUILD_OK=1 (tools/prof_ablate.sh).
+#ifndef EVAM_PP_ABLATE
+#define EVAM_PP_ABLATE 0
+#endif
+constexpr int kAblate = EVAM_PP_ABLATE;
 // Cache-policy bits of the output stores: 2 = nt (non-temporal). The outputs are written once and
 // read by nobody in the launch; streaming them past the caches measured 1.5-3 % faster on C2/C3/C4
 // and 10 % on C5 (profiles/r02r_store_policy.txt). EVAM_PP_LOAD_AUX: the same bits for the LDS-DMA
@@ -106,7 +100,6 @@ struct KParams {
     int offCol, offRow; // LDS carve: LUT at 0 (fp32 out), column table, row table
     int color_rgb;
     uint32_t fill;      // packed u8 fill, output channel order
-    int ablate;         // diagnostics only (EVAM_PP_ABLATE bits): 2 no pixel math, 4 no stores, 8 loads only, 16 no loads
 };
 
 // Per output column of a tile: absolute byte offsets of the two horizontal taps inside a source row.
@@ -151,7 +144,6 @@ struct RParams {
     int nsegx;           // TW / 64 column segments per tile row
     int color_rgb;
     uint32_t fill;
-    int ablate;
 };
 
 constexpr int kSlot = 1024;  // bytes of one staged source-row segment = one wave-wide 16 B/lane LDS-DMA
@@ -171,7 +163,6 @@ struct SParams {
     int slot_bytes;      // one staged row segment: the widest 16-byte-aligned footprint of the launch
     int color_rgb;
     uint32_t fill;
-    int ablate;
     int xcd_remap;       // 1: consecutive tiles land on one XCD (shared halo rows stay in one L2)
     int ntcol;           // tiles_x when <= kTCols (tcol valid), else 0 (the kernel reads xtab)
     int2 tcol[16];       // per tile column: crop-relative source columns of its first / last visible
@@ -388,10 +379,10 @@ __global__ __launch_bounds__(kThreads) void evam_pp_kernel(const KParams P) {
         x.wa = (uint32_t)ce.a0 | ((uint32_t)ce.a1 << 16);
         x.wb0 = (uint32_t)re.b0;
         x.wb1 = (uint32_t)re.b1;
-        const bool img = in_tile && x.wa != 0 && (x.wb0 | x.wb1) != 0 && !(P.ablate & 2);
+        const bool img = in_tile && x.wa != 0 && (x.wb0 | x.wb1) != 0 && !(kAblate & 2);
         x.mode = !in_tile ? 0 : (img ? 2 : 1);
         x.o = o_tile + __umul24((uint32_t)cy, (uint32_t)P.DW) + (uint32_t)cx;
-        if (P.ablate & 16) {  // diagnostics: no loads, math on synthetic bytes
+        if (kAblate & 16) {  // diagnostics: no loads, math on synthetic bytes
             for (int k = 0; k < 4; k++) { x.raw[k][0] = (ce.oY0 + k) & 255; x.raw[k][1] = (re.y0 + ce.oC0 * k) & 0xFFFF; x.raw[k][2] = k; }
             return;
         }
@@ -405,10 +396,10 @@ __global__ __launch_bounds__(kThreads) void evam_pp_kernel(const KParams P) {
     auto finish = [&](const Px& x) {
         if (x.mode == 0) return;
         if (x.mode == 1) {
-            if (!(P.ablate & 4)) store_px<OUT>(d0, d1, d2, lut_s, x.o, f0, f1, f2);
+            if (!(kAblate & 4)) store_px<OUT>(d0, d1, d2, lut_s, x.o, f0, f1, f2);
             return;
         }
-        if (P.ablate & 8) {  // diagnostics: loads only, trivial math
+        if (kAblate & 8) {  // diagnostics: loads only, trivial math
             uint32_t acc = 0;
             for (int k = 0; k < 4; k++) acc += x.raw[k][0] + x.raw[k][1] + x.raw[k][2];
             asm volatile("" :: "v"(acc));
@@ -429,7 +420,7 @@ __global__ __launch_bounds__(kThreads) void evam_pp_kernel(const KParams P) {
         const int vb = vresize(Db0, Db1, x.wb0, x.wb1);
         const int vg = vresize(Dg0, Dg1, x.wb0, x.wb1);
         const int vr = vresize(Dr0, Dr1, x.wb0, x.wb1);
-        if (P.ablate & 4) {
+        if (kAblate & 4) {
             asm volatile("" :: "v"(vb), "v"(vg), "v"(vr));  // keep the math alive
             return;
         }
@@ -519,7 +510,7 @@ __device__ __forceinline__ UV3 chroma_terms(const Chroma<FMT>& c) {
 // both vertical taps read the same chroma row (4:2:0, ~half the rows) their chroma is loaded and
 // converted once.
 template <int FMT, int OUT>
-__global__ EVAM_KERNEL_BOUNDS void evam_pp_rows(const RParams P) {
+__global__ __launch_bounds__(kThreads) void evam_pp_rows(const RParams P) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     using T = FmtTraits<FMT>;
     constexpr bool kYUV = FMT == kNV12 || FMT == kI420;
@@ -585,10 +576,10 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_rows(const RParams P) {
     for (int Y = Y0 + row0; Y < Y1; Y += row_step) {
         const int yr0 = ytab[Y].r0, yr1 = ytab[Y].r1, yb0 = ytab[Y].b0, yb1 = ytab[Y].b1;  // scalar loads
         const uint32_t orow = (uint32_t)(Y * P.DW);
-        if ((yb0 | yb1) == 0 || (P.ablate & 2)) {  // padding row (letterbox)
+        if ((yb0 | yb1) == 0 || (kAblate & 2)) {  // padding row (letterbox)
 #pragma unroll
             for (int j = 0; j < 2; j++)
-                if (xin[j] && !(P.ablate & 4)) store_px<OUT>(d0, d1, d2, lut_s, orow + xo[j], f0, f1, f2);
+                if (xin[j] && !(kAblate & 4)) store_px<OUT>(d0, d1, d2, lut_s, orow + xo[j], f0, f1, f2);
             continue;
         }
         const int ya = y0 + yr0, yb = y0 + yr1;
@@ -605,7 +596,7 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_rows(const RParams P) {
             // ---- gather: every tap of every owned segment, before any arithmetic ----
             uint32_t q[2][4][3];
             Chroma<FMT> ch[2][4];
-            if (P.ablate & 16) {  // diagnostics: no loads, arithmetic on synthetic bytes
+            if (kAblate & 16) {  // diagnostics: no loads, arithmetic on synthetic bytes
 #pragma unroll
                 for (int j = 0; j < 2; j++)
 #pragma unroll
@@ -660,7 +651,7 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_rows(const RParams P) {
 #pragma unroll
             for (int j = 0; j < 2; j++) {
                 if (j < nseg && xin[j]) {
-                    if (P.ablate & 8) {  // diagnostics: loads only
+                    if (kAblate & 8) {  // diagnostics: loads only
                         uint32_t acc = ch[j][0].u + ch[j][1].u + (kShare ? 0u : ch[j][2].u + ch[j][3].u);
 #pragma unroll
                         for (int k = 0; k < 4; k++) acc += q[j][k][0];
@@ -695,7 +686,7 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_rows(const RParams P) {
                         const uint32_t D1 = __umul24(c[2][ch3], a0) + __umul24(c[3][ch3], a1);
                         v[ch3] = vresize(D0, D1, wb0, wb1);
                     }
-                    if (P.ablate & 4) {
+                    if (kAblate & 4) {
                         asm volatile("" :: "v"(v[0]), "v"(v[1]), "v"(v[2]));
                     } else {
                         if (P.color_rgb) { const int tmp = v[0]; v[0] = v[2]; v[2] = tmp; }
@@ -751,6 +742,19 @@ __device__ __forceinline__ void vmcnt_at_most(int n) {
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// Same, exact for n <= 24 (a jump over immediates; larger n waits for 24).
+__device__ __forceinline__ void vmcnt_exact(int n) {
+    n = __builtin_amdgcn_readfirstlane(n);
+#define EVAM_VMC(k) case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
+    switch (n) {
+        EVAM_VMC(0) EVAM_VMC(1) EVAM_VMC(2) EVAM_VMC(3) EVAM_VMC(4) EVAM_VMC(5) EVAM_VMC(6) EVAM_VMC(7) EVAM_VMC(8)
+        EVAM_VMC(9) EVAM_VMC(10) EVAM_VMC(11) EVAM_VMC(12) EVAM_VMC(13) EVAM_VMC(14) EVAM_VMC(15) EVAM_VMC(16)
+        EVAM_VMC(17) EVAM_VMC(18) EVAM_VMC(19) EVAM_VMC(20) EVAM_VMC(21) EVAM_VMC(22) EVAM_VMC(23)
+        default: asm volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
+    }
+#undef EVAM_VMC
+}
+
 // Staged uniform-geometry kernel. A workgroup owns a TW x TH tile (TW = 64 x NSEGX) and walks it in
 // groups of R output rows. For each group the source row segments its taps need (two luma rows and
 // two chroma rows per output row, each at most kSlot bytes wide) are brought into LDS by LDS-DMA —
@@ -764,7 +768,7 @@ __device__ __forceinline__ void vmcnt_at_most(int n) {
 // exact) and waits for group g with vmcnt(operations issued after group g's DMA), so stores and later
 // groups' DMA stay in flight.
 template <int FMT, int OUT, int R, int NSEGX, int NBUF>
-__global__ EVAM_STAGED_BOUNDS void evam_pp_staged(const SParams P) {
+__global__ __launch_bounds__(kThreads) void evam_pp_staged(const SParams P) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     using T = FmtTraits<FMT>;
     constexpr bool kYUV = FMT == kNV12 || FMT == kI420;
@@ -792,7 +796,7 @@ __global__ EVAM_STAGED_BOUNDS void evam_pp_staged(const SParams P) {
     const int p_xcd = P.xcd_remap, p_tpi = P.tiles_per_item, p_tx = P.tiles_x, p_TH = P.TH, p_DH = P.DH;
     const int p_grid = gridDim.x;
     asm volatile("" ::"s"(p_xcd), "s"(p_tpi), "s"(p_tx), "s"(p_TH), "s"(p_DH), "s"(p_grid), "s"(P.ytab), "s"(P.ox),
-                 "s"(P.rw), "s"(P.slot_bytes), "s"(P.ablate), "s"(P.offBuf), "s"(P.color_rgb), "s"(P.DW),
+                 "s"(P.rw), "s"(P.slot_bytes), "s"(P.offBuf), "s"(P.color_rgb), "s"(P.DW),
                  "s"(P.ntcol));
     const int t_x = xcd_tile(blockIdx.x, p_grid);
     const int t = p_xcd ? t_x : (int)blockIdx.x;
@@ -827,16 +831,9 @@ __global__ EVAM_STAGED_BOUNDS void evam_pp_staged(const SParams P) {
     const __amdgpu_buffer_rsrc_t rsC = __builtin_amdgcn_make_buffer_rsrc((void*)(p1 ? p1 : p0), (short)0, 0x7FFFFFFF, 0x00020000);
     const __amdgpu_buffer_rsrc_t rsV = __builtin_amdgcn_make_buffer_rsrc((void*)(p2 ? p2 : p0), (short)0, 0x7FFFFFFF, 0x00020000);
     // plane of source channel 0 / 2 (B / R): swapped for RGB order
-#ifdef EVAM_PP_ONE_DST
-    // one resource for the item's three output planes; the plane offset rides in soffset
-    const __amdgpu_buffer_rsrc_t rsD = __builtin_amdgcn_make_buffer_rsrc((void*)d0, (short)0, 0x7FFFFFFF, 0x00020000);
-    const int pbytes = (int)(plane * esz);
-    const int po0 = P.color_rgb ? 2 * pbytes : 0, po2 = P.color_rgb ? 0 : 2 * pbytes;
-#else
     const __amdgpu_buffer_rsrc_t rsD0 = __builtin_amdgcn_make_buffer_rsrc((void*)(P.color_rgb ? d2 : d0), (short)0, 0x7FFFFFFF, 0x00020000);
     const __amdgpu_buffer_rsrc_t rsD1 = __builtin_amdgcn_make_buffer_rsrc((void*)d1, (short)0, 0x7FFFFFFF, 0x00020000);
     const __amdgpu_buffer_rsrc_t rsD2 = __builtin_amdgcn_make_buffer_rsrc((void*)(P.color_rgb ? d0 : d2), (short)0, 0x7FFFFFFF, 0x00020000);
-#endif
 
     float* lut_s = reinterpret_cast<float*>(smem);
     // fill in source channel order (P.fill is in output plane order); fp32: LUT byte offsets
@@ -856,7 +853,7 @@ __global__ EVAM_STAGED_BOUNDS void evam_pp_staged(const SParams P) {
         else { s0 = xtab_s[Xv0].s0; s1 = xtab_s[Xv1].s1; }
         footprint_chunks(FMT, T::bpp, x0 + s0, x0 + s1, fsY, nY, fsC, nC);
     }
-    if (P.ablate & 128) return;  // diagnostics: prologue parameters only
+    if (kAblate & 128) return;  // diagnostics: prologue parameters only
     // per-lane column state for each of this wave's SPW 64-column segments (seg = wave + 4 j, or
     // wave % NSEGX for narrow tiles), filled once the first DMA is in flight: LDS byte offsets of the taps
     // inside a slot, weights
@@ -883,7 +880,7 @@ __global__ EVAM_STAGED_BOUNDS void evam_pp_staged(const SParams P) {
     // w stages row w >> 1, tap w & 1 of every plane. Otherwise the slots are dealt round-robin.
     const int dr = wave >> 1, dtap = wave & 1;
     auto issue = [&](int g, uint8_t* buf) -> int {
-        if (!cols || (P.ablate & 16)) return 0;
+        if (!cols || (kAblate & 16)) return 0;
         if constexpr (2 * R == 4) {
             const int Y = Y0 + g * R + dr;
             if (Y >= Y1) return 0;
@@ -974,35 +971,23 @@ __global__ EVAM_STAGED_BOUNDS void evam_pp_staged(const SParams P) {
             const int sO = (int)((uint32_t)(Y * P.DW) * (uint32_t)esz);
             n += 3;
             auto put = [&](const uint32_t (&v)[3]) {
-                if (P.ablate & 4) {
+                if (kAblate & 4) {
                     asm volatile("" :: "v"(v[0]), "v"(v[1]), "v"(v[2]));
                     return;
                 }
                 if (!xin[j]) return;  // lane 0 is in: the wave still issues all three stores
                 if constexpr (OUT == 1) {
                     const uint8_t* lb = reinterpret_cast<const uint8_t*>(lut_s);
-#ifdef EVAM_PP_ONE_DST
-                    __builtin_amdgcn_raw_buffer_store_b32(*reinterpret_cast<const uint32_t*>(lb + v[0]), rsD, xo[j], sO + po0, EVAM_PP_STORE_AUX);
-                    __builtin_amdgcn_raw_buffer_store_b32(*reinterpret_cast<const uint32_t*>(lb + 1024 + v[1]), rsD, xo[j], sO + pbytes, EVAM_PP_STORE_AUX);
-                    __builtin_amdgcn_raw_buffer_store_b32(*reinterpret_cast<const uint32_t*>(lb + 2048 + v[2]), rsD, xo[j], sO + po2, EVAM_PP_STORE_AUX);
-#else
                     __builtin_amdgcn_raw_buffer_store_b32(*reinterpret_cast<const uint32_t*>(lb + v[0]), rsD0, xo[j], sO, EVAM_PP_STORE_AUX);
                     __builtin_amdgcn_raw_buffer_store_b32(*reinterpret_cast<const uint32_t*>(lb + 1024 + v[1]), rsD1, xo[j], sO, EVAM_PP_STORE_AUX);
                     __builtin_amdgcn_raw_buffer_store_b32(*reinterpret_cast<const uint32_t*>(lb + 2048 + v[2]), rsD2, xo[j], sO, EVAM_PP_STORE_AUX);
-#endif
                 } else {
-#ifdef EVAM_PP_ONE_DST
-                    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v[0], rsD, xo[j], sO + po0, EVAM_PP_STORE_AUX);
-                    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v[1], rsD, xo[j], sO + pbytes, EVAM_PP_STORE_AUX);
-                    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v[2], rsD, xo[j], sO + po2, EVAM_PP_STORE_AUX);
-#else
                     __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v[0], rsD0, xo[j], sO, EVAM_PP_STORE_AUX);
                     __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v[1], rsD1, xo[j], sO, EVAM_PP_STORE_AUX);
                     __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v[2], rsD2, xo[j], sO, EVAM_PP_STORE_AUX);
-#endif
                 }
             };
-            if ((b0 | b1) == 0 || (P.ablate & 2)) {  // padding row (wave-uniform)
+            if ((b0 | b1) == 0 || (kAblate & 2)) {  // padding row (wave-uniform)
                 put(fillv);
                 continue;
             }
@@ -1115,7 +1100,7 @@ __global__ EVAM_STAGED_BOUNDS void evam_pp_staged(const SParams P) {
     }
     asm volatile("" ::: "memory");
     if constexpr (OUT == 1) {  // sections in source channel order (B, G, R): see compute
-        if (!(P.ablate & 32))   // diagnostics: 32 skips the LUT load
+        if (!(kAblate & 32))   // diagnostics: 32 skips the LUT load
             for (int i = tid; i < 768; i += kThreads) lut_s[i] = P.lut[P.color_rgb ? 512 - (i & ~255) + (i & 255) : i];
     }
 #pragma unroll
@@ -1133,7 +1118,7 @@ __global__ EVAM_STAGED_BOUNDS void evam_pp_staged(const SParams P) {
     }
     int bi = 0;                 // buffer of group g
     int bn = NBUF - 1;          // buffer of group g + NBUF - 1
-    if ((P.ablate & 64) && ngroups != -7) {  // diagnostics: prologue only
+    if ((kAblate & 64) && ngroups != -7) {  // diagnostics: prologue only
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         asm volatile("" :: "v"(lY0[0]), "v"(lC0[0]), "v"(wa[0]), "v"(lY1[0]), "v"(lC1[0]));
         return;
@@ -1191,7 +1176,6 @@ struct WParams {
     int wave_bytes;      // one wave's staging area (two buffers)
     int color_rgb;
     uint32_t fill;
-    int ablate;          // diagnostics only (EVAM_PP_ABLATE bits): 2 no pixel math, 4 no stores, 16 no DMA
 };
 
 typedef int evam_v2i __attribute__((ext_vector_type(2)));
@@ -1264,7 +1248,7 @@ __device__ __forceinline__ void store_off(const __amdgpu_buffer_rsrc_t rs, uint3
 //  * When both vertical taps read the same 4:2:0 chroma row, its BT.601 chroma terms are computed once.
 //  * Each channel of a row leaves as one PX-wide store per lane (dwordx4 for fp32 at PX = 4).
 template <int FMT, int OUT, int PX, bool REUSE>
-__global__ EVAM_KERNEL_BOUNDS void evam_pp_wave(const WParams P) {
+__global__ __launch_bounds__(kThreads) void evam_pp_wave(const WParams P) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     using T = FmtTraits<FMT>;
     constexpr bool kYUV = FMT == kNV12 || FMT == kI420;
@@ -1275,7 +1259,7 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_wave(const WParams P) {
     const int t = blockIdx.x;
     // the launch parameters of the prologue in one batch of scalar loads (one wait): without the empty
     // asm use, branches split them into dependent round trips ahead of the first DMA
-    asm volatile("" ::"s"(P.tiles_per_item), "s"(P.tiles_x), "s"(P.ytab), "s"(P.xtab), "s"(P.ablate), "s"(P.TH),
+    asm volatile("" ::"s"(P.tiles_per_item), "s"(P.tiles_x), "s"(P.ytab), "s"(P.xtab), "s"(P.TH),
                  "s"(P.DH), "s"(P.DW), "s"(P.ox), "s"(P.rw));
     const int item = t / P.tiles_per_item;
     const int tile = t - item * P.tiles_per_item;
@@ -1366,7 +1350,7 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_wave(const WParams P) {
         }
     };
     auto issue = [&](const Plan& q, uint8_t* buf) {
-        if (q.pad || (P.ablate & 16)) return;
+        if (q.pad || (kAblate & 16)) return;
         if (q.stA) {
             dma(rsY, buf, nY, q.ya * pitch0 + fsY);
             if constexpr (kYUV) dma(rsC, buf + oC0, nC, (q.ya >> 1) * pitch1 + fsC);
@@ -1461,8 +1445,8 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_wave(const WParams P) {
     };
 
     auto store_row = [&](int Y, const int (&v)[3][PX]) {
-        if (!xin || (P.ablate & 4)) {
-            if (P.ablate & 4) asm volatile("" :: "v"(v[0][0]), "v"(v[1][0]), "v"(v[2][0]));
+        if (!xin || (kAblate & 4)) {
+            if (kAblate & 4) asm volatile("" :: "v"(v[0][0]), "v"(v[1][0]), "v"(v[2][0]));
             return;
         }
         // Row offset in the VGPR offset, soffset 0. A >8-byte buffer store with an SGPR soffset is
@@ -1523,7 +1507,7 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_wave(const WParams P) {
         // Keep every DMA of row Y + 1 ahead of row Y's stores: the vmcnt(3) above relies on that order.
         asm volatile("" ::: "memory");
         int v[3][PX];
-        if (cur.pad || (P.ablate & 2)) {
+        if (cur.pad || (kAblate & 2)) {
 #pragma unroll
             for (int j = 0; j < PX; j++) { v[0][j] = fb0; v[1][j] = fo1; v[2][j] = fb2; }
         } else {
@@ -1573,6 +1557,283 @@ __global__ EVAM_KERNEL_BOUNDS void evam_pp_wave(const WParams P) {
     }
 }
 
+// ------------------------------------------------------------------------------------------------
+// strip kernel (uniform geometry, 4:2:0 sources, no shared source rows between output rows)
+// ------------------------------------------------------------------------------------------------
+constexpr int kMaxStrips = 32;  // per-strip footprints in the kernel arguments: DW <= 2048
+
+struct TParams {
+    ItemArg items[kArgItems];
+    double scale_x, scale_y;     // OpenCV: 1. / ((double)rw / cw), 1. / ((double)rh / ch)
+    const float* lut;            // [3][256]
+    void* dst;
+    int slot_offset, slot_stride;  // output slot of item i = slot_offset + i * slot_stride
+    int DW, DH;
+    int cw, ch, rw, rh, ox, oy;  // the launch's crop size, resized size and placement (uniform)
+    int nw;                      // waves (strips) per workgroup
+    int TH, tiles_x, tiles_per_item;  // tile = nw strips x TH rows
+    int segY, segC;              // bytes of one staged luma / chroma row segment (multiples of 16)
+    int grp_bytes, wave_bytes;   // one ring entry (one output row's segments); one wave's ring
+    int offBuf;                  // LDS offset of wave 0's ring (after the LUT)
+    int color_rgb;
+    uint32_t fill;
+    int xcd_remap;               // 1: consecutive tiles land on one XCD
+    int2 sfoot[kMaxStrips];      // per strip: crop-relative source columns of the first visible column's
+                                 // first tap and the last visible column's last tap; (-1, -1): padding only
+};
+
+// Row-strip kernel for uniform-geometry 4:2:0 batches whose output rows do not share source rows
+// (downscales: C2, C4, C5). Every wave owns one 64-column strip of a tile and walks the tile's rows
+// alone, one output row per step, with no workgroup barrier after the prologue:
+//  * a ring of D row entries per wave (two luma row segments, one or two chroma row segments: the strip's
+//    16-byte-aligned footprint) fed by LDS-DMA D rows ahead; the wait for a row is one counted vmcnt,
+//    so the ring's other rows and the stores of the previous rows stay in flight;
+//  * the OpenCV coefficient tables of the strip's columns (one per lane) and of the tile's rows (one per
+//    lane, read back with v_readlane) are computed in the prologue by the kernels' shared linear_coef, so
+//    the first DMA waits for no table load;
+//  * per pixel: four luma taps and two chroma taps per chroma row from LDS, BT.601 as saturating two-tap
+//    registers, the 11-bit horizontal pass as one v_dot2 per channel, VResizeLinear 32s->8u as mulhi_u24,
+//    the LUT (fp32) and three planar stores (lane = pixel).
+// Letterbox rows are plain fill stores outside the ring; letterbox columns are a per-lane select in the
+// strips that have any. D = ring depth (rows of DMA in flight).
+template <int FMT, int OUT, int D>
+__global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    static_assert(FMT == kNV12 || FMT == kI420, "4:2:0 sources");
+    static_assert(D >= 2 && D <= 4, "ring depth");
+    constexpr int NPC = FMT == kI420 ? 2 : 1;  // chroma planes
+    constexpr int NMIN = 2 + NPC;              // fewest DMA instructions of one row (chroma row shared)
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int p_nw = P.nw, p_tpi = P.tiles_per_item, p_tx = P.tiles_x, p_TH = P.TH, p_DH = P.DH, p_DW = P.DW;
+    const int p_grid = gridDim.x;
+    asm volatile("" ::"s"(p_nw), "s"(p_tpi), "s"(p_tx), "s"(p_TH), "s"(p_DH), "s"(p_DW), "s"(p_grid), "s"(P.xcd_remap),
+                 "s"(P.ox), "s"(P.rw), "s"(P.oy), "s"(P.rh), "s"(P.segY), "s"(P.segC), "s"(P.offBuf), "s"(P.wave_bytes));
+    const int t = P.xcd_remap ? xcd_tile(blockIdx.x, p_grid) : (int)blockIdx.x;
+    const int item = t / p_tpi;
+    const int tile = t - item * p_tpi;
+    const int ty = tile / p_tx;
+    const int strip = (tile - ty * p_tx) * p_nw + wave;
+    const int Y0 = ty * p_TH, Y1 = min(Y0 + p_TH, p_DH);
+    const ItemArg& it = P.items[item];
+    const uint8_t* p0 = it.plane[0];
+    const uint8_t* p1 = it.plane[1];
+    const uint8_t* p2 = it.plane[2];
+    const int pitch0 = it.pitch[0], pitch1 = it.pitch[1], pitch2 = it.pitch[2];
+    const int x0 = it.x0, y0 = it.y0;
+    const int X0 = strip * 64;
+    const bool live = X0 < p_DW;  // a wave past the last strip only joins the LUT barrier
+    const int2 sf = P.sfoot[min(strip, kMaxStrips - 1)];
+    asm volatile("" ::"s"(p0), "s"(p1), "s"(p2), "s"(pitch0), "s"(pitch1), "s"(pitch2), "s"(x0), "s"(y0),
+                 "s"(it.index), "s"(sf.x), "s"(sf.y), "s"(P.dst), "s"(P.slot_offset), "s"(P.slot_stride));
+    const bool cols = live && sf.x >= 0;
+    int fsY = 0, nY = 0, fsC = 0, nC = 0;
+    if (cols) footprint_chunks(FMT, 1, x0 + sf.x, x0 + sf.y, fsY, nY, fsC, nC);
+    // visible output rows of the tile (the rest are letterbox fill)
+    const int vr0 = max(Y0, P.oy), vr1 = min(Y1, P.oy + P.rh);
+    const int n = cols && vr1 > vr0 ? vr1 - vr0 : 0;
+
+    // row table, one visible row per lane: source rows relative to the crop, weights << 8
+    int lr0 = 0, lr1 = 0, lb0 = 0, lb1 = 0;
+    if (lane < n) {
+        int sy, b0, b1;
+        linear_coef(vr0 + lane - P.oy, P.scale_y, P.ch, false, sy, b0, b1);
+        lr0 = min(max(sy, 0), P.ch - 1);
+        lr1 = min(max(sy + 1, 0), P.ch - 1);
+        lb0 = b0 << 8;
+        lb1 = b1 << 8;
+    }
+    const __amdgpu_buffer_rsrc_t rsY = __builtin_amdgcn_make_buffer_rsrc((void*)p0, (short)0, 0x7FFFFFFF, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsU = __builtin_amdgcn_make_buffer_rsrc((void*)p1, (short)0, 0x7FFFFFFF, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsV = __builtin_amdgcn_make_buffer_rsrc((void*)(NPC == 2 ? p2 : p1), (short)0, 0x7FFFFFFF, 0x00020000);
+    uint8_t* const wbuf = smem + P.offBuf + wave * P.wave_bytes;
+    const int segY = P.segY, segC = P.segC, grp = P.grp_bytes;
+    // ring entry: [Y tap0][Y tap1][C tap0][C tap1] (+ [V tap0][V tap1] for I420)
+    auto issue = [&](int i, int k) {
+        const int L = i;  // lane of row vr0 + i in the row table
+        const int ya = y0 + __builtin_amdgcn_readlane(lr0, L), yb = y0 + __builtin_amdgcn_readlane(lr1, L);
+        uint8_t* e = wbuf + k * grp;
+        const uint32_t vo = (uint32_t)lane * 16u;
+        if (lane < nY) {
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsY, (__attribute__((address_space(3))) void*)e, 16, vo,
+                                                     ya * pitch0 + fsY, EVAM_PP_LOAD_AUX, 0);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsY, (__attribute__((address_space(3))) void*)(e + segY), 16, vo,
+                                                     yb * pitch0 + fsY, EVAM_PP_LOAD_AUX, 0);
+        }
+        const int ca = ya >> 1, cb = yb >> 1;
+        if (lane < nC) {
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsU, (__attribute__((address_space(3))) void*)(e + 2 * segY), 16, vo,
+                                                     ca * pitch1 + fsC, EVAM_PP_LOAD_AUX, 0);
+            if constexpr (NPC == 2)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rsV, (__attribute__((address_space(3))) void*)(e + 2 * segY + 2 * segC),
+                                                         16, vo, ca * pitch2 + fsC, EVAM_PP_LOAD_AUX, 0);
+        }
+        if (ca != cb && lane < nC) {
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsU, (__attribute__((address_space(3))) void*)(e + 2 * segY + segC), 16,
+                                                     vo, cb * pitch1 + fsC, EVAM_PP_LOAD_AUX, 0);
+            if constexpr (NPC == 2)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rsV, (__attribute__((address_space(3))) void*)(e + 2 * segY + 3 * segC),
+                                                         16, vo, cb * pitch2 + fsC, EVAM_PP_LOAD_AUX, 0);
+        }
+    };
+
+    // LUT loads first (oldest VMEM: the first row's wait covers them), then the ring's first D rows.
+    float lutv[3];
+    const int nthr = p_nw * 64;
+    const bool lut_early = nthr >= 256;  // three LUT entries per thread cover the 768
+    if constexpr (OUT == 1) {
+        if (lut_early)
+#pragma unroll
+        for (int q = 0; q < 3; q++) {
+            const int idx = threadIdx.x + q * nthr;
+            lutv[q] = idx < 768 ? P.lut[P.color_rgb ? 512 - (idx & ~255) + (idx & 255) : idx] : 0.f;
+        }
+    }
+    const int npro = min(n, D);
+    for (int i = 0; i < npro; i++) issue(i, i);
+
+    // per-lane column state: tap offsets inside the staged segments, packed 11-bit weights
+    const int X = X0 + lane;
+    const bool xin = live && X < p_DW;
+    uint32_t lY = 0, lC0 = 0, lC1 = 0, wp = 0;
+    bool padc = true;
+    if (cols) {
+        const int dx = X - P.ox;
+        if (xin && dx >= 0 && dx < P.rw) {
+            int s0, a0, a1;
+            linear_coef(dx, P.scale_x, P.cw, true, s0, a0, a1);
+            const int ca = x0 + s0;  // tap 1 reads ca + 1: at the right edge (s0 = cw - 1) its weight a1 is 0
+            lY = (uint32_t)(ca - fsY);
+            if constexpr (FMT == kNV12) {
+                lC0 = (uint32_t)(2 * (ca >> 1) - fsC);
+                lC1 = (uint32_t)(2 * ((ca + 1) >> 1) - fsC);
+            } else {
+                lC0 = (uint32_t)((ca >> 1) - fsC);
+                lC1 = (uint32_t)(((ca + 1) >> 1) - fsC);
+            }
+            wp = (uint32_t)a0 | ((uint32_t)a1 << 16);
+            padc = false;
+        }
+    }
+    // every lane of a strip visible (wave-uniform): no per-pixel fill select
+    const bool anypad = cols && __builtin_amdgcn_ballot_w64(xin && padc) != 0;
+
+    const size_t plane = (size_t)p_DW * p_DH;
+    const size_t esz = OUT == 1 ? 4 : 1;
+    uint8_t* const d0 = reinterpret_cast<uint8_t*>(P.dst) + (size_t)(P.slot_offset + it.index * P.slot_stride) * 3 * plane * esz;
+    uint8_t* const d1 = d0 + plane * esz;
+    uint8_t* const d2 = d1 + plane * esz;
+    // output planes in source channel order (B, G, R): planes 0 and 2 exchanged for RGB
+    const __amdgpu_buffer_rsrc_t rsO0 = __builtin_amdgcn_make_buffer_rsrc((void*)(P.color_rgb ? d2 : d0), (short)0, 0x7FFFFFFF, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsO1 = __builtin_amdgcn_make_buffer_rsrc((void*)d1, (short)0, 0x7FFFFFFF, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsO2 = __builtin_amdgcn_make_buffer_rsrc((void*)(P.color_rgb ? d0 : d2), (short)0, 0x7FFFFFFF, 0x00020000);
+    const uint32_t vo = (uint32_t)(xin ? X : 0) * (uint32_t)esz;
+    // fill in source channel order (P.fill is in output plane order)
+    const uint32_t fq0 = P.fill & 0xFF, fq1 = (P.fill >> 8) & 0xFF, fq2 = (P.fill >> 16) & 0xFF;
+    const uint32_t fsh = OUT == 1 ? 2 : 0;
+    const uint32_t fill0 = (P.color_rgb ? fq2 : fq0) << fsh, fill1 = fq1 << fsh, fill2 = (P.color_rgb ? fq0 : fq2) << fsh;
+
+    if constexpr (OUT == 1) {
+        float* lut_s = reinterpret_cast<float*>(smem);
+        if (lut_early) {
+            // the LUT loads landed once at most the ring's DMA instructions are outstanding
+            if (npro == D) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NMIN * D) : "memory");
+            else vmcnt_exact(NMIN * npro);
+#pragma unroll
+            for (int q = 0; q < 3; q++) {
+                const int idx = threadIdx.x + q * nthr;
+                if (idx < 768) lut_s[idx] = lutv[q];
+            }
+        } else {  // workgroups of 1-3 waves (outputs narrower than 193 columns)
+            for (int idx = threadIdx.x; idx < 768; idx += nthr)
+                lut_s[idx] = P.lut[P.color_rgb ? 512 - (idx & ~255) + (idx & 255) : idx];
+        }
+        __syncthreads();
+    }
+    if (!live) return;
+    const uint8_t* lutb = smem;
+    // v: LUT byte offsets (fp32) or bytes (u8), source channel order
+    auto put = [&](int Y, uint32_t v0, uint32_t v1, uint32_t v2) {
+        if (!xin) return;
+        const int so = (int)((uint32_t)(Y * p_DW) * (uint32_t)esz);
+        if constexpr (OUT == 1) {
+            __builtin_amdgcn_raw_buffer_store_b32(*reinterpret_cast<const uint32_t*>(lutb + v0), rsO0, vo, so, EVAM_PP_STORE_AUX);
+            __builtin_amdgcn_raw_buffer_store_b32(*reinterpret_cast<const uint32_t*>(lutb + 1024 + v1), rsO1, vo, so, EVAM_PP_STORE_AUX);
+            __builtin_amdgcn_raw_buffer_store_b32(*reinterpret_cast<const uint32_t*>(lutb + 2048 + v2), rsO2, vo, so, EVAM_PP_STORE_AUX);
+        } else {
+            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v0, rsO0, vo, so, EVAM_PP_STORE_AUX);
+            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v1, rsO1, vo, so, EVAM_PP_STORE_AUX);
+            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v2, rsO2, vo, so, EVAM_PP_STORE_AUX);
+        }
+    };
+    // letterbox rows above the ring: before its DMA in issue order, so they never enter the counted waits
+    const int ra = n ? vr0 : Y1;
+    for (int Y = Y0; Y < ra; Y++) put(Y, fill0, fill1, fill2);
+
+    auto ring = [&](auto has_pad) {
+        constexpr bool PADC = decltype(has_pad)::value;
+        int k = 0;  // ring entry of row i
+        for (int i = 0; i < n; i++) {
+            // row i's DMA landed: after it this wave issued the DMA of rows i+1 .. i+D-1 (>= NMIN each) and
+            // the stores of rows i-D+1 .. i-1 (3 each)
+            if (i >= D - 1 && i + D - 1 < n) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 1) * (NMIN + 3)) : "memory");
+            else vmcnt_exact(NMIN * (min(i + D - 1, n - 1) - i) + 3 * min(i, D - 1));
+            const int Y = vr0 + i;
+            const uint32_t wb0 = (uint32_t)__builtin_amdgcn_readlane(lb0, i), wb1 = (uint32_t)__builtin_amdgcn_readlane(lb1, i);
+            const int ya = __builtin_amdgcn_readlane(lr0, i), yb = __builtin_amdgcn_readlane(lr1, i);
+            const bool share = ((y0 + ya) >> 1) == ((y0 + yb) >> 1);
+            const uint8_t* e = wbuf + k * grp;
+            const uint8_t* sy0 = e + lY;
+            const uint8_t* sy1 = e + segY + lY;
+            const uint8_t* sc0 = e + 2 * segY;
+            const uint8_t* sc1 = share ? sc0 : sc0 + segC;
+            UVs tA, tB;
+            auto chroma = [&](const uint8_t* sc, uint32_t o) -> UVs {
+                if constexpr (FMT == kNV12) {
+                    const uint32_t uv = *reinterpret_cast<const uint16_t*>(sc + o);
+                    return uv_terms_sat(uv & 0xFF, uv >> 8);
+                } else {
+                    return uv_terms_sat(sc[o], sc[2 * segC + o]);
+                }
+            };
+            tA = chroma(sc0, lC0);
+            tB = chroma(sc0, lC1);
+            const uint32_t yA = luma_term(sy0[0]), yB = luma_term(sy0[1]);
+            const uint32_t yC = luma_term(sy1[0]), yD = luma_term(sy1[1]);
+            uint32_t h0[3], h1[3];
+            h0[0] = hpass_sat(yA, tA.b, yB, tB.b, wp);
+            h0[1] = hpass_sat(yA, tA.g, yB, tB.g, wp);
+            h0[2] = hpass_sat(yA, tA.r, yB, tB.r, wp);
+            if (share) {
+                h1[0] = hpass_sat(yC, tA.b, yD, tB.b, wp);
+                h1[1] = hpass_sat(yC, tA.g, yD, tB.g, wp);
+                h1[2] = hpass_sat(yC, tA.r, yD, tB.r, wp);
+            } else {
+                const UVs tC = chroma(sc1, lC0), tE = chroma(sc1, lC1);
+                h1[0] = hpass_sat(yC, tC.b, yD, tE.b, wp);
+                h1[1] = hpass_sat(yC, tC.g, yD, tE.g, wp);
+                h1[2] = hpass_sat(yC, tC.r, yD, tE.r, wp);
+            }
+            uint32_t v[3];
+#pragma unroll
+            for (int c = 0; c < 3; c++) v[c] = vfinal<OUT>(h0[c], h1[c], wb0, wb1);
+            if constexpr (PADC) {
+                v[0] = padc ? fill0 : v[0];
+                v[1] = padc ? fill1 : v[1];
+                v[2] = padc ? fill2 : v[2];
+            }
+            put(Y, v[0], v[1], v[2]);
+            asm volatile("" ::: "memory");  // the stores stay ahead of the next DMA (counted waits)
+            if (i + D < n) issue(i + D, k);  // this entry's reads are done: the stores consumed them
+            asm volatile("" ::: "memory");
+            k = k + 1 == D ? 0 : k + 1;
+        }
+    };
+    if (anypad) ring(std::true_type{});
+    else ring(std::false_type{});
+    // letterbox rows below the ring
+    for (int Y = max(ra, vr1); Y < Y1; Y++) put(Y, fill0, fill1, fill2);
+}
 
 static_assert(sizeof(evam_roi) == 20, "evam_roi layout");
 
@@ -1595,11 +1856,6 @@ static_assert(sizeof(RoiRec) == 64, "RoiRec layout");
 #define EVAM_PP_ROI_K 6
 #endif
 constexpr int kRoiK = EVAM_PP_ROI_K;  // max pixels per lane per row group in the ROI kernel
-#ifdef EVAM_PP_ROI_ALU_NORM
-constexpr bool kRoiAluNorm = true;    // fp32 normalisation in the ALU (PX 1), no LDS LUT
-#else
-constexpr bool kRoiAluNorm = false;
-#endif
 
 struct QParams {
     const RoiRec* recs;       // this launch's ROI tiles in launch order (largest work first)
@@ -1613,12 +1869,6 @@ struct QParams {
     int buf_bytes;            // one staging buffer
     int color_rgb;
     uint32_t fill;
-    int ablate;               // diagnostics only (EVAM_PP_ABLATE bits): 2 no pixel math, 4 no stores, 16 no DMA,
-                              // 32 stop after setup, 64 stop after geometry, 128 return at entry
-    // EVAM_PP_ROI_ALU_NORM builds: the normalisation in the reference operation order, per SOURCE channel
-    // (B, G, R; swapped for RGB like the planes), instead of the LDS LUT
-    float na, nb, nm[3], ns[3];
-    int nflags;
 };
 
 // Diagnostic builds only (-DEVAM_PP_TRACE, tools/roi_timeline.py): per-workgroup timestamps of the
@@ -1687,9 +1937,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(96))) void
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     // the parameters of the prologue in one batch of scalar loads, so the record's PCIe read below is not
     // queued behind a kernarg round trip for the diagnostics test
-    asm volatile("" ::"s"(P.ablate), "s"(P.recs), "s"(P.lut), "s"(P.color_rgb), "s"(P.mode), "s"(P.placement),
+    asm volatile("" ::"s"(P.recs), "s"(P.lut), "s"(P.color_rgb), "s"(P.mode), "s"(P.placement),
                  "s"(P.DW), "s"(P.DH));
-    if (P.ablate & 128) return;  // diagnostics: launch cost only
+    if (kAblate & 128) return;  // diagnostics: launch cost only
     EVAM_STAMP(0);
     // The whole 64-byte record in one scalar load, issued first: it is a PCIe read from pinned host
     // memory (~1-2 us under load), and field-by-field loads became up to three dependent round trips
@@ -1698,7 +1948,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(96))) void
     const u32x16 rec = *((const __attribute__((address_space(4))) u32x16*)(P.recs) + blockIdx.x);
     // The LUT is loaded once per workgroup, whatever number of units it processes.
     float* lut_s = reinterpret_cast<float*>(smem);
-    if constexpr (OUT == 1 && !(kRoiAluNorm && PX == 1)) {
+    if constexpr (OUT == 1) {
 #pragma unroll
         // sections in source channel order (B, G, R): RGB output swaps the B / R output planes instead
         // of the values (see rsD0 / rsD2), so the per-pixel path carries no swap
@@ -1732,7 +1982,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(96))) void
     const int ox = __builtin_amdgcn_readfirstlane(g.ox), oy = __builtin_amdgcn_readfirstlane(g.oy);
     EVAM_STAMP(1);
     // diagnostics: stop after the geometry (64) / after the per-lane setup (32)
-    if ((P.ablate & 64) && rw != -7) return;
+    if ((kAblate & 64) && rw != -7) return;
     const double scx = 1. / ((double)rw / cw), scy = 1. / ((double)rh / ch);
     const size_t plane = (size_t)P.DW * P.DH;
     const size_t esz = OUT == 1 ? 4 : 1;
@@ -1829,7 +2079,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(96))) void
         return cnt;
     };
     auto issue = [&](int grp, uint8_t* buf) -> int {
-        if (nY == 0 || (P.ablate & 16)) return 0;  // no visible columns: every pixel is fill
+        if (nY == 0 || (kAblate & 16)) return 0;  // no visible columns: every pixel is fill
         const int nr = min(R, rows - grp * R);
         int cnt = issue_plane(grp, buf, nr, nY, mY, 0);
         if constexpr (NP >= 2) cnt += issue_plane(grp, buf + offC, nr, nC, mC, 1);
@@ -1897,7 +2147,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(96))) void
         EVAM_TRACE_VAL(6, (unsigned long long)xcc | ((unsigned long long)hw << 32));
     }
 #endif
-    if ((P.ablate & 32) && ngroups != -7) {
+    if ((kAblate & 32) && ngroups != -7) {
         asm volatile("" :: "v"(lY[0][0]), "v"(lC[0][0]), "v"(wa[0][0]), "v"(rr[0]), "s"(mY), "s"(mC));
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // group 0's DMA lands before the LDS is released
         return;
@@ -1911,7 +2161,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(96))) void
             const int ly = grp * R + rr[k];
             if (rr[k] < 0 || ly >= rows) continue;
             const YTab e = yt[ly];
-            const bool padrow = (e.b0 | e.b1) == 0 || (P.ablate & 2);  // letterbox padding row
+            const bool padrow = (e.b0 | e.b1) == 0 || (kAblate & 2);  // letterbox padding row
             const uint8_t* sy0 = buf + 2 * rr[k] * segY;
             const uint8_t* sy1 = sy0 + segY;
             const uint8_t* sc0 = buf + offC + 2 * rr[k] * segC;
@@ -1987,20 +2237,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(96))) void
             // soffset 0: the row offset is in voffset (a > 8-byte store with an SGPR soffset misses
             // the compiler's store-data hazard wait on gfx950, see evam_pp_wave)
             const uint32_t vo = (gbase + (uint32_t)(tid + k * kThreads) * PX) * (uint32_t)esz;
-            if (P.ablate & 4) {
+            if (kAblate & 4) {
                 asm volatile("" :: "v"(v[0][0]), "v"(v[1][0]), "v"(v[2][0]));
-                continue;
-            }
-            if constexpr (kRoiAluNorm && OUT == 1 && PX == 1) {  // (the PX 4 variant keeps the LUT)
-                auto nrm = [&](uint32_t v4, int c) -> uint32_t {
-                    float x = (float)(v4 >> 2);
-                    if (P.nflags & 1) { x = __fmul_rn(x, P.na); x = __fadd_rn(x, P.nb); }
-                    if (P.nflags & 2) { x = __fsub_rn(x, P.nm[c]); x = __fdiv_rn(x, P.ns[c]); }
-                    return __float_as_uint(x);
-                };
-                __builtin_amdgcn_raw_buffer_store_b32(nrm(v[0][0], 0), rsD0, vo, 0, EVAM_PP_STORE_AUX);
-                __builtin_amdgcn_raw_buffer_store_b32(nrm(v[1][0], 1), rsD1, vo, 0, EVAM_PP_STORE_AUX);
-                __builtin_amdgcn_raw_buffer_store_b32(nrm(v[2][0], 2), rsD2, vo, 0, EVAM_PP_STORE_AUX);
                 continue;
             }
             const uint8_t* lb = reinterpret_cast<const uint8_t*>(lut_s);
@@ -2128,8 +2366,10 @@ struct Knobs {
     int roi_th = -1, roi_buf = -1, roi_px = 1, roi_sort = 1, roi_xcd = 0;  // roi_buf -1: sized for one round
     int roi_unit = 0;                              // ROI work-unit size in row groups (0: one unit per base tile)
     int roi_nbuf = 2;                              // ROI staging buffers (3: two groups of DMA in flight)
-    int ablate = 0;                                // stage-removal diagnostics (results invalid)
+    int strip = 1, strip_th = -1, strip_d = -1, strip_nw = -1;  // strip kernel: allowed, rows per tile, ring depth, waves
     void read() {
+        strip = env_int("EVAM_PP_STRIP", strip); strip_th = env_int("EVAM_PP_STRIP_TH", strip_th);
+        strip_d = env_int("EVAM_PP_STRIP_D", strip_d); strip_nw = env_int("EVAM_PP_STRIP_NW", strip_nw);
         staged = env_int("EVAM_PP_STAGED", staged); wave = env_int("EVAM_PP_WAVE", wave);
         rows = env_int("EVAM_PP_ROWS", rows); roi = env_int("EVAM_PP_ROI", roi);
         th = env_int("EVAM_PP_TH", th); tw = env_int("EVAM_PP_TW", tw); xcd = env_int("EVAM_PP_XCD", xcd);
@@ -2141,7 +2381,6 @@ struct Knobs {
         roi_px = env_int("EVAM_PP_ROI_PX", roi_px); roi_sort = env_int("EVAM_PP_ROI_SORT", roi_sort);
         roi_xcd = env_int("EVAM_PP_ROI_XCD", roi_xcd); roi_unit = env_int("EVAM_PP_ROI_UNIT", roi_unit);
         roi_nbuf = env_int("EVAM_PP_ROI_NBUF", roi_nbuf);
-        ablate = env_int("EVAM_PP_ABLATE", ablate);
     }
 };
 
@@ -2456,6 +2695,107 @@ bool plan_wave(int f, const Geom& g, int DW, int DH, int count, int out_dtype, i
 }
 
 template <int FMT, int OUT>
+const void* strip_fn_t(int d) {
+    return d == 4 ? (const void*)evam_pp_strip<FMT, OUT, 4>
+                  : (d == 3 ? (const void*)evam_pp_strip<FMT, OUT, 3> : (const void*)evam_pp_strip<FMT, OUT, 2>);
+}
+const void* strip_fn(int f, int out, int d) {
+    switch (f * 2 + out) {
+    case kNV12 * 2 + 0: return strip_fn_t<kNV12, 0>(d);
+    case kNV12 * 2 + 1: return strip_fn_t<kNV12, 1>(d);
+    case kI420 * 2 + 0: return strip_fn_t<kI420, 0>(d);
+    default: return strip_fn_t<kI420, 1>(d);
+    }
+}
+
+// Strip-kernel plan for a uniform 4:2:0 group (fills everything in TParams but the items, LUT, output
+// and colour fields). Waves per workgroup: 4..8 strips with the fewest idle waves. Ring depth D: the
+// deepest (<= 4) whose LDS still admits the workgroups that fill a CU's 32 wave slots. Tile height:
+// one round of workgroups over the chip (a second round repeats every wave's ring fill at the tail),
+// at most 64 rows (the lane-held row table). Returns false when the geometry does not suit it: outputs
+// wider than kMaxStrips strips, footprints over 1 KB per 64 columns, or consecutive output rows that
+// share source rows (vertical upscales: the wave kernel's REUSE path).
+bool plan_strip(int f, const Geom& g, int DW, int DH, int count, int out_dtype, int n_cu, const XTab* xt,
+                const YTab* yt, uint32_t x0_mask, const Knobs& kn, TParams& p, int& D, int& lds, int& grid) {
+    if (f != kNV12 && f != kI420) return false;
+    const int nstrips = (DW + 63) / 64;
+    if (nstrips > kMaxStrips) return false;
+    int shared = 0, vis = 0;
+    for (int Y = 0; Y + 1 < DH; Y++) {
+        const bool pad0 = (yt[Y].b0 | yt[Y].b1) == 0, pad1 = (yt[Y + 1].b0 | yt[Y + 1].b1) == 0;
+        if (pad0 || pad1) continue;
+        vis++;
+        shared += yt[Y + 1].r0 <= yt[Y].r1;
+    }
+    if (kn.strip != 2 && shared * 8 > vis) return false;  // more than 1 in 8 rows re-stages a row
+    if (!x0_mask) x0_mask = 1u << (g.x0 & 31);
+    int mY = 0, mC = 0;
+    wave_segments(f, g.ox, g.rw, DW, xt, x0_mask, 64, mY, mC);
+    if (mY > 64 || mC > 64) return false;
+    const int npc = f == kI420 ? 2 : 1;
+    p.segY = 16 * std::max(1, mY);
+    p.segC = 16 * std::max(1, mC);
+    p.grp_bytes = 2 * p.segY + 2 * npc * p.segC;
+    int nw = 4, best = 1 << 30;
+    for (int c = 4; c <= 8; c++) {
+        const int idle = (nstrips + c - 1) / c * c - nstrips;
+        if (idle < best) { best = idle; nw = c; }
+    }
+    if (nstrips < 4) nw = nstrips;
+    if (kn.strip_nw > 0) nw = std::min(8, kn.strip_nw);
+    p.nw = nw;
+    p.tiles_x = (nstrips + nw - 1) / nw;
+    p.offBuf = out_dtype == EVAM_DTYPE_F32 ? kLutBytes : 0;
+    const int wg_target = std::max(1, 32 / nw);
+    D = 2;
+    for (int d : {4, 3, 2}) {
+        if (p.offBuf + nw * d * p.grp_bytes + 16 <= (160 * 1024) / wg_target) { D = d; break; }
+    }
+    if (kn.strip_d >= 2 && kn.strip_d <= 4) D = kn.strip_d;
+    p.wave_bytes = D * p.grp_bytes;
+    lds = p.offBuf + nw * p.wave_bytes + 16;  // + 16: a right-edge tap reads one byte past its footprint (weight 0)
+    if (lds > 64 * 1024) return false;
+    const int res = std::max(1, resident_per_cu(strip_fn(f, out_dtype, D), lds));
+    const int64_t slots = (int64_t)n_cu * res;
+    const int64_t work = (int64_t)count * p.tiles_x * DH;
+    int th = (int)std::max<int64_t>(1, (work + slots - 1) / slots);
+    th = std::max(th, std::min(DH, D));
+    if (kn.strip_th > 0) th = kn.strip_th;
+    p.TH = std::max(1, std::min(std::min(DH, 64), th));
+    p.tiles_per_item = p.tiles_x * ((DH + p.TH - 1) / p.TH);
+    p.DW = DW; p.DH = DH;
+    p.cw = g.cw; p.ch = g.ch; p.rw = g.rw; p.rh = g.rh; p.ox = g.ox; p.oy = g.oy;
+    p.scale_x = 1. / ((double)g.rw / g.cw);
+    p.scale_y = 1. / ((double)g.rh / g.ch);
+    for (int s = 0; s < kMaxStrips; s++) {
+        const int Xv0 = std::max(s * 64, g.ox), Xv1 = std::min(std::min(s * 64 + 64, DW), g.ox + g.rw) - 1;
+        p.sfoot[s] = s < nstrips && Xv0 <= Xv1 ? int2{xt[Xv0].s0, xt[Xv1].s1} : int2{-1, -1};
+    }
+    const int64_t gr = (int64_t)std::min(count, kArgItems) * p.tiles_per_item;
+    if (gr > 0x7FFFFFFF) return false;
+    grid = (int)gr;
+    return true;
+}
+
+template <int FMT, int OUT>
+hipError_t launch_strip_t(int d, const TParams& p, int grid, int lds, hipStream_t s) {
+    const dim3 blk(64 * p.nw);
+    if (d == 4) hipLaunchKernelGGL((evam_pp_strip<FMT, OUT, 4>), dim3(grid), blk, lds, s, p);
+    else if (d == 3) hipLaunchKernelGGL((evam_pp_strip<FMT, OUT, 3>), dim3(grid), blk, lds, s, p);
+    else hipLaunchKernelGGL((evam_pp_strip<FMT, OUT, 2>), dim3(grid), blk, lds, s, p);
+    return hipGetLastError();
+}
+
+hipError_t launch_strip(int f, int out, int d, const TParams& p, int grid, int lds, hipStream_t s) {
+    switch (f * 2 + out) {
+    case kNV12 * 2 + 0: return launch_strip_t<kNV12, 0>(d, p, grid, lds, s);
+    case kNV12 * 2 + 1: return launch_strip_t<kNV12, 1>(d, p, grid, lds, s);
+    case kI420 * 2 + 0: return launch_strip_t<kI420, 0>(d, p, grid, lds, s);
+    default: return launch_strip_t<kI420, 1>(d, p, grid, lds, s);
+    }
+}
+
+template <int FMT, int OUT>
 const void* roi_fn_t(int px, int nb) {
     return px == 4 ? (const void*)evam_pp_roi<FMT, OUT, 4, 2>
                    : (nb == 3 ? (const void*)evam_pp_roi<FMT, OUT, 1, 3> : (const void*)evam_pp_roi<FMT, OUT, 1, 2>);
@@ -2493,7 +2833,7 @@ bool plan_roi(int f, int DW, int DH, int out_dtype, int px, int max_row_bytes, i
     q.TH = (int64_t)DW * DH <= 32768 ? DH : std::max(8, std::min(DH, 16384 / DW));
     if (kn.roi_th > 0) q.TH = std::max(1, std::min(DH, kn.roi_th));
     base_tiles = (DH + q.TH - 1) / q.TH;
-    q.offXT = out_dtype == EVAM_DTYPE_F32 && !(kRoiAluNorm && !(px == 4 && DW % 4 == 0)) ? kLutBytes : 0;
+    q.offXT = out_dtype == EVAM_DTYPE_F32 ? kLutBytes : 0;
     q.offYT = q.offXT + (int)sizeof(XTab) * DW;
     q.offBuf = q.offYT + (int)sizeof(YTab) * q.TH;
     const int64_t grid = (int64_t)count * base_tiles;
@@ -2589,6 +2929,7 @@ struct evam_pp {
     std::vector<int> sc_members;   // item indices grouped by source format
     std::vector<Geom> sc_geo;
     std::vector<int> sc_units;     // ROI work units: (item, row0, row1, cost)
+    TParams sc_tparams;            // strip-kernel arguments (3.5 KB: kept off the stack)
 };
 
 namespace {
@@ -2727,6 +3068,13 @@ const char* evam_pp_last_error(void) { return g_last_error.c_str(); }
 int evam_pp_create(int hip_device, void* hip_stream, evam_pp** out) {
     if (!out) return fail(EVAM_PP_ERR_INVALID_ARG, "evam_pp_create: out is NULL");
     *out = nullptr;
+    if (kAblate != 0) {  // a stage-removal diagnostic build computes invalid tensors: never by accident
+        const char* ok = getenv("EVAM_PP_DIAGNOSTIC_BUILD_OK");
+        if (!ok || strcmp(ok, "1") != 0)
+            return fail(EVAM_PP_ERR_UNSUPPORTED, "evam_pp_create: diagnostic build (EVAM_PP_ABLATE=%d) refused; "
+                        "set EVAM_PP_DIAGNOSTIC_BUILD_OK=1 for profiling runs", kAblate);
+        fprintf(stderr, "[evam_pp] DIAGNOSTIC BUILD (EVAM_PP_ABLATE=%d): outputs are invalid\n", kAblate);
+    }
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n <= 0)
         return fail(EVAM_PP_ERR_NO_DEVICE, "evam_pp_create: no HIP device");
@@ -3174,15 +3522,6 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
             q.slot_stride = dst->slot_stride;
             q.color_rgb = color_rgb;
             q.fill = fill;
-            q.ablate = kn.ablate;
-            q.na = (float)(((double)cfg->range[1] - (double)cfg->range[0]) / 255.0);
-            q.nb = cfg->range[0];
-            for (int c = 0; c < 3; c++) {
-                const int oc = color_rgb ? 2 - c : c;  // source channel c lands in output plane oc
-                q.nm[c] = cfg->mean[oc];
-                q.ns[c] = cfg->std[oc];
-            }
-            q.nflags = cfg->norm_flags;
             const int64_t grid = qrec[f];
             if (grid > 0x7FFFFFFF) return fail(EVAM_PP_ERR_INVALID_ARG, "evam_pp_run: too many tiles");
             hipError_t e = launch_roi(f, cfg->out_dtype, kn.roi_px, kn.roi_nbuf, q, (int)grid, qlds[f], h->stream);
@@ -3195,6 +3534,32 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
             const XTab* xt_d = reinterpret_cast<const XTab*>(d_block + tab_off[f]);
             const YTab* yt_d = reinterpret_cast<const YTab*>(xt_d + DW);
             const int per_launch = std::min(count[f], kArgItems);
+            if (kn.strip && kn.wave != 2) {
+                TParams* tp = &h->sc_tparams;
+                int D = 0, lds = 0, grid = 0;
+                const XTab* hx = reinterpret_cast<const XTab*>(h->h_block.data() + tab_off[f]);
+                if (plan_strip(f, g0, DW, DH, count[f], cfg->out_dtype, h->n_cu, hx, reinterpret_cast<const YTab*>(hx + DW),
+                               x0_mask[f], kn, *tp, D, lds, grid)) {
+                    tp->lut = lut_d;
+                    tp->dst = dst->data;
+                    tp->slot_offset = dst->slot_offset;
+                    tp->slot_stride = dst->slot_stride;
+                    tp->color_rgb = color_rgb;
+                    tp->fill = fill;
+                    for (int m0 = mfirst[f]; m0 < mfirst[f + 1]; m0 += kArgItems) {
+                        const int nm = std::min(kArgItems, mfirst[f + 1] - m0);
+                        fill_args(tp->items, m0, nm);
+                        const int64_t gr = (int64_t)nm * tp->tiles_per_item;
+                        // XCD-contiguous tiles: the strips of one row band share source lines at their edges
+                        tp->xcd_remap = kn.xcd >= 0 ? kn.xcd : (int)(gr >= 8 * (int64_t)h->n_cu);
+                        hipError_t e = launch_strip(f, cfg->out_dtype, D, *tp, (int)gr, lds, h->stream);
+                        if (e != hipSuccess) return fail(EVAM_PP_ERR_HIP, "kernel launch failed: %s", hipGetErrorString(e));
+                        launches++;
+                    }
+                    (void)grid;
+                    continue;
+                }
+            }
             if (kn.wave) {
                 WParams w{};
                 int px = 0, lds = 0, grid = 0;
@@ -3215,7 +3580,6 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
                     w.slot_stride = dst->slot_stride;
                     w.color_rgb = color_rgb;
                     w.fill = fill;
-                    w.ablate = kn.ablate;
                     for (int m0 = mfirst[f]; m0 < mfirst[f + 1]; m0 += kArgItems) {
                         const int n = std::min(kArgItems, mfirst[f + 1] - m0);
                         fill_args(w.items, m0, n);
@@ -3285,7 +3649,6 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
                 }
                 sp.color_rgb = color_rgb;
                 sp.fill = fill;
-                sp.ablate = kn.ablate;
                 const int lds = sp.offBuf + nbuf * sp.buf_bytes;
                 for (int m0 = mfirst[f]; m0 < mfirst[f + 1]; m0 += kArgItems) {
                     const int n = std::min(kArgItems, mfirst[f + 1] - m0);
@@ -3318,7 +3681,6 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
             r.nsegx = rc.TW / 64;
             r.color_rgb = color_rgb;
             r.fill = fill;
-            r.ablate = kn.ablate;
             const int lds = cfg->out_dtype == EVAM_DTYPE_F32 ? kLutBytes : 0;
             for (int m0 = mfirst[f]; m0 < mfirst[f + 1]; m0 += kArgItems) {
                 const int n = std::min(kArgItems, mfirst[f + 1] - m0);
@@ -3351,7 +3713,6 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
         p.offCol = t.offCol; p.offRow = t.offRow;
         p.color_rgb = color_rgb;
         p.fill = fill;
-        p.ablate = kn.ablate;
         const int lds = t.lds;
         if (lds > 64 * 1024) {
             hipError_t e = hipSuccess;

@@ -37,6 +37,7 @@ device ``Image``s, or host planes uploaded on arrival.
 """
 from __future__ import annotations
 
+import collections
 import gc
 import itertools
 import json
@@ -454,9 +455,10 @@ class DeviceRunner:
     def __init__(self, hub: "BatchHub"):
         self.hub = hub
         self._pipes: list = []
+        self._draining: list = []  # ended pipelines whose destination still holds back results (queue full)
         self._cv = threading.Condition()
         self._stop = False
-        self._thread = threading.Thread(target=self._loop, name=f"evam-runner-{hub.device}", daemon=True)
+        self._thread = threading.Thread(target=self._guarded_loop, name=f"evam-runner-{hub.device}", daemon=True)
         self._thread.start()
 
     def add(self, pipe):
@@ -472,27 +474,73 @@ class DeviceRunner:
             self._cv.notify_all()
         self._thread.join(10)
 
+    def _guarded_loop(self):
+        """The runner thread. Whatever escapes the loop (a bug, not a stream's error: those fail only their
+        own pipeline) fails every pipeline the runner still holds, so no ``wait()`` blocks on a dead thread."""
+        try:
+            self._loop()
+        except BaseException as e:  # noqa: BLE001
+            with self._cv:
+                pipes, self._pipes = list(self._pipes), []
+                self._stop = True
+            for p in pipes:
+                p._fail(e)
+
+    def _drain(self):
+        """Hand held-back results to destinations that have room again; forget the pipelines that are done."""
+        keep = []
+        for p in self._draining:
+            try:
+                if not p._flush_out():
+                    keep.append(p)
+            except Exception:  # noqa: BLE001 — the destination itself failed: nothing left to deliver to
+                pass
+        self._draining = keep
+
+    def _finish(self, p, e=None):
+        """End pipeline ``p`` (``e``: its error), isolated from the other pipelines of the device."""
+        try:
+            if e is not None:
+                p._fail(e)
+            else:
+                p._end()
+        except Exception as e2:  # noqa: BLE001 — a destination that raised on end of stream
+            p.error, p.state = f"{type(e2).__name__}: {e2}", p.ERROR
+            p._done.set()
+        if p._out_backlog:
+            self._draining.append(p)
+
     def _loop(self):
         hub = self.hub
         idle = 0.0005
         while True:
             with self._cv:
-                while not self._pipes and not self._stop:
+                while not self._pipes and not self._draining and not self._stop:
                     self._cv.wait()
                 if self._stop and not self._pipes:
+                    self._drain()  # shutdown: what a full destination still cannot take is dropped
                     return
                 pipes = list(self._pipes)
+            if self._draining:
+                self._drain()
             ready, oldest, total, done = [], None, 0, []
             for p in pipes:
+                if p._out_backlog:
+                    try:
+                        p._flush_out()
+                    except Exception as e:  # noqa: BLE001
+                        self._finish(p, e)
+                        done.append(p)
+                        continue
                 try:
                     p._ingest()
                 except Exception as e:  # noqa: BLE001 — reported through status(), as the reference does
-                    p._fail(e)
+                    self._finish(p, e)
                     done.append(p)
                     continue
                 n = len(p._pend) - p._head
                 if p._stop.is_set() or (p._eos and not n):
-                    p._end()
+                    self._finish(p)
                     done.append(p)
                 elif n >= p._batch or p._eos:
                     ready.append(p)
@@ -539,7 +587,7 @@ class DeviceRunner:
                         continue
                     w, units = st.prepare(items)
                 except Exception as e:  # noqa: BLE001
-                    p._fail(e)
+                    self._finish(p, e)
                     failed.add(p)
                     continue
                 if units > 0:
@@ -560,15 +608,26 @@ class DeviceRunner:
                             del hub.batches[:2048]
                     except Exception as e:  # noqa: BLE001 — delivered to every pipeline of the batch
                         for p, _ in chunk:
-                            p._fail(e)
+                            self._finish(p, e)
                             failed.add(p)
                         continue
                     for p, r in chunk:
                         if p not in failed:
-                            r.stage.finish(r.items)
+                            try:
+                                r.stage.finish(r.items)
+                            except Exception as e:  # noqa: BLE001 — this stream's bookkeeping only
+                                self._finish(p, e)
+                                failed.add(p)
         for p, items in work:
             if p not in failed:
-                p._emit_all(items)
+                try:
+                    p._emit_all(items)
+                except Exception as e:  # noqa: BLE001 — this stream's destination only
+                    self._finish(p, e)
+                    failed.add(p)
+        if failed:
+            with self._cv:
+                self._pipes = [p for p in self._pipes if p not in failed]
 
 
 class _InferenceStage:
@@ -579,10 +638,11 @@ class _InferenceStage:
     requests of all pipelines sharing ``hub_key()``.
     """
 
-    def __init__(self, el: Element, server, device: int):
+    def __init__(self, el: Element, server, device: int, slot: int = 0):
         self.el = el
         self.backend = _backend_of(el)
         self.device = device
+        self.slot = slot  # the pipeline's logical device: its BatchHub / DeviceRunner
         self.server = server
         net = el.properties.get("model") or el.properties.get("enc-model")
         self.model = server.model_for(net)
@@ -614,7 +674,7 @@ class _InferenceStage:
     def process(self, items):
         """Thread runner: gate, hand the work to the device's BatchHub (blocks until its batch ran), finish."""
         work, units = self.prepare(items)
-        self.server.hub().submit(self, work, units)
+        self.server.hub(self.slot).submit(self, work, units)
         self.finish(work)
 
     def hub_key(self):
@@ -681,12 +741,13 @@ class ClassifyStage(_InferenceStage):
     results are attached again. Untracked regions (object_id 0) are classified on every gated frame.
     """
 
-    def __init__(self, el, server, device):
-        super().__init__(el, server, device)
+    def __init__(self, el, server, device, slot=0):
+        super().__init__(el, server, device, slot)
         oc = el.properties.get("object-class")
         self.object_class = set(str(oc).split(",")) if oc else None
         self.reclassify = max(1, int(el.properties.get("reclassify-interval", 1)))
         self._cache: dict = {}   # object_id -> (frame index classified at, tensors)
+        self._deferred: list = []  # (region, region of an earlier frame of this call it takes results from)
 
     def _make_hub_key(self):
         oc = tuple(sorted(self.object_class)) if self.object_class else None
@@ -694,6 +755,8 @@ class ClassifyStage(_InferenceStage):
 
     def prepare(self, items):
         work = []          # (frame_index, Image, [regions to classify])
+        sched = {}         # object_id -> (frame index, region) classified by this call
+        self._deferred = []
         for fi, img, fr in items:
             if fi % self.interval:
                 continue
@@ -708,6 +771,12 @@ class ClassifyStage(_InferenceStage):
                     if hit is not None and fi - hit[0] < self.reclassify:
                         r.tensors.extend(hit[1])
                         continue
+                    # an earlier frame of this same call classifies the object: its results, once run
+                    s = sched.get(r.object_id)
+                    if s is not None and fi - s[0] < self.reclassify:
+                        self._deferred.append((r, s[1]))
+                        continue
+                    sched[r.object_id] = (fi, r)
                 todo.append(r)
             if todo:
                 work.append((fi, img, todo))
@@ -719,6 +788,9 @@ class ClassifyStage(_InferenceStage):
                 for r in todo:
                     if r.object_id:
                         self._cache[r.object_id] = (fi, [t for t in r.tensors if t.model == self.model.name])
+            for r, src in self._deferred:
+                r.tensors.extend(t for t in src.tensors if t.model == self.model.name)
+            self._deferred = []
             if len(self._cache) > 65536:
                 self._cache.clear()
 
@@ -764,8 +836,8 @@ class ActionRecognitionStage(_InferenceStage):
     CLIP = 16
     batchable = False
 
-    def __init__(self, el, server, device):
-        super().__init__(el, server, device)
+    def __init__(self, el, server, device, slot=0):
+        super().__init__(el, server, device, slot)
         self.ring = None
         self.t = 0
         dec = el.properties.get("dec-model")
@@ -846,6 +918,10 @@ class Pipeline:
         self._batch = 1
         self._done = threading.Event()
         self._runner = False
+        self._out_backlog = collections.deque()  # runner mode: results a full destination queue could not take
+        # logical device: pipeline k of the server runs on devices[(k - 1) mod G] (streams partitioned over GPUs)
+        self.slot = server.slot_for(instance_id)
+        self.device = server.devices[self.slot]
 
     # -- construction ------------------------------------------------------------------------
     def build(self, source=None, parameters=None):
@@ -874,7 +950,7 @@ class Pipeline:
     def start(self, source=None, destination=None, parameters=None):
         """Build the element graph, instantiate the HIP stages, and run the frame loop in a thread."""
         self.build(source, parameters)
-        self.stages = [STAGES[e.factory](e, self.server, self.server.device)
+        self.stages = [STAGES[e.factory](e, self.server, self.device, self.slot)
                        for e in self.elements if e.factory in STAGES]
         self.source = source or {}
         self.destination = destination or {}
@@ -887,7 +963,7 @@ class Pipeline:
             self._runner = True
             self._batch = max([getattr(s, "batch_size", 1) for s in self.stages] + [1])
             self._pend_t0 = time.perf_counter()
-            self.server.runner().add(self)
+            self.server.runner(self.slot).add(self)
         return self.id
 
     # -- device-runner side (called on the DeviceRunner thread only) ----------------------------------
@@ -907,7 +983,7 @@ class Pipeline:
         room = self.kIngest - backlog
         if kind == "application":
             q = src.get("input")
-            if isinstance(q, queue.Queue):
+            if type(q) is queue.Queue:  # FIFO deque inside; subclasses (LIFO, priority, custom _get) go item by item
                 with q.mutex:
                     d = q.queue
                     if len(d) <= room:
@@ -979,7 +1055,7 @@ class Pipeline:
         self.end_time = time.time()
         dst = self.destination.get("metadata", self.destination)
         if dst.get("output") is not None:
-            dst["output"].put(None)
+            self._put(dst["output"], None)
         self._done.set()
 
     def _frames(self):
@@ -1015,7 +1091,7 @@ class Pipeline:
             return item
         if isinstance(item, dict):         # host frame {fourcc, width, height, planes}
             return Image.from_host(item["fourcc"], item["width"], item["height"], item["planes"],
-                                   device=f"cuda:{self.server.device}")
+                                   device=f"cuda:{self.device}")
         raise TypeError(f"unsupported frame object {type(item).__name__}")
 
     def _emit(self, fr: P.FrameResult, img):
@@ -1024,10 +1100,39 @@ class Pipeline:
         mode = dst.get("mode", "frames")
         if out is None:
             return
-        if mode == "frames":
-            out.put((img, fr))
+        item = (img, fr) if mode == "frames" else P.gvametaconvert_json(fr)
+        if self._runner:
+            self._put(out, item)
         else:
-            out.put(P.gvametaconvert_json(fr))
+            out.put(item)  # threads mode: a full queue blocks this stream's own thread only
+
+    def _put(self, out, item):
+        """Runner mode: never block the device's shared runner on one stream's destination. A full bounded
+        queue keeps the results (in order) in this pipeline's backlog; the runner retries them."""
+        if not self._runner or not hasattr(out, "put_nowait"):
+            out.put(item)
+            return
+        if self._out_backlog:  # keep the order: behind what is already held back
+            self._out_backlog.append(item)
+            self._flush_out()
+            return
+        try:
+            out.put_nowait(item)
+        except queue.Full:
+            self._out_backlog.append(item)
+
+    def _flush_out(self) -> bool:
+        """Move backlog results into the destination while it has room; True when none are left."""
+        dst = self.destination.get("metadata", self.destination)
+        out = dst.get("output")
+        b = self._out_backlog
+        while b:
+            try:
+                out.put_nowait(b[0])
+            except queue.Full:
+                return False
+            b.popleft()
+        return True
 
     def _run(self):
         try:
@@ -1092,27 +1197,35 @@ class _Server:
         self.instances: list[Pipeline] = []
         self.started = False
         self.device = 0
-        self._hub = None
-        self._runner = None
+        self.devices = [0]      # logical devices: pipeline k runs on devices[(k - 1) % len(devices)]
+        self._hubs: dict = {}    # logical device -> BatchHub
+        self._runners: dict = {}  # logical device -> DeviceRunner
         self._gc_saved = None
         self._hub_lock = threading.Lock()
 
-    def hub(self) -> BatchHub:
-        """The device's batching hub (created on first use; options ``batch_max``, ``batch_wait_ms``,
-        ``batch_target``)."""
-        with self._hub_lock:
-            if self._hub is None:
-                o = self.options
-                self._hub = BatchHub(self.device, max_batch=int(o.get("batch_max", 64)),
-                                     max_wait_s=float(o.get("batch_wait_ms", 2.0)) / 1e3,
-                                     target=o.get("batch_target"))
-            return self._hub
+    def slot_for(self, instance_id: int) -> int:
+        """Logical device of pipeline instance ``instance_id`` (1-based): streams s -> GPU s mod G
+        (SURVEY.md §8e), the same partition bench.py and streams.py apply across ranks."""
+        return (int(instance_id) - 1) % len(self.devices)
 
-    def runner(self) -> DeviceRunner:
-        """The device's pipeline runner (created on first use; it batches through the hub's limits)."""
-        hub = self.hub()
+    def hub(self, slot: int = 0) -> BatchHub:
+        """The batching hub of logical device ``slot`` (created on first use; options ``batch_max``,
+        ``batch_wait_ms``, ``batch_target``). Each one owns its own pre-processing handle and stream."""
         with self._hub_lock:
-            if self._runner is None:
+            h = self._hubs.get(slot)
+            if h is None:
+                o = self.options
+                h = self._hubs[slot] = BatchHub(self.devices[slot], max_batch=int(o.get("batch_max", 64)),
+                                                max_wait_s=float(o.get("batch_wait_ms", 2.0)) / 1e3,
+                                                target=o.get("batch_target"))
+            return h
+
+    def runner(self, slot: int = 0) -> DeviceRunner:
+        """The pipeline runner of logical device ``slot`` (created on first use; it batches through that
+        device's hub)."""
+        hub = self.hub(slot)
+        with self._hub_lock:
+            if not self._runners and self._gc_saved is None:
                 self._gc_saved = (gc.get_threshold(), False)
                 if self.options.get("gc_freeze", True):
                     # The heap built so far (torch, models, templates) leaves the collector's generations:
@@ -1125,28 +1238,37 @@ class _Server:
                     # Per-frame records die by reference count, never in cycles; collecting them every 700
                     # allocations (the default) cost as much as the rest of the runner at 32 streams.
                     gc.set_threshold(*gct)
-                self._runner = DeviceRunner(hub)
-            return self._runner
+            r = self._runners.get(slot)
+            if r is None:
+                r = self._runners[slot] = DeviceRunner(hub)
+            return r
 
     def close_hub(self):
         with self._hub_lock:
-            if self._runner is not None:
-                self._runner.close()
-                self._runner = None
-                if self._gc_saved is not None:  # the process's collector settings, as before the runner
-                    thresholds, frozen = self._gc_saved
-                    gc.set_threshold(*thresholds)
-                    if frozen:
-                        gc.unfreeze()
-                    self._gc_saved = None
-            if self._hub is not None:
-                self._hub.close()
-                self._hub = None
+            for r in self._runners.values():
+                r.close()
+            self._runners = {}
+            if self._gc_saved is not None:  # the process's collector settings, as before the runners
+                thresholds, frozen = self._gc_saved
+                gc.set_threshold(*thresholds)
+                if frozen:
+                    gc.unfreeze()
+                self._gc_saved = None
+            for h in self._hubs.values():
+                h.close()
+            self._hubs = {}
 
     def start(self, options=None):
         o = dict(options or {})
         self.options = o
         self.device = int(o.get("device", os.environ.get("EVAM_HIP_DEVICE", 0)))
+        devs = o.get("devices")
+        if devs is None and os.environ.get("EVAM_HIP_DEVICES"):
+            devs = [int(x) for x in os.environ["EVAM_HIP_DEVICES"].split(",") if x.strip()]
+        self.devices = [int(d) for d in devs] if devs else [self.device]
+        if not self.devices:
+            raise ValueError("PipelineServer.start: 'devices' must name at least one device")
+        self.device = self.devices[0]
         pdir = o.get("pipeline_dir") or os.environ.get("PIPELINE_DIR", "pipelines")
         mdir = o.get("model_dir") or os.environ.get("MODEL_DIR", "models")
         self.models = scan_models(mdir)
@@ -1240,6 +1362,11 @@ class PipelineServer:
         _SERVER.started = False
 
     @staticmethod
-    def hub():
-        """The per-device batching hub (inspection: ``hub().batches``)."""
-        return _SERVER.hub()
+    def hub(slot: int = 0):
+        """The batching hub of logical device ``slot`` (inspection: ``hub().batches``)."""
+        return _SERVER.hub(slot)
+
+    @staticmethod
+    def devices():
+        """The logical devices pipelines are partitioned over (option ``devices``; default ``[device]``)."""
+        return list(_SERVER.devices)

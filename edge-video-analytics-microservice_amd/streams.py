@@ -34,6 +34,15 @@ def local_batch(frames_by_stream, world: int, rank: int) -> list:
     return [frames_by_stream[s] for s in streams_for_rank(len(frames_by_stream), world, rank)]
 
 
+def device_key(local_device: int) -> int:
+    """Identity of a physical device across ranks: host and local device index (ranks that share a GPU in a
+    rehearsal share a key)."""
+    import socket
+    import zlib
+
+    return (zlib.crc32(socket.gethostname().encode()) << 8) | (int(local_device) & 0xFF)
+
+
 @dataclass
 class RunTotals:
     world: int
@@ -41,29 +50,32 @@ class RunTotals:
     frames: int               # frames processed by all ranks
     alg_bytes: int            # algorithmic bytes moved by all ranks
     per_rank_frames: list
+    devices: int = 1          # distinct physical devices over the ranks (device_key), not the rank count
 
     @property
     def frames_per_s(self) -> float:
         return self.frames / self.elapsed_max_s if self.elapsed_max_s > 0 else 0.0
 
 
-def reduce_run(elapsed_s: float, frames: int, alg_bytes: int, device=None) -> RunTotals:
-    """Combine one timed region across ranks: max elapsed, summed counters.
+def reduce_run(elapsed_s: float, frames: int, alg_bytes: int, device=None, device_key: int = 0) -> RunTotals:
+    """Combine one timed region across ranks: max elapsed, summed counters, distinct devices.
 
     Call it on every rank after the timed region. It is never used inside the hot loop. With
     ``torch.distributed`` uninitialised (a single process), it returns this process's numbers.
     ``device`` is where the small exchange tensors live: a CUDA device for RCCL, CPU for gloo.
+    ``device_key``: this rank's physical device (``device_key()``); ranks sharing a GPU count once.
     """
     import torch
     import torch.distributed as dist
 
     if not (dist.is_available() and dist.is_initialized()):
-        return RunTotals(1, float(elapsed_s), int(frames), int(alg_bytes), [int(frames)])
+        return RunTotals(1, float(elapsed_s), int(frames), int(alg_bytes), [int(frames)], 1)
     world = dist.get_world_size()
     el = torch.tensor([float(elapsed_s)], dtype=torch.float64, device=device)
     dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    mine = torch.tensor([int(frames), int(alg_bytes)], dtype=torch.int64, device=device)
+    mine = torch.tensor([int(frames), int(alg_bytes), int(device_key)], dtype=torch.int64, device=device)
     allst = [torch.zeros_like(mine) for _ in range(world)]
     dist.all_gather(allst, mine)
     per = [int(t[0].item()) for t in allst]
-    return RunTotals(world, float(el.item()), sum(per), sum(int(t[1].item()) for t in allst), per)
+    devs = len({int(t[2].item()) for t in allst})
+    return RunTotals(world, float(el.item()), sum(per), sum(int(t[1].item()) for t in allst), per, devs)

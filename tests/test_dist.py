@@ -21,7 +21,7 @@ def test_partition_disjoint_and_complete(evam):
 
 def test_reduce_run_single_process(evam):
     t = evam.streams.reduce_run(0.5, 32, 1000)
-    assert (t.world, t.frames, t.alg_bytes) == (1, 32, 1000)
+    assert (t.world, t.frames, t.alg_bytes, t.devices) == (1, 32, 1000, 1)
     assert t.frames_per_s == 64.0
 
 
@@ -42,8 +42,11 @@ def _worker(rank, world, port, q):
         evam = g.import_package()
         streams = evam.streams.streams_for_rank(64, world, rank)
         # per-rank "work": 32 frames of this rank's streams, elapsed differs per rank
-        t = evam.streams.reduce_run(elapsed_s=1.0 + rank, frames=len(streams), alg_bytes=100 * len(streams))
-        q.put((rank, t.world, t.elapsed_max_s, t.frames, t.alg_bytes, t.per_rank_frames))
+        t = evam.streams.reduce_run(elapsed_s=1.0 + rank, frames=len(streams), alg_bytes=100 * len(streams),
+                                    device_key=evam.streams.device_key(rank))
+        # two ranks on one device (a rehearsal): counted as one GPU
+        shared = evam.streams.reduce_run(1.0, 1, 1, device_key=evam.streams.device_key(0))
+        q.put((rank, t.world, t.elapsed_max_s, t.frames, t.alg_bytes, t.per_rank_frames, t.devices, shared.devices))
     finally:
         dist.destroy_process_group()
 
@@ -61,8 +64,9 @@ def test_reduce_run_gloo_world2():
         p.join(120)
         assert p.exitcode == 0
     res = sorted(q.get(timeout=10) for _ in range(2))
-    for rank, world, el, frames, nbytes, per in res:
+    for rank, world, el, frames, nbytes, per, devs, shared_devs in res:
         assert world == 2
+        assert devs == 2 and shared_devs == 1
         assert el == 2.0                 # max over ranks
         assert frames == 64 and nbytes == 6400
         assert per == [32, 32]

@@ -48,21 +48,28 @@ def _run(world, config, tmp_path, streams=8):
     return res
 
 
-@pytest.mark.parametrize("config", ["c2", "c4"])
+@pytest.mark.parametrize("config", ["c2", "c4", "c5"])
 def test_two_ranks_match_single_process(gpu, tmp_path, config):
+    """C2 / C4 frames and C5 clip rings (each stream's 16-slot ring lives on its owner rank)."""
     single = _run(1, config, tmp_path)
     (meta1, s1, out1), = single
-    assert list(s1) == list(range(8)) and meta1["frames"] == 8
-    by_stream = {int(s): out1[i] for i, s in enumerate(s1)}
+    ring = meta1["ring"]
+    steps = 3 if ring > 1 else 1
+    assert list(s1) == list(range(8)) and meta1["frames"] == 8 * steps
+    assert meta1["devices"] == 1
+    by_stream = {int(s): out1[i * ring:(i + 1) * ring] for i, s in enumerate(s1)}
     two = _run(2, config, tmp_path)
     seen = []
     for meta, streams, out in two:
-        assert meta["world"] == 2
-        assert meta["frames"] == 8 and meta["per_rank_frames"] == [4, 4]
+        assert meta["world"] == 2 and meta["devices"] == 1       # two ranks, one physical GPU
+        assert meta["frames"] == 8 * steps and meta["per_rank_frames"] == [4 * steps, 4 * steps]
         assert meta["alg_bytes"] == meta1["alg_bytes"]           # summed over ranks == single process
         assert list(streams) == list(range(meta["rank"], 8, 2))  # s mod 2 ownership
         for i, s in enumerate(streams):
-            a, b = out[i], by_stream[int(s)]
+            a, b = out[i * ring:(i + 1) * ring], by_stream[int(s)]
             assert (a.view(np.uint32) == b.view(np.uint32)).all(), f"{config} stream {s} rank {meta['rank']}"
             seen.append(int(s))
     assert sorted(seen) == list(range(8))
+    if ring > 1:  # slots no step wrote keep their initial value; slots 0 and 1 were written
+        r = by_stream[0]
+        assert (r[5] == 7.0).all() and not (r[0] == 7.0).all() and not (r[1] == 7.0).all()

@@ -362,12 +362,14 @@ def test_stats_and_timing(evam, O, gpu):
     ((480, 270), (224, 224), "aspect-crop"),        # C5 shape: central crop
 ])
 @pytest.mark.parametrize("variant", ["auto", "wave", "px1", "px2", "noreuse", "staged", "staged_xcd", "staged_r1",
-                                     "staged_wide", "staged_b3", "staged_slot2k"])
+                                     "staged_wide", "staged_b3", "staged_slot2k", "strip", "strip_d2", "strip_d3",
+                                     "strip_th5", "strip_nw8", "strip_xcd"])
 def test_wave_kernel_variants(evam, O, coracle, gpu, fmt, src, dst, resize, variant, monkeypatch):
     """Uniform-geometry batches through the default kernel choice, the wave-row kernel forced
-    (EVAM_PP_WAVE=2; every PX / REUSE choice) and the staged kernel (EVAM_PP_WAVE=0; with the
-    XCD-contiguous tile order forced on small, non-multiple-of-8 grids: EVAM_PP_XCD=1), RGB order, fp32
-    with normalisation and u8."""
+    (EVAM_PP_WAVE=2; every PX / REUSE choice), the staged kernel (EVAM_PP_WAVE=0 EVAM_PP_STRIP=0; with the
+    XCD-contiguous tile order forced on small, non-multiple-of-8 grids: EVAM_PP_XCD=1) and the strip kernel
+    (EVAM_PP_STRIP=2: forced even where output rows share source rows; every ring depth, an odd tile height,
+    8 waves per workgroup, XCD order), RGB order, fp32 with normalisation and u8."""
     import torch
 
     env = {"wave": {"EVAM_PP_WAVE": "2"}, "px1": {"EVAM_PP_WAVE": "2", "EVAM_PP_PX": "1"},
@@ -376,7 +378,14 @@ def test_wave_kernel_variants(evam, O, coracle, gpu, fmt, src, dst, resize, vari
            "staged_r1": {"EVAM_PP_WAVE": "0", "EVAM_PP_STAGE_R": "1"},
            "staged_wide": {"EVAM_PP_WAVE": "0", "EVAM_PP_NSEGX": "8"},
            "staged_b3": {"EVAM_PP_WAVE": "0", "EVAM_PP_STAGE_NBUF": "3"},
-           "staged_slot2k": {"EVAM_PP_WAVE": "0", "EVAM_PP_WIDE_SLOT": "1"}}.get(variant, {})
+           "staged_slot2k": {"EVAM_PP_WAVE": "0", "EVAM_PP_WIDE_SLOT": "1"},
+           "strip": {"EVAM_PP_STRIP": "2"}, "strip_d2": {"EVAM_PP_STRIP": "2", "EVAM_PP_STRIP_D": "2"},
+           "strip_d3": {"EVAM_PP_STRIP": "2", "EVAM_PP_STRIP_D": "3"},
+           "strip_th5": {"EVAM_PP_STRIP": "2", "EVAM_PP_STRIP_TH": "5"},
+           "strip_nw8": {"EVAM_PP_STRIP": "2", "EVAM_PP_STRIP_NW": "8"},
+           "strip_xcd": {"EVAM_PP_STRIP": "2", "EVAM_PP_XCD": "1", "EVAM_PP_STRIP_TH": "3"}}.get(variant, {})
+    if variant.startswith("staged"):
+        env["EVAM_PP_STRIP"] = "0"
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     if variant == "px2" and dst[0] % 2:
@@ -474,7 +483,7 @@ def test_roi_kernel_xcd_order(evam, O, coracle, gpu, fmt, monkeypatch):
 
 
 @pytest.mark.parametrize("fmt", FORMATS)
-@pytest.mark.parametrize("variant", ["wave", "staged"])
+@pytest.mark.parametrize("variant", ["wave", "staged", "strip"])
 def test_uniform_rois_varied_x0(evam, O, coracle, gpu, fmt, variant, monkeypatch):
     """Equal-size ROIs (one uniform-geometry group) at crop origins covering every x0 mod 32 residue, upscaled
     so the wave kernel's REUSE path runs: its LDS row segments must hold the widest 16-byte-aligned footprint
@@ -482,6 +491,7 @@ def test_uniform_rois_varied_x0(evam, O, coracle, gpu, fmt, variant, monkeypatch
     import torch
 
     monkeypatch.setenv("EVAM_PP_WAVE", "2" if variant == "wave" else "0")
+    monkeypatch.setenv("EVAM_PP_STRIP", "2" if variant == "strip" else "0")
     rng = np.random.default_rng(zlib.crc32(f"x0{fmt}".encode()))
     W, H = 256, 120
     frames = [O.random_frame(rng, fc(O, fmt), W, H, pattern="gradient" if i else "uniform") for i in range(2)]
@@ -553,6 +563,7 @@ def test_staged_many_tile_columns(evam, O, coracle, gpu, fmt, monkeypatch):
     import torch
 
     monkeypatch.setenv("EVAM_PP_WAVE", "0")
+    monkeypatch.setenv("EVAM_PP_STRIP", "0")
     monkeypatch.setenv("EVAM_PP_NSEGX", "2")  # 128-column tiles: 2200 / 128 -> 18 tile columns
     rng = np.random.default_rng(zlib.crc32(f"tcol{fmt}".encode()))
     frames = [O.random_frame(rng, fc(O, fmt), 2400, 64, pattern=p) for p in ("uniform", "gradient")]

@@ -178,3 +178,98 @@ def test_runner_restores_collector_settings(stubbed):
     assert gc.get_threshold() == (20000, 100, 1000) and gc.get_freeze_count() > 0
     ps.PipelineServer.stop()
     assert gc.get_threshold() == before and gc.get_freeze_count() == 0
+
+
+class _BadOut:
+    """A destination whose put fails (a consumer's bug)."""
+
+    def put(self, item):
+        raise OSError("destination gone")
+
+    def put_nowait(self, item):
+        raise OSError("destination gone")
+
+
+def _start(ps, pre, n, out, batch=2):
+    qin = queue.Queue()
+    for im in frames(pre, n):
+        qin.put(im)
+    qin.put(None)
+    p = ps.PipelineServer.pipeline("detect_classify", "hip")
+    p.start(source={"type": "application", "input": qin},
+            destination={"metadata": {"type": "application", "output": out, "mode": "json"}},
+            parameters={"detection-properties": {"batch-size": batch}})
+    return p
+
+
+def _drain(q, timeout=10):
+    got = []
+    while (x := q.get(timeout=timeout)) is not None:
+        got.append(x)
+    return got
+
+
+def test_runner_isolates_a_failing_destination(stubbed):
+    """an exception from one pipeline's destination fails that pipeline only; the device's other
+    pipelines (same runner thread, same launches) complete and deliver every frame."""
+    ps, pre, mdir = stubbed
+    ps.PipelineServer.start({"pipeline_dir": PIPES, "model_dir": mdir, "batch_max": 8, "batch_target": 4})
+    register(ps)
+    good_q = queue.Queue()
+    bad = _start(ps, pre, 6, _BadOut())
+    good = _start(ps, pre, 6, good_q)
+    assert bad.wait(30)["state"] == "ERROR" and "destination gone" in bad.status()["message"]
+    assert good.wait(30)["state"] == "COMPLETED"
+    assert len(_drain(good_q)) == 6
+
+
+def test_runner_full_destination_does_not_stall_others(stubbed):
+    """A bounded destination queue nobody reads must not block the runner that serves every stream of the
+    device: its results wait in that pipeline's backlog (in order) while the other streams complete."""
+    ps, pre, mdir = stubbed
+    ps.PipelineServer.start({"pipeline_dir": PIPES, "model_dir": mdir, "batch_max": 8, "batch_target": 4})
+    register(ps)
+    slow_q, fast_q = queue.Queue(maxsize=1), queue.Queue()
+    slow = _start(ps, pre, 9, slow_q)
+    fast = _start(ps, pre, 9, fast_q)
+    assert fast.wait(30)["state"] == "COMPLETED"
+    assert len(_drain(fast_q)) == 9
+    assert slow.wait(30)["state"] == "COMPLETED"
+    got = _drain(slow_q)  # the runner hands the held-back results over as the queue empties
+    assert [json.loads(x)["timestamp"] for x in got] == list(range(9))
+
+
+def test_runner_partitions_streams_over_devices(stubbed):
+    """Option ``devices``: pipeline k runs on devices[(k - 1) mod G] with that logical device's own hub and
+    runner (streams partitioned over GPUs); the default stays one device (manager.py's call)."""
+    ps, pre, mdir = stubbed
+    ps.PipelineServer.start({"pipeline_dir": PIPES, "model_dir": mdir, "devices": [0, 1], "batch_max": 8,
+                             "batch_target": 4, "batch_wait_ms": 100})
+    register(ps)
+    outs = [queue.Queue() for _ in range(4)]
+    pipes = [_start(ps, pre, 4, q) for q in outs]
+    assert [p.slot for p in pipes] == [0, 1, 0, 1] and [p.device for p in pipes] == [0, 1, 0, 1]
+    assert ps.PipelineServer.devices() == [0, 1]
+    for p, q in zip(pipes, outs):
+        assert p.wait(30)["state"] == "COMPLETED"
+        assert len(_drain(q)) == 4
+    for slot in (0, 1):
+        b = ps.PipelineServer.hub(slot).batches
+        assert sum(x[1] for x in b if x[0][0] == "gvadetect") == 8   # two streams of 4 frames each
+    assert ps.PipelineServer.hub(0) is not ps.PipelineServer.hub(1)
+
+
+def test_runner_survives_an_internal_error(stubbed, monkeypatch):
+    """Whatever escapes the runner loop fails every pipeline it holds (their wait() returns) instead of
+    leaving them RUNNING behind a dead thread."""
+    ps, pre, mdir = stubbed
+    ps.PipelineServer.start({"pipeline_dir": PIPES, "model_dir": mdir})
+    register(ps)
+
+    def boom(self, work):
+        raise RuntimeError("runner bug")
+
+    monkeypatch.setattr(ps.DeviceRunner, "_tick", boom)
+    p = _start(ps, pre, 4, queue.Queue())
+    st = p.wait(30)
+    assert st["state"] == "ERROR" and "runner bug" in st["message"]

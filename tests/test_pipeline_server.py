@@ -375,11 +375,14 @@ def test_hub_batches_across_pipelines(ps, evam, model_dir, gpu, O):
     ps.PipelineServer.stop()
 
 
-def test_classify_reclassify_interval(ps, evam):
+@pytest.mark.parametrize("per_call", [1, 7, 4])
+def test_classify_reclassify_interval(ps, evam, per_call):
     """gvaclassify reclassify-interval (pipelines/object_classification/vehicle_attributes/pipeline.json:68-71):
     a tracked region (object_id != 0) is sent for classification only every N-th frame of its stream and gets
     its last results attached in between; untracked regions are classified every frame; degenerate boxes are
-    never sent (the C ABI would read w/h <= 0 as the full frame)."""
+    never sent (the C ABI would read w/h <= 0 as the full frame). per_call: frames handed to one prepare()
+    (the device runner passes a stream's whole batch): frames of one call that fall inside the interval of
+    an earlier frame of the same call take that frame's results."""
     P = evam.postproc
 
     class FakeHub:
@@ -400,7 +403,7 @@ def test_classify_reclassify_interval(ps, evam):
         def model_for(self, net):
             return ps.InferenceModel(None, (24, 24), {"input_preproc": []}, name="cls")
 
-        def hub(self):
+        def hub(self, slot=0):
             return hub
 
     el = ps.Element("gvaclassify", {"model": "m.xml", "reclassify-interval": "3", "object-class": "car"})
@@ -412,12 +415,15 @@ def test_classify_reclassify_interval(ps, evam):
     def region(oid, x=10, w=40, label="car"):
         return P.Region(x, 10, w, 30, (0, 0, 0.1, 0.1), label, 1, 0.9, object_id=oid)
 
-    results = []
+    results, call = [], []
     for fi in range(7):
         fr = P.FrameResult(320, 180, regions=[region(5), region(0), region(6, label="person"), region(7, x=400),
                                              region(8, w=0)])
-        st.process([(fi, Img(), fr)])
+        call.append((fi, Img(), fr))
         results.append(fr)
+        if len(call) == per_call or fi == 6:
+            st.process(call)
+            call = []
     tracked = [fi for fi, oid in hub.sent if oid == 5]
     untracked = [fi for fi, oid in hub.sent if oid == 0]
     assert tracked == [0, 3, 6] and untracked == list(range(7))

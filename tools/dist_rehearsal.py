@@ -25,7 +25,7 @@ sys.path.insert(0, ROOT)
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--config", default="c2", choices=["c2", "c4"])
+    ap.add_argument("--config", default="c2", choices=["c2", "c4", "c5"])
     ap.add_argument("--streams", type=int, default=8)
     ap.add_argument("--out", required=True)
     args = ap.parse_args()
@@ -47,25 +47,36 @@ def main():
 
     wl = bench.WORKLOADS[args.config]
     mine = evam.streams.streams_for_rank(args.streams, world, rank)
-    # every stream's frame depends only on the stream id, so any partition sees the same bytes
-    imgs = [bench.device_frames(evam, torch, wl, 1, device, seed=100 + s)[0] for s in mine]
     DW, DH = wl["dst"]
-    out = torch.empty((len(mine), 3, DH, DW), dtype=torch.float32, device=device)
+    ring = wl.get("ring")
     pp = evam.HipPreProcessor(device=local)
     pp.set_option(evam.native.OPT_STATS, 1)
+    info = bench.make_info(evam, wl)
+    # C5: each owned stream keeps its own 16-slot clip ring on this rank (rings partitioned over ranks); the
+    # rehearsal runs steps t = 0, 1 and 17 (slot 1 written twice: the later frame wins), every step's
+    # frame a function of (stream, t) only, so any partition sees the same bytes
+    steps = (0, 1, 17) if ring else (0,)
+    out = torch.full((len(mine) * (ring or 1), 3, DH, DW), 7.0, dtype=torch.float32, device=device)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    if mine:
-        pp.convert(imgs, out, bench.make_info(evam, wl))
+    alg = 0
+    for t in steps:
+        imgs = [bench.device_frames(evam, torch, wl, 1, device, seed=100 + s + 1000 * t)[0] for s in mine]
+        if mine:
+            if ring:
+                pp.convert(imgs, out, info, slot_offset=t % ring, slot_stride=ring)
+            else:
+                pp.convert(imgs, out, info)
+            st = pp.stats()
+            alg += int(st.src_bytes + st.dst_bytes)
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    st = pp.stats()
-    alg = int(st.src_bytes + st.dst_bytes) if mine else 0
-    tot = evam.streams.reduce_run(elapsed, len(mine), alg)
+    tot = evam.streams.reduce_run(elapsed, len(mine) * len(steps), alg, device_key=evam.streams.device_key(local))
     np.savez(args.out, streams=np.array(mine, dtype=np.int64), out=out.cpu().numpy())
     print(json.dumps({"rank": rank, "world": tot.world, "frames": tot.frames, "alg_bytes": tot.alg_bytes,
                       "per_rank_frames": tot.per_rank_frames, "elapsed_max_s": tot.elapsed_max_s,
-                      "my_streams": mine, "device": local}), flush=True)
+                      "my_streams": mine, "device": local, "devices": tot.devices, "ring": ring or 1}),
+          flush=True)
     pp.close()
     if world > 1:
         dist.destroy_process_group()

@@ -1,6 +1,8 @@
 #!/bin/bash
-# rocprofv3 kernel durations of the default workload under EVAM_PP_ABLATE settings (diagnostics: the
-# ablated launches compute invalid results). Usage: tools/prof_ablate.sh TAG CFG "0 22 86" [extra bench args]
+# rocprofv3 kernel durations of a workload under stage-removal diagnostic builds (the ablated launches
+# compute INVALID results). Build the variants first, on the CPU side:
+#   for a in 2 4 16; do tools/build_variant.sh abl$a "-DEVAM_PP_ABLATE=$a"; done
+# Usage: tools/prof_ablate.sh TAG CFG "0 2 4 16" [extra bench args]   (0 = the product library)
 set -euo pipefail
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 OUT="$ROOT/gpurun_out"; mkdir -p "$OUT"
@@ -9,7 +11,8 @@ export TMPDIR=/tmp
 cd /tmp
 for a in $ABL; do
   d="$OUT/profabl_${TAG}_${CFG}_$a"
-  EVAM_PP_ABLATE=$a timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d "$d" -o run -- \
+  lib="$ROOT/ab/libevam_pp_abl$a.so"; [ "$a" = 0 ] && lib="$ROOT/edge-video-analytics-microservice_amd/libevam_pp.so"
+  EVAM_PP_LIB="$lib" EVAM_PP_DIAGNOSTIC_BUILD_OK=1 timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d "$d" -o run -- \
     python3 "$ROOT/bench.py" --config "$CFG" --steps 200 --warmup 30 --no-cpu-baseline --resident-steps 0 "$@" \
     > "$d.json" 2> "$d.err" || { tail -5 "$d.err"; exit 1; }
   python3 - "$d" "$a" "$CFG" <<'PY' | tee -a "$OUT/profabl_$TAG.txt"
