@@ -38,6 +38,7 @@
 
 #define EVAM_HD __host__ __device__
 #include "evam_geom.h"
+#include "evam_rings.h"
 
 namespace {
 
@@ -1650,6 +1651,7 @@ __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
     const int segY = P.segY, segC = P.segC, grp = P.grp_bytes;
     // ring entry: [Y tap0][Y tap1][C tap0][C tap1] (+ [V tap0][V tap1] for I420)
     auto issue = [&](int i, int k) {
+        if (kAblate & 16) return;  // diagnostics: no DMA
         const int L = i;  // lane of row vr0 + i in the row table
         const int ya = y0 + __builtin_amdgcn_readlane(lr0, L), yb = y0 + __builtin_amdgcn_readlane(lr1, L);
         uint8_t* e = wbuf + k * grp;
@@ -1755,6 +1757,10 @@ __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
     // v: LUT byte offsets (fp32) or bytes (u8), source channel order
     auto put = [&](int Y, uint32_t v0, uint32_t v1, uint32_t v2) {
         if (!xin) return;
+        if (kAblate & 4) {  // diagnostics: no stores
+            asm volatile("" ::"v"(v0), "v"(v1), "v"(v2));
+            return;
+        }
         const int so = (int)((uint32_t)(Y * p_DW) * (uint32_t)esz);
         if constexpr (OUT == 1) {
             __builtin_amdgcn_raw_buffer_store_b32(*reinterpret_cast<const uint32_t*>(lutb + v0), rsO0, vo, so, EVAM_PP_STORE_AUX);
@@ -1782,6 +1788,12 @@ __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
             const uint32_t wb0 = (uint32_t)__builtin_amdgcn_readlane(lb0, i), wb1 = (uint32_t)__builtin_amdgcn_readlane(lb1, i);
             const int ya = __builtin_amdgcn_readlane(lr0, i), yb = __builtin_amdgcn_readlane(lr1, i);
             const bool share = ((y0 + ya) >> 1) == ((y0 + yb) >> 1);
+            if (kAblate & 2) {  // diagnostics: no pixel math (no tap reads)
+                put(Y, fill0, fill1, fill2);
+                if (i + D < n) issue(i + D, k);
+                k = k + 1 == D ? 0 : k + 1;
+                continue;
+            }
             const uint8_t* e = wbuf + k * grp;
             const uint8_t* sy0 = e + lY;
             const uint8_t* sy1 = e + segY + lY;
@@ -2856,41 +2868,55 @@ bool plan_roi(int f, int DW, int DH, int out_dtype, int px, int max_row_bytes, i
     return true;
 }
 
-// Descriptor upload ring. The per-call descriptor block ([LUT][ItemDesc x n][tables]) changes with
-// every new ROI set; it is written into a pinned host slot and copied on a private copy stream into a
-// device slot of the same index, so the host never blocks on the copy and the copy of call k+1 can
-// overlap the kernel of call k. Slot reuse is fenced by two events: `copied` (the H2D out of the host
-// slot finished) and `used` (the last kernel that read the device slot finished).
-struct DescRing {
-    static constexpr int N = 3;
-    uint8_t* host[N] = {};
-    uint8_t* dev[N] = {};
-    size_t cap[N] = {};
-    hipEvent_t copied[N] = {};
-    hipEvent_t used[N] = {};
-    bool copied_rec[N] = {};
-    bool used_rec[N] = {};
-    hipStream_t copy = nullptr;
-    int cur = -1;
-    std::vector<uint8_t> last;  // bytes currently held by dev[cur]
+// HIP backend of the descriptor rings (evam_rings.h): events, streams, pinned and device memory. Every
+// failure is reported through fail() with the HIP error string.
+struct HipRings {
+    using Event = hipEvent_t;
+    using Stream = hipStream_t;
+    static int err(hipError_t e, const char* what) {
+        return e == hipSuccess ? 0 : fail(EVAM_PP_ERR_HIP, "%s failed: %s", what, hipGetErrorString(e));
+    }
+    int event_create(Event* e) { return err(hipEventCreateWithFlags(e, hipEventDisableTiming), "hipEventCreate"); }
+    int event_destroy(Event e) { return err(hipEventDestroy(e), "hipEventDestroy"); }
+    int event_record(Event e, Stream s) { return err(hipEventRecord(e, s), "hipEventRecord"); }
+    int event_sync(Event e) { return err(hipEventSynchronize(e), "hipEventSynchronize"); }
+    int stream_create(Stream* s) { return err(hipStreamCreateWithFlags(s, hipStreamNonBlocking), "hipStreamCreate"); }
+    int stream_destroy(Stream s) { return err(hipStreamDestroy(s), "hipStreamDestroy"); }
+    int stream_wait(Stream s, Event e) { return err(hipStreamWaitEvent(s, e, 0), "hipStreamWaitEvent"); }
+    int stream_sync(Stream s) { return err(hipStreamSynchronize(s), "hipStreamSynchronize"); }
+    int pinned_alloc(uint8_t** h, const uint8_t** d, size_t n) {
+        if (hipHostMalloc((void**)h, n, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
+            *h = nullptr;
+            return fail(EVAM_PP_ERR_OOM, "evam_pp_run: hipHostMalloc(%zu) failed", n);
+        }
+        void* dp = nullptr;
+        if (int rc = err(hipHostGetDevicePointer(&dp, *h, 0), "hipHostGetDevicePointer")) return rc;
+        *d = reinterpret_cast<const uint8_t*>(dp);
+        return 0;
+    }
+    int pinned_free(uint8_t* h) { return err(hipHostFree(h), "hipHostFree"); }
+    int host_alloc(uint8_t** h, size_t n) {
+        if (hipHostMalloc((void**)h, n, hipHostMallocDefault) != hipSuccess) {
+            *h = nullptr;
+            return fail(EVAM_PP_ERR_OOM, "evam_pp_run: hipHostMalloc(%zu) failed", n);
+        }
+        return 0;
+    }
+    int host_free(uint8_t* h) { return err(hipHostFree(h), "hipHostFree"); }
+    int dev_alloc(uint8_t** d, size_t n) {
+        if (hipMalloc((void**)d, n) != hipSuccess) {
+            *d = nullptr;
+            return fail(EVAM_PP_ERR_OOM, "evam_pp_run: hipMalloc(%zu) failed", n);
+        }
+        return 0;
+    }
+    int dev_free(uint8_t* d) { return err(hipFree(d), "hipFree"); }
+    int copy_h2d(uint8_t* dst, const uint8_t* src, size_t n, Stream s) {
+        return err(hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, s), "hipMemcpyAsync");
+    }
 };
-
-// Per-call ROI descriptors ([RoiRec x n], launch order) change with every
-// detection result. They are written into a slot of pinned, coherent (fine-grained) host memory that
-// the ROI kernel reads directly over PCIe: each workgroup fetches only its own ~70 bytes, so a call
-// costs one memcpy and no copy command. Slots are used in order and fenced in runs of kFence: one event,
-// recorded after the call that used the run's last slot, covers the run (an event record per call adds
-// a packet the command processor serves between every two ROI launches).
-struct PinRing {
-    static constexpr int N = 16;
-    static constexpr int kFence = 4;
-    uint8_t* host[N] = {};
-    const uint8_t* dev[N] = {};  // device address of host[k]
-    size_t cap[N] = {};
-    hipEvent_t used[N] = {};
-    bool used_rec[N] = {};
-    int cur = -1;
-};
+using DescRing = DescRingT<HipRings>;
+using PinRing = PinRingT<HipRings>;
 
 }  // namespace
 
@@ -2934,108 +2960,18 @@ struct evam_pp {
 
 namespace {
 
-void ring_release(DescRing& r) {
-    for (int k = 0; k < DescRing::N; k++) {
-        if (r.host[k]) (void)hipHostFree(r.host[k]);
-        if (r.dev[k]) (void)hipFree(r.dev[k]);
-        if (r.copied[k]) (void)hipEventDestroy(r.copied[k]);
-        if (r.used[k]) (void)hipEventDestroy(r.used[k]);
-        r.host[k] = r.dev[k] = nullptr;
-        r.copied[k] = r.used[k] = nullptr;
-        r.cap[k] = 0;
-    }
-    if (r.copy) (void)hipStreamDestroy(r.copy);
-    r.copy = nullptr;
-    r.cur = -1;
-}
-
-void pin_release(PinRing& r) {
-    for (int k = 0; k < PinRing::N; k++) {
-        if (r.host[k]) (void)hipHostFree(r.host[k]);
-        if (r.used[k]) (void)hipEventDestroy(r.used[k]);
-        r.host[k] = nullptr;
-        r.dev[k] = nullptr;
-        r.used[k] = nullptr;
-        r.cap[k] = 0;
-    }
-    r.cur = -1;
-}
-
-// Next pinned slot with at least n bytes (waits only if a kernel of PinRing::N calls ago still reads it).
-int pin_acquire(evam_pp* h, size_t n, uint8_t** host, const uint8_t** dev) {
-    PinRing& r = h->pin;
-    const int k = (r.cur + 1) % PinRing::N;
-    const int fk = k | (PinRing::kFence - 1);  // the run's fence: recorded after slot fk's previous use
-    if (!r.used[fk]) HIP_TRY(hipEventCreateWithFlags(&r.used[fk], hipEventDisableTiming));
-    if (r.used_rec[fk]) HIP_TRY(hipEventSynchronize(r.used[fk]));
-    if (r.cap[k] < n) {
-        if (r.host[k]) HIP_TRY(hipHostFree(r.host[k]));
-        r.host[k] = nullptr;
-        r.dev[k] = nullptr;
-        r.cap[k] = 0;
-        const size_t cap = std::max<size_t>(n * 2, 64 * 1024);
-        if (hipHostMalloc((void**)&r.host[k], cap, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
-            return fail(EVAM_PP_ERR_OOM, "evam_pp_run: hipHostMalloc(%zu) failed", cap);
-        void* d = nullptr;
-        HIP_TRY(hipHostGetDevicePointer(&d, r.host[k], 0));
-        r.dev[k] = reinterpret_cast<const uint8_t*>(d);
-        r.cap[k] = cap;
-    }
-    r.cur = k;
-    *host = r.host[k];
-    *dev = r.dev[k];
-    return EVAM_PP_OK;
-}
-
-// Make h->h_block visible to kernels on h->stream; returns the device copy. Re-uploads only when the
-// bytes differ from the block already resident in the current slot.
-int ring_upload(evam_pp* h, const uint8_t** out) {
-    DescRing& r = h->ring;
-    const size_t n = h->h_block.size();
-    if (r.cur >= 0 && r.last.size() == n && memcmp(r.last.data(), h->h_block.data(), n) == 0) {
-        *out = r.dev[r.cur];
-        return EVAM_PP_OK;
-    }
-    if (!r.copy) {
-        HIP_TRY(hipStreamCreateWithFlags(&r.copy, hipStreamNonBlocking));
-        for (int k = 0; k < DescRing::N; k++) {
-            HIP_TRY(hipEventCreateWithFlags(&r.copied[k], hipEventDisableTiming));
-            HIP_TRY(hipEventCreateWithFlags(&r.used[k], hipEventDisableTiming));
+// A failed evam_pp_run after its pinned slot was taken: drain the stream (PinRingT::abandon), so a run
+// whose fence the failed call should have recorded cannot leave slots that kernels still read.
+struct PinGuard {
+    evam_pp* h;
+    bool armed = false;
+    ~PinGuard() {
+        if (armed) {
+            HipRings b;
+            (void)h->pin.abandon(b, h->stream);
         }
     }
-    // Fence the slot being retired: every kernel that read it is already on h->stream (a stream
-    // switch orders the new stream behind the old one, evam_pp_set_stream), so one event recorded now
-    // covers them all. Calls that reuse the resident block record nothing.
-    if (r.cur >= 0) {
-        HIP_TRY(hipEventRecord(r.used[r.cur], h->stream));
-        r.used_rec[r.cur] = true;
-    }
-    const int k = (r.cur + 1) % DescRing::N;
-    if (r.copied_rec[k]) HIP_TRY(hipEventSynchronize(r.copied[k]));  // host slot free
-    if (r.cap[k] < n) {
-        if (r.used_rec[k]) HIP_TRY(hipEventSynchronize(r.used[k]));  // device slot no longer read
-        if (r.host[k]) HIP_TRY(hipHostFree(r.host[k]));
-        if (r.dev[k]) HIP_TRY(hipFree(r.dev[k]));
-        r.host[k] = r.dev[k] = nullptr;
-        r.cap[k] = 0;
-        const size_t cap = std::max<size_t>(n * 2, 64 * 1024);
-        if (hipHostMalloc((void**)&r.host[k], cap, hipHostMallocDefault) != hipSuccess)
-            return fail(EVAM_PP_ERR_OOM, "evam_pp_run: hipHostMalloc(%zu) failed", cap);
-        if (hipMalloc((void**)&r.dev[k], cap) != hipSuccess)
-            return fail(EVAM_PP_ERR_OOM, "evam_pp_run: hipMalloc(%zu) failed", cap);
-        r.cap[k] = cap;
-    }
-    memcpy(r.host[k], h->h_block.data(), n);
-    if (r.used_rec[k]) HIP_TRY(hipStreamWaitEvent(r.copy, r.used[k], 0));
-    HIP_TRY(hipMemcpyAsync(r.dev[k], r.host[k], n, hipMemcpyHostToDevice, r.copy));
-    HIP_TRY(hipEventRecord(r.copied[k], r.copy));
-    r.copied_rec[k] = true;
-    HIP_TRY(hipStreamWaitEvent(h->stream, r.copied[k], 0));
-    r.cur = k;
-    r.last.assign(h->h_block.begin(), h->h_block.end());
-    *out = r.dev[k];
-    return EVAM_PP_OK;
-}
+};
 
 }  // namespace
 
@@ -3106,12 +3042,13 @@ void evam_pp_destroy(evam_pp* h) {
     }
 #endif
     (void)hipSetDevice(h->device);
-    if (h->ring.copy || h->pin.cur >= 0) {
+    if (h->ring.have_copy || h->pin.cur >= 0) {
         (void)hipStreamSynchronize(h->stream);
-        if (h->ring.copy) (void)hipStreamSynchronize(h->ring.copy);
+        if (h->ring.have_copy) (void)hipStreamSynchronize(h->ring.copy);
     }
-    ring_release(h->ring);
-    pin_release(h->pin);
+    HipRings b;
+    h->ring.release(b);
+    h->pin.release(b);
     if (h->ev_switch) (void)hipEventDestroy(h->ev_switch);
     if (h->ev0) (void)hipEventDestroy(h->ev0);
     if (h->ev1) (void)hipEventDestroy(h->ev1);
@@ -3393,8 +3330,11 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
     HIP_TRY(hipSetDevice(h->device));
     uint8_t* dyn = nullptr;
     const uint8_t* d_dyn = nullptr;
+    PinGuard pin_guard{h};
     if (any_roi) {
-        if (int rc = pin_acquire(h, dyn_bytes, &dyn, &d_dyn)) return rc;
+        HipRings b;
+        if (int rc = h->pin.acquire(b, dyn_bytes, &dyn, &d_dyn)) return rc;
+        pin_guard.armed = true;
         HP(5);
         // Launch order: largest estimated work first (counting sort on 64 buckets of the staged
         // bytes, crop width x touched rows). Workgroups are dispatched in order as slots free, so
@@ -3489,7 +3429,10 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
     }
     HP(8);
     const uint8_t* d_block = nullptr;
-    if (int rc = ring_upload(h, &d_block)) return rc;
+    {
+        HipRings b;
+        if (int rc = h->ring.upload(b, h->stream, h->h_block.data(), h->h_block.size(), &d_block)) return rc;
+    }
     HP(9);
 
     // ---- launches ----
@@ -3728,9 +3671,10 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
         if (e != hipSuccess) return fail(EVAM_PP_ERR_HIP, "kernel launch failed: %s", hipGetErrorString(e));
         launches++;
     }
-    if (any_roi && (h->pin.cur & (PinRing::kFence - 1)) == PinRing::kFence - 1) {
-        HIP_TRY(hipEventRecord(h->pin.used[h->pin.cur], h->stream));
-        h->pin.used_rec[h->pin.cur] = true;
+    if (any_roi) {
+        HipRings b;
+        if (int rc = h->pin.fence(b, h->stream)) return rc;
+        pin_guard.armed = false;
     }
     if (h->opt_timing) HIP_TRY(hipEventRecord(h->ev1, h->stream));
     h->timed = h->opt_timing != 0;

@@ -35,3 +35,21 @@ def test_planner_and_oracle_under_asan_ubsan(tmp_path):
     print(r.stdout)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-6000:]
     assert "all checks passed" in r.stdout
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="needs g++")
+def test_descriptor_rings_under_asan_ubsan(tmp_path):
+    """The pinned ROI-record ring and the descriptor upload ring (csrc/evam_rings.h, the code evam_pp_run
+    runs) against a simulated device timeline: no host write, copy or free of a slot while an enqueued
+    kernel may still read it, over slot reuse across the run-of-4 fences, capacity growth, stream switches
+    and failed calls; the negative controls (no event waits; failed calls left undrained) must
+    report violations."""
+    exe = tmp_path / "ring_check"
+    subprocess.run(["g++", *SAN, "-std=c++17", os.path.join(ROOT, "tests", "native", "ring_check.cpp"), "-o",
+                    str(exe)], check=True)
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0:verify_asan_link_order=0",
+               UBSAN_OPTIONS="print_stacktrace=1")
+    r = subprocess.run([str(exe)], capture_output=True, text=True, env=env, timeout=600)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "all checks passed" in r.stdout and "rings: 8000 calls" in r.stdout and " 0 violations" in r.stdout
