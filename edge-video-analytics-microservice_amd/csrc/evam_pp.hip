@@ -1584,24 +1584,29 @@ struct TParams {
 };
 
 // Row-strip kernel for uniform-geometry 4:2:0 batches whose output rows do not share source rows
-// (downscales: C2, C4, C5). Every wave owns one 64-column strip of a tile and walks the tile's rows
-// alone, one output row per step, with no workgroup barrier after the prologue:
+// (downscales: C2, C4, C5). Every wave owns one strip of 64 x PX output columns of a tile (lane l holds
+// columns l, l + 64, ...) and walks the tile's rows alone, one output row per step, with no workgroup
+// barrier after the prologue:
 //  * a ring of D row entries per wave (two luma row segments, one or two chroma row segments: the strip's
 //    16-byte-aligned footprint) fed by LDS-DMA D rows ahead; the wait for a row is one counted vmcnt,
 //    so the ring's other rows and the stores of the previous rows stay in flight;
-//  * the OpenCV coefficient tables of the strip's columns (one per lane) and of the tile's rows (one per
+//  * the OpenCV coefficient tables of the strip's columns (per lane) and of the tile's rows (one per
 //    lane, read back with v_readlane) are computed in the prologue by the kernels' shared linear_coef, so
 //    the first DMA waits for no table load;
 //  * per pixel: four luma taps and two chroma taps per chroma row from LDS, BT.601 as saturating two-tap
 //    registers, the 11-bit horizontal pass as one v_dot2 per channel, VResizeLinear 32s->8u as mulhi_u24,
-//    the LUT (fp32) and three planar stores (lane = pixel).
+//    the LUT (fp32) and three planar stores (256 contiguous bytes per store instruction).
+// Strip width: the C2 data movement alone takes 39.4 us in 64-column strips and 36.4 us in 128-column
+// strips (one 480-byte DMA segment per source row instead of 240: half the DMA instructions for the same
+// bytes), the copy floor of those bytes on the same box (profiles/r03c_strip_bw.txt).
 // Letterbox rows are plain fill stores outside the ring; letterbox columns are a per-lane select in the
 // strips that have any. D = ring depth (rows of DMA in flight).
-template <int FMT, int OUT, int D>
+template <int FMT, int OUT, int D, int PX>
 __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     static_assert(FMT == kNV12 || FMT == kI420, "4:2:0 sources");
     static_assert(D >= 2 && D <= 4, "ring depth");
+    static_assert(PX == 1 || PX == 2, "pixels per lane");
     constexpr int NPC = FMT == kI420 ? 2 : 1;  // chroma planes
     constexpr int NMIN = 2 + NPC;              // fewest DMA instructions of one row (chroma row shared)
     const int lane = threadIdx.x & 63;
@@ -1622,7 +1627,7 @@ __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
     const uint8_t* p2 = it.plane[2];
     const int pitch0 = it.pitch[0], pitch1 = it.pitch[1], pitch2 = it.pitch[2];
     const int x0 = it.x0, y0 = it.y0;
-    const int X0 = strip * 64;
+    const int X0 = strip * 64 * PX;
     const bool live = X0 < p_DW;  // a wave past the last strip only joins the LUT barrier
     const int2 sf = P.sfoot[min(strip, kMaxStrips - 1)];
     asm volatile("" ::"s"(p0), "s"(p1), "s"(p2), "s"(pitch0), "s"(pitch1), "s"(pitch2), "s"(x0), "s"(y0),
@@ -1649,11 +1654,10 @@ __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
     const __amdgpu_buffer_rsrc_t rsV = __builtin_amdgcn_make_buffer_rsrc((void*)(NPC == 2 ? p2 : p1), (short)0, 0x7FFFFFFF, 0x00020000);
     uint8_t* const wbuf = smem + P.offBuf + wave * P.wave_bytes;
     const int segY = P.segY, segC = P.segC, grp = P.grp_bytes;
-    // ring entry: [Y tap0][Y tap1][C tap0][C tap1] (+ [V tap0][V tap1] for I420)
+    // ring entry: [Y tap0][Y tap1][C tap0][C tap1] (+ [V tap0][V tap1] for I420); a segment is <= 64 chunks
     auto issue = [&](int i, int k) {
         if (kAblate & 16) return;  // diagnostics: no DMA
-        const int L = i;  // lane of row vr0 + i in the row table
-        const int ya = y0 + __builtin_amdgcn_readlane(lr0, L), yb = y0 + __builtin_amdgcn_readlane(lr1, L);
+        const int ya = y0 + __builtin_amdgcn_readlane(lr0, i), yb = y0 + __builtin_amdgcn_readlane(lr1, i);
         uint8_t* e = wbuf + k * grp;
         const uint32_t vo = (uint32_t)lane * 16u;
         if (lane < nY) {
@@ -1694,34 +1698,43 @@ __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
     const int npro = min(n, D);
     for (int i = 0; i < npro; i++) issue(i, i);
 
-    // per-lane column state: tap offsets inside the staged segments, packed 11-bit weights
-    const int X = X0 + lane;
-    const bool xin = live && X < p_DW;
-    uint32_t lY = 0, lC0 = 0, lC1 = 0, wp = 0;
-    bool padc = true;
-    if (cols) {
+    // per-lane column state of the lane's PX pixels: tap offsets inside the staged segments, packed
+    // 11-bit weights, store offsets
+    bool xin[PX], padc[PX];
+    uint32_t lY[PX], lC0[PX], lC1[PX], wp[PX], vo[PX];
+    bool anyp = false;
+    const size_t esz = OUT == 1 ? 4 : 1;
+#pragma unroll
+    for (int j = 0; j < PX; j++) {
+        const int X = X0 + lane + 64 * j;
+        xin[j] = live && X < p_DW;
+        vo[j] = (uint32_t)(xin[j] ? X : 0) * (uint32_t)esz;
+        lY[j] = lC0[j] = lC1[j] = wp[j] = 0;
+        padc[j] = true;
         const int dx = X - P.ox;
-        if (xin && dx >= 0 && dx < P.rw) {
+        if (cols && xin[j] && dx >= 0 && dx < P.rw) {
             int s0, a0, a1;
             linear_coef(dx, P.scale_x, P.cw, true, s0, a0, a1);
             const int ca = x0 + s0;  // tap 1 reads ca + 1: at the right edge (s0 = cw - 1) its weight a1 is 0
-            lY = (uint32_t)(ca - fsY);
+            lY[j] = (uint32_t)(ca - fsY);
             if constexpr (FMT == kNV12) {
-                lC0 = (uint32_t)(2 * (ca >> 1) - fsC);
-                lC1 = (uint32_t)(2 * ((ca + 1) >> 1) - fsC);
+                lC0[j] = (uint32_t)(2 * (ca >> 1) - fsC);
+                lC1[j] = (uint32_t)(2 * ((ca + 1) >> 1) - fsC);
             } else {
-                lC0 = (uint32_t)((ca >> 1) - fsC);
-                lC1 = (uint32_t)(((ca + 1) >> 1) - fsC);
+                lC0[j] = (uint32_t)((ca >> 1) - fsC);
+                lC1[j] = (uint32_t)(((ca + 1) >> 1) - fsC);
             }
-            wp = (uint32_t)a0 | ((uint32_t)a1 << 16);
-            padc = false;
+            wp[j] = (uint32_t)a0 | ((uint32_t)a1 << 16);
+            padc[j] = false;
         }
+        anyp |= xin[j] && padc[j];
     }
-    // every lane of a strip visible (wave-uniform): no per-pixel fill select
-    const bool anypad = cols && __builtin_amdgcn_ballot_w64(xin && padc) != 0;
+    // some visible lane shows letterbox columns (wave-uniform): only then the per-pixel fill select
+    const bool anypad = cols && __builtin_amdgcn_ballot_w64(anyp) != 0;
+    // stores per row of this wave: 3 per pixel column group with any lane inside the output (counted waits)
+    const bool full = X0 + 64 * (PX - 1) < p_DW;
 
     const size_t plane = (size_t)p_DW * p_DH;
-    const size_t esz = OUT == 1 ? 4 : 1;
     uint8_t* const d0 = reinterpret_cast<uint8_t*>(P.dst) + (size_t)(P.slot_offset + it.index * P.slot_stride) * 3 * plane * esz;
     uint8_t* const d1 = d0 + plane * esz;
     uint8_t* const d2 = d1 + plane * esz;
@@ -1729,7 +1742,6 @@ __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
     const __amdgpu_buffer_rsrc_t rsO0 = __builtin_amdgcn_make_buffer_rsrc((void*)(P.color_rgb ? d2 : d0), (short)0, 0x7FFFFFFF, 0x00020000);
     const __amdgpu_buffer_rsrc_t rsO1 = __builtin_amdgcn_make_buffer_rsrc((void*)d1, (short)0, 0x7FFFFFFF, 0x00020000);
     const __amdgpu_buffer_rsrc_t rsO2 = __builtin_amdgcn_make_buffer_rsrc((void*)(P.color_rgb ? d0 : d2), (short)0, 0x7FFFFFFF, 0x00020000);
-    const uint32_t vo = (uint32_t)(xin ? X : 0) * (uint32_t)esz;
     // fill in source channel order (P.fill is in output plane order)
     const uint32_t fq0 = P.fill & 0xFF, fq1 = (P.fill >> 8) & 0xFF, fq2 = (P.fill >> 16) & 0xFF;
     const uint32_t fsh = OUT == 1 ? 2 : 0;
@@ -1746,7 +1758,7 @@ __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
                 const int idx = threadIdx.x + q * nthr;
                 if (idx < 768) lut_s[idx] = lutv[q];
             }
-        } else {  // workgroups of 1-3 waves (outputs narrower than 193 columns)
+        } else {  // workgroups of 1-3 waves (outputs narrower than 64 x PX x 3 + 1 columns)
             for (int idx = threadIdx.x; idx < 768; idx += nthr)
                 lut_s[idx] = P.lut[P.color_rgb ? 512 - (idx & ~255) + (idx & 255) : idx];
         }
@@ -1754,52 +1766,58 @@ __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
     }
     if (!live) return;
     const uint8_t* lutb = smem;
-    // v: LUT byte offsets (fp32) or bytes (u8), source channel order
-    auto put = [&](int Y, uint32_t v0, uint32_t v1, uint32_t v2) {
-        if (!xin) return;
+    // pixel column group j of row Y; v: LUT byte offsets (fp32) or bytes (u8), source channel order
+    auto put = [&](int Y, int j, uint32_t v0, uint32_t v1, uint32_t v2) {
+        if (!xin[j]) return;
         if (kAblate & 4) {  // diagnostics: no stores
             asm volatile("" ::"v"(v0), "v"(v1), "v"(v2));
             return;
         }
         const int so = (int)((uint32_t)(Y * p_DW) * (uint32_t)esz);
         if constexpr (OUT == 1) {
-            __builtin_amdgcn_raw_buffer_store_b32(*reinterpret_cast<const uint32_t*>(lutb + v0), rsO0, vo, so, EVAM_PP_STORE_AUX);
-            __builtin_amdgcn_raw_buffer_store_b32(*reinterpret_cast<const uint32_t*>(lutb + 1024 + v1), rsO1, vo, so, EVAM_PP_STORE_AUX);
-            __builtin_amdgcn_raw_buffer_store_b32(*reinterpret_cast<const uint32_t*>(lutb + 2048 + v2), rsO2, vo, so, EVAM_PP_STORE_AUX);
+            __builtin_amdgcn_raw_buffer_store_b32(*reinterpret_cast<const uint32_t*>(lutb + v0), rsO0, vo[j], so, EVAM_PP_STORE_AUX);
+            __builtin_amdgcn_raw_buffer_store_b32(*reinterpret_cast<const uint32_t*>(lutb + 1024 + v1), rsO1, vo[j], so, EVAM_PP_STORE_AUX);
+            __builtin_amdgcn_raw_buffer_store_b32(*reinterpret_cast<const uint32_t*>(lutb + 2048 + v2), rsO2, vo[j], so, EVAM_PP_STORE_AUX);
         } else {
-            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v0, rsO0, vo, so, EVAM_PP_STORE_AUX);
-            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v1, rsO1, vo, so, EVAM_PP_STORE_AUX);
-            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v2, rsO2, vo, so, EVAM_PP_STORE_AUX);
+            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v0, rsO0, vo[j], so, EVAM_PP_STORE_AUX);
+            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v1, rsO1, vo[j], so, EVAM_PP_STORE_AUX);
+            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v2, rsO2, vo[j], so, EVAM_PP_STORE_AUX);
         }
+    };
+    auto put_fill = [&](int Y) {
+#pragma unroll
+        for (int j = 0; j < PX; j++) put(Y, j, fill0, fill1, fill2);
     };
     // letterbox rows above the ring: before its DMA in issue order, so they never enter the counted waits
     const int ra = n ? vr0 : Y1;
-    for (int Y = Y0; Y < ra; Y++) put(Y, fill0, fill1, fill2);
+    for (int Y = Y0; Y < ra; Y++) put_fill(Y);
 
+    const int nst = full ? 3 * PX : 3;
     auto ring = [&](auto has_pad) {
         constexpr bool PADC = decltype(has_pad)::value;
         int k = 0;  // ring entry of row i
         for (int i = 0; i < n; i++) {
             // row i's DMA landed: after it this wave issued the DMA of rows i+1 .. i+D-1 (>= NMIN each) and
-            // the stores of rows i-D+1 .. i-1 (3 each)
-            if (i >= D - 1 && i + D - 1 < n) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 1) * (NMIN + 3)) : "memory");
-            else vmcnt_exact(NMIN * (min(i + D - 1, n - 1) - i) + 3 * min(i, D - 1));
+            // the stores of rows i-D+1 .. i-1 (nst each)
+            if (i >= D - 1 && i + D - 1 < n) {
+                if (PX == 1 || !full) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 1) * (NMIN + 3)) : "memory");
+                else asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 1) * (NMIN + 3 * PX)) : "memory");
+            } else {
+                vmcnt_exact(NMIN * (min(i + D - 1, n - 1) - i) + nst * min(i, D - 1));
+            }
             const int Y = vr0 + i;
             const uint32_t wb0 = (uint32_t)__builtin_amdgcn_readlane(lb0, i), wb1 = (uint32_t)__builtin_amdgcn_readlane(lb1, i);
             const int ya = __builtin_amdgcn_readlane(lr0, i), yb = __builtin_amdgcn_readlane(lr1, i);
             const bool share = ((y0 + ya) >> 1) == ((y0 + yb) >> 1);
             if (kAblate & 2) {  // diagnostics: no pixel math (no tap reads)
-                put(Y, fill0, fill1, fill2);
+                put_fill(Y);
                 if (i + D < n) issue(i + D, k);
                 k = k + 1 == D ? 0 : k + 1;
                 continue;
             }
             const uint8_t* e = wbuf + k * grp;
-            const uint8_t* sy0 = e + lY;
-            const uint8_t* sy1 = e + segY + lY;
             const uint8_t* sc0 = e + 2 * segY;
             const uint8_t* sc1 = share ? sc0 : sc0 + segC;
-            UVs tA, tB;
             auto chroma = [&](const uint8_t* sc, uint32_t o) -> UVs {
                 if constexpr (FMT == kNV12) {
                     const uint32_t uv = *reinterpret_cast<const uint16_t*>(sc + o);
@@ -1808,33 +1826,37 @@ __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
                     return uv_terms_sat(sc[o], sc[2 * segC + o]);
                 }
             };
-            tA = chroma(sc0, lC0);
-            tB = chroma(sc0, lC1);
-            const uint32_t yA = luma_term(sy0[0]), yB = luma_term(sy0[1]);
-            const uint32_t yC = luma_term(sy1[0]), yD = luma_term(sy1[1]);
-            uint32_t h0[3], h1[3];
-            h0[0] = hpass_sat(yA, tA.b, yB, tB.b, wp);
-            h0[1] = hpass_sat(yA, tA.g, yB, tB.g, wp);
-            h0[2] = hpass_sat(yA, tA.r, yB, tB.r, wp);
-            if (share) {
-                h1[0] = hpass_sat(yC, tA.b, yD, tB.b, wp);
-                h1[1] = hpass_sat(yC, tA.g, yD, tB.g, wp);
-                h1[2] = hpass_sat(yC, tA.r, yD, tB.r, wp);
-            } else {
-                const UVs tC = chroma(sc1, lC0), tE = chroma(sc1, lC1);
-                h1[0] = hpass_sat(yC, tC.b, yD, tE.b, wp);
-                h1[1] = hpass_sat(yC, tC.g, yD, tE.g, wp);
-                h1[2] = hpass_sat(yC, tC.r, yD, tE.r, wp);
-            }
-            uint32_t v[3];
 #pragma unroll
-            for (int c = 0; c < 3; c++) v[c] = vfinal<OUT>(h0[c], h1[c], wb0, wb1);
-            if constexpr (PADC) {
-                v[0] = padc ? fill0 : v[0];
-                v[1] = padc ? fill1 : v[1];
-                v[2] = padc ? fill2 : v[2];
+            for (int j = 0; j < PX; j++) {
+                const uint8_t* sy0 = e + lY[j];
+                const uint8_t* sy1 = e + segY + lY[j];
+                const UVs tA = chroma(sc0, lC0[j]), tB = chroma(sc0, lC1[j]);
+                const uint32_t yA = luma_term(sy0[0]), yB = luma_term(sy0[1]);
+                const uint32_t yC = luma_term(sy1[0]), yD = luma_term(sy1[1]);
+                uint32_t h0[3], h1[3];
+                h0[0] = hpass_sat(yA, tA.b, yB, tB.b, wp[j]);
+                h0[1] = hpass_sat(yA, tA.g, yB, tB.g, wp[j]);
+                h0[2] = hpass_sat(yA, tA.r, yB, tB.r, wp[j]);
+                if (share) {
+                    h1[0] = hpass_sat(yC, tA.b, yD, tB.b, wp[j]);
+                    h1[1] = hpass_sat(yC, tA.g, yD, tB.g, wp[j]);
+                    h1[2] = hpass_sat(yC, tA.r, yD, tB.r, wp[j]);
+                } else {
+                    const UVs tC = chroma(sc1, lC0[j]), tE = chroma(sc1, lC1[j]);
+                    h1[0] = hpass_sat(yC, tC.b, yD, tE.b, wp[j]);
+                    h1[1] = hpass_sat(yC, tC.g, yD, tE.g, wp[j]);
+                    h1[2] = hpass_sat(yC, tC.r, yD, tE.r, wp[j]);
+                }
+                uint32_t v[3];
+#pragma unroll
+                for (int c = 0; c < 3; c++) v[c] = vfinal<OUT>(h0[c], h1[c], wb0, wb1);
+                if constexpr (PADC) {
+                    v[0] = padc[j] ? fill0 : v[0];
+                    v[1] = padc[j] ? fill1 : v[1];
+                    v[2] = padc[j] ? fill2 : v[2];
+                }
+                put(Y, j, v[0], v[1], v[2]);
             }
-            put(Y, v[0], v[1], v[2]);
             asm volatile("" ::: "memory");  // the stores stay ahead of the next DMA (counted waits)
             if (i + D < n) issue(i + D, k);  // this entry's reads are done: the stores consumed them
             asm volatile("" ::: "memory");
@@ -1844,7 +1866,7 @@ __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
     if (anypad) ring(std::true_type{});
     else ring(std::false_type{});
     // letterbox rows below the ring
-    for (int Y = max(ra, vr1); Y < Y1; Y++) put(Y, fill0, fill1, fill2);
+    for (int Y = max(ra, vr1); Y < Y1; Y++) put_fill(Y);
 }
 
 static_assert(sizeof(evam_roi) == 20, "evam_roi layout");
@@ -2378,10 +2400,12 @@ struct Knobs {
     int roi_th = -1, roi_buf = -1, roi_px = 1, roi_sort = 1, roi_xcd = 0;  // roi_buf -1: sized for one round
     int roi_unit = 0;                              // ROI work-unit size in row groups (0: one unit per base tile)
     int roi_nbuf = 2;                              // ROI staging buffers (3: two groups of DMA in flight)
-    int strip = 1, strip_th = -1, strip_d = -1, strip_nw = -1;  // strip kernel: allowed, rows per tile, ring depth, waves
+    int strip = 1, strip_th = -1, strip_d = -1, strip_nw = -1, strip_px = 0;  // strip kernel: allowed (2: forced),
+                                                                              // rows per tile, ring depth, waves, px
     void read() {
         strip = env_int("EVAM_PP_STRIP", strip); strip_th = env_int("EVAM_PP_STRIP_TH", strip_th);
         strip_d = env_int("EVAM_PP_STRIP_D", strip_d); strip_nw = env_int("EVAM_PP_STRIP_NW", strip_nw);
+        strip_px = env_int("EVAM_PP_STRIP_PX", strip_px);
         staged = env_int("EVAM_PP_STAGED", staged); wave = env_int("EVAM_PP_WAVE", wave);
         rows = env_int("EVAM_PP_ROWS", rows); roi = env_int("EVAM_PP_ROI", roi);
         th = env_int("EVAM_PP_TH", th); tw = env_int("EVAM_PP_TW", tw); xcd = env_int("EVAM_PP_XCD", xcd);
@@ -2706,32 +2730,39 @@ bool plan_wave(int f, const Geom& g, int DW, int DH, int count, int out_dtype, i
     return true;
 }
 
-template <int FMT, int OUT>
-const void* strip_fn_t(int d) {
-    return d == 4 ? (const void*)evam_pp_strip<FMT, OUT, 4>
-                  : (d == 3 ? (const void*)evam_pp_strip<FMT, OUT, 3> : (const void*)evam_pp_strip<FMT, OUT, 2>);
+template <int FMT, int OUT, int PX>
+const void* strip_fn_p(int d) {
+    return d == 4 ? (const void*)evam_pp_strip<FMT, OUT, 4, PX>
+                  : (d == 3 ? (const void*)evam_pp_strip<FMT, OUT, 3, PX> : (const void*)evam_pp_strip<FMT, OUT, 2, PX>);
 }
-const void* strip_fn(int f, int out, int d) {
-    switch (f * 2 + out) {
-    case kNV12 * 2 + 0: return strip_fn_t<kNV12, 0>(d);
-    case kNV12 * 2 + 1: return strip_fn_t<kNV12, 1>(d);
-    case kI420 * 2 + 0: return strip_fn_t<kI420, 0>(d);
-    default: return strip_fn_t<kI420, 1>(d);
+const void* strip_fn(int f, int out, int d, int px) {
+    switch ((f * 2 + out) * 2 + (px == 2)) {
+    case (kNV12 * 2 + 0) * 2: return strip_fn_p<kNV12, 0, 1>(d);
+    case (kNV12 * 2 + 0) * 2 + 1: return strip_fn_p<kNV12, 0, 2>(d);
+    case (kNV12 * 2 + 1) * 2: return strip_fn_p<kNV12, 1, 1>(d);
+    case (kNV12 * 2 + 1) * 2 + 1: return strip_fn_p<kNV12, 1, 2>(d);
+    case (kI420 * 2 + 0) * 2: return strip_fn_p<kI420, 0, 1>(d);
+    case (kI420 * 2 + 0) * 2 + 1: return strip_fn_p<kI420, 0, 2>(d);
+    case (kI420 * 2 + 1) * 2: return strip_fn_p<kI420, 1, 1>(d);
+    default: return strip_fn_p<kI420, 1, 2>(d);
     }
 }
 
 // Strip-kernel plan for a uniform 4:2:0 group (fills everything in TParams but the items, LUT, output
-// and colour fields). Waves per workgroup: 4..8 strips with the fewest idle waves. Ring depth D: the
-// deepest (<= 4) whose LDS still admits the workgroups that fill a CU's 32 wave slots. Tile height:
-// one round of workgroups over the chip (a second round repeats every wave's ring fill at the tail),
-// at most 64 rows (the lane-held row table). Returns false when the geometry does not suit it: outputs
-// wider than kMaxStrips strips, footprints over 1 KB per 64 columns, or consecutive output rows that
-// share source rows (vertical upscales: the wave kernel's REUSE path).
+// and colour fields).
+//  * Pixels per lane PX: 2 (128-column strips: one ~480-byte DMA segment per source row at 3.75x) unless the
+//    output is narrower than 128 columns or a strip's footprint exceeds one 1 KB DMA instruction; the strip
+//    pattern's data movement alone is 3 us faster at 128 columns than at 64 (profiles/r03c_strip_bw.txt).
+//  * Waves per workgroup: 4..8 strips with the fewest idle waves.
+//  * Tile height: about 16 waves per CU over the whole launch (the data-movement microbenchmark's best:
+//    fewer, longer-lived waves beat a full 32), at most 64 rows (the lane-held row table).
+//  * Ring depth D: the deepest (<= 4) whose LDS still admits those workgroups.
+// Returns false when the geometry does not suit it: outputs wider than kMaxStrips strips, footprints over
+// 1 KB per strip, or consecutive output rows that share source rows (vertical upscales: the wave kernel's
+// REUSE path).
 bool plan_strip(int f, const Geom& g, int DW, int DH, int count, int out_dtype, int n_cu, const XTab* xt,
-                const YTab* yt, uint32_t x0_mask, const Knobs& kn, TParams& p, int& D, int& lds, int& grid) {
+                const YTab* yt, uint32_t x0_mask, const Knobs& kn, TParams& p, int& D, int& px, int& lds, int& grid) {
     if (f != kNV12 && f != kI420) return false;
-    const int nstrips = (DW + 63) / 64;
-    if (nstrips > kMaxStrips) return false;
     int shared = 0, vis = 0;
     for (int Y = 0; Y + 1 < DH; Y++) {
         const bool pad0 = (yt[Y].b0 | yt[Y].b1) == 0, pad1 = (yt[Y + 1].b0 | yt[Y + 1].b1) == 0;
@@ -2741,10 +2772,18 @@ bool plan_strip(int f, const Geom& g, int DW, int DH, int count, int out_dtype, 
     }
     if (kn.strip != 2 && shared * 8 > vis) return false;  // more than 1 in 8 rows re-stages a row
     if (!x0_mask) x0_mask = 1u << (g.x0 & 31);
-    int mY = 0, mC = 0;
-    wave_segments(f, g.ox, g.rw, DW, xt, x0_mask, 64, mY, mC);
-    if (mY > 64 || mC > 64) return false;
     const int npc = f == kI420 ? 2 : 1;
+    int mY = 0, mC = 0;
+    px = 0;
+    for (int cand : {2, 1}) {
+        if (kn.strip_px > 0 && cand != kn.strip_px) continue;
+        if (cand == 2 && DW < 128 && kn.strip_px != 2) continue;
+        wave_segments(f, g.ox, g.rw, DW, xt, x0_mask, 64 * cand, mY, mC);
+        if (mY <= 64 && mC <= 64) { px = cand; break; }
+    }
+    if (!px) return false;
+    const int nstrips = (DW + 64 * px - 1) / (64 * px);
+    if (nstrips > kMaxStrips) return false;
     p.segY = 16 * std::max(1, mY);
     p.segC = 16 * std::max(1, mC);
     p.grp_bytes = 2 * p.segY + 2 * npc * p.segC;
@@ -2758,7 +2797,7 @@ bool plan_strip(int f, const Geom& g, int DW, int DH, int count, int out_dtype, 
     p.nw = nw;
     p.tiles_x = (nstrips + nw - 1) / nw;
     p.offBuf = out_dtype == EVAM_DTYPE_F32 ? kLutBytes : 0;
-    const int wg_target = std::max(1, 32 / nw);
+    const int wg_target = std::max(1, 16 / nw);
     D = 2;
     for (int d : {4, 3, 2}) {
         if (p.offBuf + nw * d * p.grp_bytes + 16 <= (160 * 1024) / wg_target) { D = d; break; }
@@ -2767,9 +2806,9 @@ bool plan_strip(int f, const Geom& g, int DW, int DH, int count, int out_dtype, 
     p.wave_bytes = D * p.grp_bytes;
     lds = p.offBuf + nw * p.wave_bytes + 16;  // + 16: a right-edge tap reads one byte past its footprint (weight 0)
     if (lds > 64 * 1024) return false;
-    const int res = std::max(1, resident_per_cu(strip_fn(f, out_dtype, D), lds));
+    const int res = std::max(1, std::min(wg_target, resident_per_cu(strip_fn(f, out_dtype, D, px), lds)));
     const int64_t slots = (int64_t)n_cu * res;
-    const int64_t work = (int64_t)count * p.tiles_x * DH;
+    const int64_t work = (int64_t)std::min(count, kArgItems) * p.tiles_x * DH;
     int th = (int)std::max<int64_t>(1, (work + slots - 1) / slots);
     th = std::max(th, std::min(DH, D));
     if (kn.strip_th > 0) th = kn.strip_th;
@@ -2779,8 +2818,9 @@ bool plan_strip(int f, const Geom& g, int DW, int DH, int count, int out_dtype, 
     p.cw = g.cw; p.ch = g.ch; p.rw = g.rw; p.rh = g.rh; p.ox = g.ox; p.oy = g.oy;
     p.scale_x = 1. / ((double)g.rw / g.cw);
     p.scale_y = 1. / ((double)g.rh / g.ch);
+    const int sw = 64 * px;
     for (int s = 0; s < kMaxStrips; s++) {
-        const int Xv0 = std::max(s * 64, g.ox), Xv1 = std::min(std::min(s * 64 + 64, DW), g.ox + g.rw) - 1;
+        const int Xv0 = std::max(s * sw, g.ox), Xv1 = std::min(std::min(s * sw + sw, DW), g.ox + g.rw) - 1;
         p.sfoot[s] = s < nstrips && Xv0 <= Xv1 ? int2{xt[Xv0].s0, xt[Xv1].s1} : int2{-1, -1};
     }
     const int64_t gr = (int64_t)std::min(count, kArgItems) * p.tiles_per_item;
@@ -2789,21 +2829,25 @@ bool plan_strip(int f, const Geom& g, int DW, int DH, int count, int out_dtype, 
     return true;
 }
 
-template <int FMT, int OUT>
+template <int FMT, int OUT, int PX>
 hipError_t launch_strip_t(int d, const TParams& p, int grid, int lds, hipStream_t s) {
     const dim3 blk(64 * p.nw);
-    if (d == 4) hipLaunchKernelGGL((evam_pp_strip<FMT, OUT, 4>), dim3(grid), blk, lds, s, p);
-    else if (d == 3) hipLaunchKernelGGL((evam_pp_strip<FMT, OUT, 3>), dim3(grid), blk, lds, s, p);
-    else hipLaunchKernelGGL((evam_pp_strip<FMT, OUT, 2>), dim3(grid), blk, lds, s, p);
+    if (d == 4) hipLaunchKernelGGL((evam_pp_strip<FMT, OUT, 4, PX>), dim3(grid), blk, lds, s, p);
+    else if (d == 3) hipLaunchKernelGGL((evam_pp_strip<FMT, OUT, 3, PX>), dim3(grid), blk, lds, s, p);
+    else hipLaunchKernelGGL((evam_pp_strip<FMT, OUT, 2, PX>), dim3(grid), blk, lds, s, p);
     return hipGetLastError();
 }
 
-hipError_t launch_strip(int f, int out, int d, const TParams& p, int grid, int lds, hipStream_t s) {
-    switch (f * 2 + out) {
-    case kNV12 * 2 + 0: return launch_strip_t<kNV12, 0>(d, p, grid, lds, s);
-    case kNV12 * 2 + 1: return launch_strip_t<kNV12, 1>(d, p, grid, lds, s);
-    case kI420 * 2 + 0: return launch_strip_t<kI420, 0>(d, p, grid, lds, s);
-    default: return launch_strip_t<kI420, 1>(d, p, grid, lds, s);
+hipError_t launch_strip(int f, int out, int d, int px, const TParams& p, int grid, int lds, hipStream_t s) {
+    switch ((f * 2 + out) * 2 + (px == 2)) {
+    case (kNV12 * 2 + 0) * 2: return launch_strip_t<kNV12, 0, 1>(d, p, grid, lds, s);
+    case (kNV12 * 2 + 0) * 2 + 1: return launch_strip_t<kNV12, 0, 2>(d, p, grid, lds, s);
+    case (kNV12 * 2 + 1) * 2: return launch_strip_t<kNV12, 1, 1>(d, p, grid, lds, s);
+    case (kNV12 * 2 + 1) * 2 + 1: return launch_strip_t<kNV12, 1, 2>(d, p, grid, lds, s);
+    case (kI420 * 2 + 0) * 2: return launch_strip_t<kI420, 0, 1>(d, p, grid, lds, s);
+    case (kI420 * 2 + 0) * 2 + 1: return launch_strip_t<kI420, 0, 2>(d, p, grid, lds, s);
+    case (kI420 * 2 + 1) * 2: return launch_strip_t<kI420, 1, 1>(d, p, grid, lds, s);
+    default: return launch_strip_t<kI420, 1, 2>(d, p, grid, lds, s);
     }
 }
 
@@ -3479,10 +3523,10 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
             const int per_launch = std::min(count[f], kArgItems);
             if (kn.strip && kn.wave != 2) {
                 TParams* tp = &h->sc_tparams;
-                int D = 0, lds = 0, grid = 0;
+                int D = 0, spx = 0, lds = 0, grid = 0;
                 const XTab* hx = reinterpret_cast<const XTab*>(h->h_block.data() + tab_off[f]);
                 if (plan_strip(f, g0, DW, DH, count[f], cfg->out_dtype, h->n_cu, hx, reinterpret_cast<const YTab*>(hx + DW),
-                               x0_mask[f], kn, *tp, D, lds, grid)) {
+                               x0_mask[f], kn, *tp, D, spx, lds, grid)) {
                     tp->lut = lut_d;
                     tp->dst = dst->data;
                     tp->slot_offset = dst->slot_offset;
@@ -3493,9 +3537,11 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
                         const int nm = std::min(kArgItems, mfirst[f + 1] - m0);
                         fill_args(tp->items, m0, nm);
                         const int64_t gr = (int64_t)nm * tp->tiles_per_item;
-                        // XCD-contiguous tiles: the strips of one row band share source lines at their edges
-                        tp->xcd_remap = kn.xcd >= 0 ? kn.xcd : (int)(gr >= 8 * (int64_t)h->n_cu);
-                        hipError_t e = launch_strip(f, cfg->out_dtype, D, *tp, (int)gr, lds, h->stream);
+                        // Dispatch order, not XCD-contiguous: the C2 data movement in the strip pattern takes
+                        // 1.7 us longer with each XCD on its own run of tiles (profiles/r03c_strip_bw.txt);
+                        // EVAM_PP_XCD=1 forces that order
+                        tp->xcd_remap = kn.xcd > 0 ? 1 : 0;
+                        hipError_t e = launch_strip(f, cfg->out_dtype, D, spx, *tp, (int)gr, lds, h->stream);
                         if (e != hipSuccess) return fail(EVAM_PP_ERR_HIP, "kernel launch failed: %s", hipGetErrorString(e));
                         launches++;
                     }

@@ -52,7 +52,8 @@ def test_c1_bench_batch(evam, O, coracle, gpu):
 # kernel shapes forced on the full-size workloads: the default choice (the strip kernel for C2 / C4 / C5),
 # the strip kernel's other ring depths and tile heights, and the staged kernel's pipeline shapes
 STAGED_SHAPES = {"default": {}, "strip_d2": {"EVAM_PP_STRIP_D": "2"}, "strip_d3": {"EVAM_PP_STRIP_D": "3"},
-                 "strip_th32": {"EVAM_PP_STRIP_TH": "32"},
+                 "strip_th32": {"EVAM_PP_STRIP_TH": "32"}, "strip_px1": {"EVAM_PP_STRIP_PX": "1"},
+                 "strip_xcd": {"EVAM_PP_XCD": "1"},
                  "staged": {"EVAM_PP_STRIP": "0"},
                  "r2": {"EVAM_PP_STRIP": "0", "EVAM_PP_STAGE_R": "2", "EVAM_PP_NSEGX": "4"},
                  "r1": {"EVAM_PP_STRIP": "0", "EVAM_PP_STAGE_R": "1", "EVAM_PP_NSEGX": "4"},
@@ -103,7 +104,7 @@ def test_c3_bench_roi_set(evam, O, coracle, gpu, seed):
 
 
 @pytest.mark.parametrize("placement", ["top_left", "center"])
-@pytest.mark.parametrize("shape", ["default", "strip_d2", "strip_th32", "staged", "r2", "wide", "b3"])
+@pytest.mark.parametrize("shape", ["default", "strip_d2", "strip_th32", "strip_px1", "staged", "r2", "wide", "b3"])
 def test_c4_random_4k_letterbox(evam, O, coracle, gpu, placement, shape, monkeypatch):
     """C4: random (not constant) 3840x2160 NV12 bench frames letterboxed to 640x640 fp32: every 6x gather
     (column taps 6dx+2, weights 1024/1024) on the real 4K pitch is checked, in both placements."""
@@ -125,7 +126,7 @@ def test_c4_random_4k_letterbox(evam, O, coracle, gpu, placement, shape, monkeyp
     pp.close()
 
 
-@pytest.mark.parametrize("shape", ["default", "strip_d2", "staged", "b3"])
+@pytest.mark.parametrize("shape", ["default", "strip_d2", "strip_px1", "staged", "b3"])
 def test_c5_ring_step(evam, O, coracle, gpu, shape, monkeypatch):
     """C5: a 32-stream clip-ring step (1080p NV12 -> aspect(max) 398x224 -> central crop 224x224 fp32 into
     slot t % 16 of a [32, 16, 3, 224, 224] ring), two steps with different frames and slots."""

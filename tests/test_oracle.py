@@ -220,3 +220,35 @@ def test_cpu_fast_matches_oracle(O, coracle, fmt, mode, placement, rgb, dst, dty
         assert (got.view(np.uint32) == ref.view(np.uint32)).all()
     else:
         assert (got == ref).all()
+
+
+# Unit-scale model-proc ranges (DL Streamer "range": [min, max]) with non-zero minima, and the bench's
+# mean / std (ImageNet values in BGR order) next to a neutral setting.
+_RANGES = [(0.0, 1.0), (-1.0, 1.0), (-0.5, 0.5), (0.1, 0.9), (-2.0, 2.0), (0.25, 3.0), (-8.0, 8.0)]
+_MEAN_STD = [((0.406, 0.456, 0.485), (0.225, 0.224, 0.229)), ((0.0, 0.0, 0.0), (1.0, 1.0, 1.0)),
+             ((0.5, 0.5, 0.5), (0.5, 0.5, 0.5))]
+
+
+@pytest.mark.parametrize("rng_", _RANGES)
+@pytest.mark.parametrize("mean,std", _MEAN_STD)
+def test_norm_lut_within_tolerance_of_single_fma(O, rng_, mean, std):
+    """SURVEY.md §8 a8 / north_star fp32 bar. The LUT (oracle and kernels) rounds u * alpha and + beta
+    separately, as the scalar convertTo does; OpenCV's SIMD convertTo may fuse them into one FMA [3P,
+    unverified]. The two differ by at most one rounding of u * alpha + beta; here both forms are built for
+    every u and channel and the result stays within 1e-6 relative under SURVEY's max(|b|, 1/std) guard
+    (b = the reference value). Holds for ranges of magnitude <= 8 (every model-proc range in the reference
+    tree is [0, 1] or unset); a [16, 235]-scale range would exceed it near b = 0 (1 ulp of 235 is 1.5e-5)."""
+    two = O.np_norm_lut(3, rng_, mean, std)
+    alpha = np.float32((float(rng_[1]) - float(rng_[0])) / 255.0)
+    beta = np.float32(rng_[0])
+    u = np.arange(256, dtype=np.float64)
+    fused = (u * np.float64(alpha) + np.float64(beta)).astype(np.float32)  # exact product + sum, one rounding
+    for c in range(3):
+        b = ((fused - np.float32(mean[c])).astype(np.float32) / np.float32(std[c])).astype(np.float32)
+        guard = np.maximum(np.abs(b.astype(np.float64)), 1.0 / std[c])
+        err = np.abs(two[c].astype(np.float64) - b.astype(np.float64))
+        assert (err <= 1e-6 * guard).all(), (c, float((err / guard).max()))
+    if rng_[0] == 0.0:  # beta = 0: the two forms are the same rounding
+        for c in range(3):
+            b = ((fused - np.float32(mean[c])).astype(np.float32) / np.float32(std[c])).astype(np.float32)
+            assert np.array_equal(two[c].view(np.uint32), b.view(np.uint32))
