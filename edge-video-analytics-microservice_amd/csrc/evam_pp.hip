@@ -1562,6 +1562,9 @@ __global__ __launch_bounds__(kThreads) void evam_pp_wave(const WParams P) {
 // strip kernel (uniform geometry, 4:2:0 sources, no shared source rows between output rows)
 // ------------------------------------------------------------------------------------------------
 constexpr int kMaxStrips = 32;  // per-strip footprints in the kernel arguments: DW <= 2048
+// One staged row segment of the strip kernel: a strip's footprint is at most 64 16-byte chunks (one DMA
+// instruction), so every LDS offset of the ring is a compile-time immediate.
+constexpr int kStripSlot = 1024;
 
 struct TParams {
     ItemArg items[kArgItems];
@@ -1573,9 +1576,7 @@ struct TParams {
     int cw, ch, rw, rh, ox, oy;  // the launch's crop size, resized size and placement (uniform)
     int nw;                      // waves (strips) per workgroup
     int TH, tiles_x, tiles_per_item;  // tile = nw strips x TH rows
-    int segY, segC;              // bytes of one staged luma / chroma row segment (multiples of 16)
-    int grp_bytes, wave_bytes;   // one ring entry (one output row's segments); one wave's ring
-    int offBuf;                  // LDS offset of wave 0's ring (after the LUT)
+    int wave_bytes;              // one wave's ring: D entries of kStripSlot-byte segments
     int color_rgb;
     uint32_t fill;
     int xcd_remap;               // 1: consecutive tiles land on one XCD
@@ -1603,6 +1604,8 @@ struct TParams {
 // strips that have any. D = ring depth (rows of DMA in flight).
 template <int FMT, int OUT, int D, int PX>
 __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
+    // the LUT at a static LDS address (folds into the reads' immediate offsets); the rings after it
+    __shared__ __attribute__((aligned(16))) float lut_s[OUT == 1 ? 768 : 4];
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     static_assert(FMT == kNV12 || FMT == kI420, "4:2:0 sources");
     static_assert(D >= 2 && D <= 4, "ring depth");
@@ -1611,10 +1614,11 @@ __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
     constexpr int NMIN = 2 + NPC;              // fewest DMA instructions of one row (chroma row shared)
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (kAblate & 128) return;  // diagnostics: launch cost only
     const int p_nw = P.nw, p_tpi = P.tiles_per_item, p_tx = P.tiles_x, p_TH = P.TH, p_DH = P.DH, p_DW = P.DW;
     const int p_grid = gridDim.x;
     asm volatile("" ::"s"(p_nw), "s"(p_tpi), "s"(p_tx), "s"(p_TH), "s"(p_DH), "s"(p_DW), "s"(p_grid), "s"(P.xcd_remap),
-                 "s"(P.ox), "s"(P.rw), "s"(P.oy), "s"(P.rh), "s"(P.segY), "s"(P.segC), "s"(P.offBuf), "s"(P.wave_bytes));
+                 "s"(P.ox), "s"(P.rw), "s"(P.oy), "s"(P.rh), "s"(P.wave_bytes));
     const int t = P.xcd_remap ? xcd_tile(blockIdx.x, p_grid) : (int)blockIdx.x;
     const int item = t / p_tpi;
     const int tile = t - item * p_tpi;
@@ -1652,13 +1656,14 @@ __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
     const __amdgpu_buffer_rsrc_t rsY = __builtin_amdgcn_make_buffer_rsrc((void*)p0, (short)0, 0x7FFFFFFF, 0x00020000);
     const __amdgpu_buffer_rsrc_t rsU = __builtin_amdgcn_make_buffer_rsrc((void*)p1, (short)0, 0x7FFFFFFF, 0x00020000);
     const __amdgpu_buffer_rsrc_t rsV = __builtin_amdgcn_make_buffer_rsrc((void*)(NPC == 2 ? p2 : p1), (short)0, 0x7FFFFFFF, 0x00020000);
-    uint8_t* const wbuf = smem + P.offBuf + wave * P.wave_bytes;
-    const int segY = P.segY, segC = P.segC, grp = P.grp_bytes;
-    // ring entry: [Y tap0][Y tap1][C tap0][C tap1] (+ [V tap0][V tap1] for I420); a segment is <= 64 chunks
+    uint8_t* const wbuf = smem + wave * P.wave_bytes;
+    // ring entry: [Y tap0][Y tap1][C tap0][C tap1] (+ [V tap0][V tap1] for I420), kStripSlot bytes each
+    constexpr int SY = kStripSlot, SC = kStripSlot, GRP = 2 * SY + 2 * NPC * SC;
+    constexpr int segY = SY, segC = SC;
     auto issue = [&](int i, int k) {
         if (kAblate & 16) return;  // diagnostics: no DMA
         const int ya = y0 + __builtin_amdgcn_readlane(lr0, i), yb = y0 + __builtin_amdgcn_readlane(lr1, i);
-        uint8_t* e = wbuf + k * grp;
+        uint8_t* e = wbuf + k * GRP;
         const uint32_t vo = (uint32_t)lane * 16u;
         if (lane < nY) {
             __builtin_amdgcn_raw_ptr_buffer_load_lds(rsY, (__attribute__((address_space(3))) void*)e, 16, vo,
@@ -1748,7 +1753,6 @@ __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
     const uint32_t fill0 = (P.color_rgb ? fq2 : fq0) << fsh, fill1 = fq1 << fsh, fill2 = (P.color_rgb ? fq0 : fq2) << fsh;
 
     if constexpr (OUT == 1) {
-        float* lut_s = reinterpret_cast<float*>(smem);
         if (lut_early) {
             // the LUT loads landed once at most the ring's DMA instructions are outstanding
             if (npro == D) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NMIN * D) : "memory");
@@ -1765,7 +1769,33 @@ __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
         __syncthreads();
     }
     if (!live) return;
-    const uint8_t* lutb = smem;
+    if (kAblate & 64) {  // diagnostics: prologue only (tables, LUT, the ring's first DMA)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("" ::"v"(lY[0]), "v"(lC0[0]), "v"(lC1[0]), "v"(wp[0]), "v"(vo[0]), "v"(lb0), "v"(lb1));
+        return;
+    }
+    const uint8_t* lutb = reinterpret_cast<const uint8_t*>(lut_s);
+    // per-lane LDS addresses of the taps in ring entry 0 (entry k adds k * GRP, an immediate offset)
+    const uint8_t* aY[PX];
+    const uint8_t* aC0[PX];
+    const uint8_t* aC1[PX];
+#pragma unroll
+    for (int j = 0; j < PX; j++) {
+        aY[j] = wbuf + lY[j];
+        aC0[j] = wbuf + 2 * SY + lC0[j];
+        aC1[j] = wbuf + 2 * SY + lC1[j];
+    }
+    // BT.601 chroma-term constants: the additive ones in VGPRs so every term is one v_mad (a VOP3 reads one
+    // scalar operand: the multiplier)
+    uint32_t kb = kKBs, kg = kKGs, kr = kKRs;
+    int cvg = kCVG, cug = kCUG;
+    asm volatile("" : "+v"(kb), "+v"(kg), "+v"(kr), "+s"(cvg), "+s"(cug));
+    auto uvt = [&](uint32_t U, uint32_t V) {
+        // g = V * CVG + (U * CUG + K): two v_mad_i32_i24 (the sum of two products would select mul, mul, add3)
+        int gu = __mul24((int)U, cug) + (int)kg;
+        asm("" : "+v"(gu));  // keeps the association (no asm volatile: still scheduled freely)
+        return UVs{__umul24(U, (uint32_t)kCUB) + kb, (uint32_t)(__mul24((int)V, cvg) + gu), __umul24(V, (uint32_t)kCVR) + kr};
+    };
     // pixel column group j of row Y; v: LUT byte offsets (fp32) or bytes (u8), source channel order
     auto put = [&](int Y, int j, uint32_t v0, uint32_t v1, uint32_t v2) {
         if (!xin[j]) return;
@@ -1793,59 +1823,53 @@ __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
     for (int Y = Y0; Y < ra; Y++) put_fill(Y);
 
     const int nst = full ? 3 * PX : 3;
-    auto ring = [&](auto has_pad) {
+    // one output row: row i of the tile's visible rows, ring entry kk (compile-time after unrolling)
+    auto row = [&](int i, int kk, auto has_pad) {
         constexpr bool PADC = decltype(has_pad)::value;
-        int k = 0;  // ring entry of row i
-        for (int i = 0; i < n; i++) {
-            // row i's DMA landed: after it this wave issued the DMA of rows i+1 .. i+D-1 (>= NMIN each) and
-            // the stores of rows i-D+1 .. i-1 (nst each)
-            if (i >= D - 1 && i + D - 1 < n) {
-                if (PX == 1 || !full) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 1) * (NMIN + 3)) : "memory");
-                else asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 1) * (NMIN + 3 * PX)) : "memory");
-            } else {
-                vmcnt_exact(NMIN * (min(i + D - 1, n - 1) - i) + nst * min(i, D - 1));
-            }
-            const int Y = vr0 + i;
-            const uint32_t wb0 = (uint32_t)__builtin_amdgcn_readlane(lb0, i), wb1 = (uint32_t)__builtin_amdgcn_readlane(lb1, i);
-            const int ya = __builtin_amdgcn_readlane(lr0, i), yb = __builtin_amdgcn_readlane(lr1, i);
-            const bool share = ((y0 + ya) >> 1) == ((y0 + yb) >> 1);
-            if (kAblate & 2) {  // diagnostics: no pixel math (no tap reads)
-                put_fill(Y);
-                if (i + D < n) issue(i + D, k);
-                k = k + 1 == D ? 0 : k + 1;
-                continue;
-            }
-            const uint8_t* e = wbuf + k * grp;
-            const uint8_t* sc0 = e + 2 * segY;
-            const uint8_t* sc1 = share ? sc0 : sc0 + segC;
-            auto chroma = [&](const uint8_t* sc, uint32_t o) -> UVs {
-                if constexpr (FMT == kNV12) {
-                    const uint32_t uv = *reinterpret_cast<const uint16_t*>(sc + o);
-                    return uv_terms_sat(uv & 0xFF, uv >> 8);
-                } else {
-                    return uv_terms_sat(sc[o], sc[2 * segC + o]);
-                }
+        // row i's DMA landed: after it this wave issued the DMA of rows i+1 .. i+D-1 (>= NMIN each) and
+        // the stores of rows i-D+1 .. i-1 (nst each)
+        if (i >= D - 1 && i + D - 1 < n) {
+            if (PX == 1 || !full) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 1) * (NMIN + 3)) : "memory");
+            else asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 1) * (NMIN + 3 * PX)) : "memory");
+        } else {
+            vmcnt_exact(NMIN * (min(i + D - 1, n - 1) - i) + nst * min(i, D - 1));
+        }
+        const int Y = vr0 + i;
+        const uint32_t wb0 = (uint32_t)__builtin_amdgcn_readlane(lb0, i), wb1 = (uint32_t)__builtin_amdgcn_readlane(lb1, i);
+        const int ya = __builtin_amdgcn_readlane(lr0, i), yb = __builtin_amdgcn_readlane(lr1, i);
+        const bool share = ((y0 + ya) >> 1) == ((y0 + yb) >> 1);
+        if (kAblate & 2) {  // diagnostics: no pixel math (no tap reads)
+            put_fill(Y);
+        } else {
+            const int eo = kk * GRP;  // this entry's offset from entry 0
+            // NV12: U and V of a tap are adjacent bytes of the UV row; I420: the same offset in the U and V slots
+            auto chroma = [&](const uint8_t* a, int o) -> UVs {
+                if constexpr (FMT == kNV12) return uvt(a[o], a[o + 1]);
+                else return uvt(a[o], a[o + 2 * SC]);
             };
 #pragma unroll
             for (int j = 0; j < PX; j++) {
-                const uint8_t* sy0 = e + lY[j];
-                const uint8_t* sy1 = e + segY + lY[j];
-                const UVs tA = chroma(sc0, lC0[j]), tB = chroma(sc0, lC1[j]);
-                const uint32_t yA = luma_term(sy0[0]), yB = luma_term(sy0[1]);
-                const uint32_t yC = luma_term(sy1[0]), yD = luma_term(sy1[1]);
+                const uint8_t* ay = aY[j] + eo;
+                const UVs tA = chroma(aC0[j], eo), tB = chroma(aC1[j], eo);
+                const uint32_t yA = luma_term(ay[0]), yB = luma_term(ay[1]);
+                const uint32_t yC = luma_term(ay[SY]), yD = luma_term(ay[SY + 1]);
                 uint32_t h0[3], h1[3];
                 h0[0] = hpass_sat(yA, tA.b, yB, tB.b, wp[j]);
                 h0[1] = hpass_sat(yA, tA.g, yB, tB.g, wp[j]);
                 h0[2] = hpass_sat(yA, tA.r, yB, tB.r, wp[j]);
-                if (share) {
+                if (share) {  // both vertical taps in one chroma row: its terms serve both source rows
                     h1[0] = hpass_sat(yC, tA.b, yD, tB.b, wp[j]);
                     h1[1] = hpass_sat(yC, tA.g, yD, tB.g, wp[j]);
                     h1[2] = hpass_sat(yC, tA.r, yD, tB.r, wp[j]);
+                    // distinct markers end the two branches, so the compiler does not merge their common
+                    // tail behind register copies of the chroma terms
+                    asm volatile("; strip: shared chroma row" ::"v"(h1[0]), "v"(h1[1]), "v"(h1[2]));
                 } else {
-                    const UVs tC = chroma(sc1, lC0[j]), tE = chroma(sc1, lC1[j]);
+                    const UVs tC = chroma(aC0[j], eo + SC), tE = chroma(aC1[j], eo + SC);
                     h1[0] = hpass_sat(yC, tC.b, yD, tE.b, wp[j]);
                     h1[1] = hpass_sat(yC, tC.g, yD, tE.g, wp[j]);
                     h1[2] = hpass_sat(yC, tC.r, yD, tE.r, wp[j]);
+                    asm volatile("; strip: two chroma rows" ::"v"(h1[0]), "v"(h1[1]), "v"(h1[2]));
                 }
                 uint32_t v[3];
 #pragma unroll
@@ -1857,10 +1881,16 @@ __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
                 }
                 put(Y, j, v[0], v[1], v[2]);
             }
-            asm volatile("" ::: "memory");  // the stores stay ahead of the next DMA (counted waits)
-            if (i + D < n) issue(i + D, k);  // this entry's reads are done: the stores consumed them
-            asm volatile("" ::: "memory");
-            k = k + 1 == D ? 0 : k + 1;
+        }
+        asm volatile("" ::: "memory");  // the stores stay ahead of the next DMA (counted waits)
+        if (i + D < n) issue(i + D, kk);  // this entry's reads are done: the stores consumed them
+        asm volatile("" ::: "memory");
+    };
+    auto ring = [&](auto has_pad) {
+        for (int i0 = 0; i0 < n; i0 += D) {
+#pragma unroll
+            for (int kk = 0; kk < D; kk++)
+                if (i0 + kk < n) row(i0 + kk, kk, has_pad);
         }
     };
     if (anypad) ring(std::true_type{});
@@ -2784,9 +2814,7 @@ bool plan_strip(int f, const Geom& g, int DW, int DH, int count, int out_dtype, 
     if (!px) return false;
     const int nstrips = (DW + 64 * px - 1) / (64 * px);
     if (nstrips > kMaxStrips) return false;
-    p.segY = 16 * std::max(1, mY);
-    p.segC = 16 * std::max(1, mC);
-    p.grp_bytes = 2 * p.segY + 2 * npc * p.segC;
+    const int grp_bytes = (2 + 2 * npc) * kStripSlot;  // one ring entry: 2 luma + 2 x npc chroma segments
     int nw = 4, best = 1 << 30;
     for (int c = 4; c <= 8; c++) {
         const int idle = (nstrips + c - 1) / c * c - nstrips;
@@ -2796,16 +2824,17 @@ bool plan_strip(int f, const Geom& g, int DW, int DH, int count, int out_dtype, 
     if (kn.strip_nw > 0) nw = std::min(8, kn.strip_nw);
     p.nw = nw;
     p.tiles_x = (nstrips + nw - 1) / nw;
-    p.offBuf = out_dtype == EVAM_DTYPE_F32 ? kLutBytes : 0;
+    const int lut_static = out_dtype == EVAM_DTYPE_F32 ? kLutBytes : 16;  // the kernel's static LDS
     const int wg_target = std::max(1, 16 / nw);
     D = 2;
     for (int d : {4, 3, 2}) {
-        if (p.offBuf + nw * d * p.grp_bytes + 16 <= (160 * 1024) / wg_target) { D = d; break; }
+        const int need = lut_static + nw * d * grp_bytes + 16;
+        if (need <= std::min(64 * 1024, (160 * 1024) / wg_target)) { D = d; break; }
     }
     if (kn.strip_d >= 2 && kn.strip_d <= 4) D = kn.strip_d;
-    p.wave_bytes = D * p.grp_bytes;
-    lds = p.offBuf + nw * p.wave_bytes + 16;  // + 16: a right-edge tap reads one byte past its footprint (weight 0)
-    if (lds > 64 * 1024) return false;
+    p.wave_bytes = D * grp_bytes;
+    lds = nw * p.wave_bytes + 16;  // dynamic LDS; + 16: a right-edge tap reads past its footprint (weight 0)
+    if (lds + lut_static > 64 * 1024) return false;
     const int res = std::max(1, std::min(wg_target, resident_per_cu(strip_fn(f, out_dtype, D, px), lds)));
     const int64_t slots = (int64_t)n_cu * res;
     const int64_t work = (int64_t)std::min(count, kArgItems) * p.tiles_x * DH;
