@@ -1608,7 +1608,7 @@ __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
     __shared__ __attribute__((aligned(16))) float lut_s[OUT == 1 ? 768 : 4];
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     static_assert(FMT == kNV12 || FMT == kI420, "4:2:0 sources");
-    static_assert(D >= 2 && D <= 4, "ring depth");
+    static_assert(D >= 1 && D <= 4, "ring depth");
     static_assert(PX == 1 || PX == 2, "pixels per lane");
     constexpr int NPC = FMT == kI420 ? 2 : 1;  // chroma planes
     constexpr int NMIN = 2 + NPC;              // fewest DMA instructions of one row (chroma row shared)
@@ -1828,7 +1828,9 @@ __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
         constexpr bool PADC = decltype(has_pad)::value;
         // row i's DMA landed: after it this wave issued the DMA of rows i+1 .. i+D-1 (>= NMIN each) and
         // the stores of rows i-D+1 .. i-1 (nst each)
-        if (i >= D - 1 && i + D - 1 < n) {
+        if (D == 1) {  // nothing was issued after row i's DMA
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        } else if (i >= D - 1 && i + D - 1 < n) {
             if (PX == 1 || !full) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 1) * (NMIN + 3)) : "memory");
             else asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 1) * (NMIN + 3 * PX)) : "memory");
         } else {
@@ -2763,7 +2765,8 @@ bool plan_wave(int f, const Geom& g, int DW, int DH, int count, int out_dtype, i
 template <int FMT, int OUT, int PX>
 const void* strip_fn_p(int d) {
     return d == 4 ? (const void*)evam_pp_strip<FMT, OUT, 4, PX>
-                  : (d == 3 ? (const void*)evam_pp_strip<FMT, OUT, 3, PX> : (const void*)evam_pp_strip<FMT, OUT, 2, PX>);
+         : d == 3 ? (const void*)evam_pp_strip<FMT, OUT, 3, PX>
+         : d == 2 ? (const void*)evam_pp_strip<FMT, OUT, 2, PX> : (const void*)evam_pp_strip<FMT, OUT, 1, PX>;
 }
 const void* strip_fn(int f, int out, int d, int px) {
     switch ((f * 2 + out) * 2 + (px == 2)) {
@@ -2780,9 +2783,10 @@ const void* strip_fn(int f, int out, int d, int px) {
 
 // Strip-kernel plan for a uniform 4:2:0 group (fills everything in TParams but the items, LUT, output
 // and colour fields).
-//  * Pixels per lane PX: 2 (128-column strips: one ~480-byte DMA segment per source row at 3.75x) unless the
-//    output is narrower than 128 columns or a strip's footprint exceeds one 1 KB DMA instruction; the strip
-//    pattern's data movement alone is 3 us faster at 128 columns than at 64 (profiles/r03c_strip_bw.txt).
+//  * Pixels per lane PX: 2 (128-column strips: one ~480-byte DMA segment per source row at 3.75x) where
+//    the output has at least 4 such strips per row and a strip's footprint fits one 1 KB DMA instruction;
+//    the strip pattern's data movement alone is 3 us faster at 128 columns than at 64
+//    (profiles/r03c_strip_bw.txt).
 //  * Waves per workgroup: 4..8 strips with the fewest idle waves.
 //  * Tile height: about 16 waves per CU over the whole launch (the data-movement microbenchmark's best:
 //    fewer, longer-lived waves beat a full 32), at most 64 rows (the lane-held row table).
@@ -2807,7 +2811,10 @@ bool plan_strip(int f, const Geom& g, int DW, int DH, int count, int out_dtype, 
     px = 0;
     for (int cand : {2, 1}) {
         if (kn.strip_px > 0 && cand != kn.strip_px) continue;
-        if (cand == 2 && DW < 128 && kn.strip_px != 2) continue;
+        // 128-column strips only where they still give a workgroup 4 strips per row: C5 (224 columns: two
+        // 128-column strips, the second 3/4 full) runs 13.0 us in four 64-column strips and 15.6 us in
+        // two 128-column ones (profiles/r03g_c5_px.txt)
+        if (cand == 2 && (DW + 127) / 128 < 4 && kn.strip_px != 2) continue;
         wave_segments(f, g.ox, g.rw, DW, xt, x0_mask, 64 * cand, mY, mC);
         if (mY <= 64 && mC <= 64) { px = cand; break; }
     }
@@ -2831,7 +2838,7 @@ bool plan_strip(int f, const Geom& g, int DW, int DH, int count, int out_dtype, 
         const int need = lut_static + nw * d * grp_bytes + 16;
         if (need <= std::min(64 * 1024, (160 * 1024) / wg_target)) { D = d; break; }
     }
-    if (kn.strip_d >= 2 && kn.strip_d <= 4) D = kn.strip_d;
+    if (kn.strip_d >= 1 && kn.strip_d <= 4) D = kn.strip_d;
     p.wave_bytes = D * grp_bytes;
     lds = nw * p.wave_bytes + 16;  // dynamic LDS; + 16: a right-edge tap reads past its footprint (weight 0)
     if (lds + lut_static > 64 * 1024) return false;
@@ -2863,7 +2870,8 @@ hipError_t launch_strip_t(int d, const TParams& p, int grid, int lds, hipStream_
     const dim3 blk(64 * p.nw);
     if (d == 4) hipLaunchKernelGGL((evam_pp_strip<FMT, OUT, 4, PX>), dim3(grid), blk, lds, s, p);
     else if (d == 3) hipLaunchKernelGGL((evam_pp_strip<FMT, OUT, 3, PX>), dim3(grid), blk, lds, s, p);
-    else hipLaunchKernelGGL((evam_pp_strip<FMT, OUT, 2, PX>), dim3(grid), blk, lds, s, p);
+    else if (d == 2) hipLaunchKernelGGL((evam_pp_strip<FMT, OUT, 2, PX>), dim3(grid), blk, lds, s, p);
+    else hipLaunchKernelGGL((evam_pp_strip<FMT, OUT, 1, PX>), dim3(grid), blk, lds, s, p);
     return hipGetLastError();
 }
 

@@ -51,7 +51,8 @@ def test_c1_bench_batch(evam, O, coracle, gpu):
 
 # kernel shapes forced on the full-size workloads: the default choice (the strip kernel for C2 / C4 / C5),
 # the strip kernel's other ring depths and tile heights, and the staged kernel's pipeline shapes
-STAGED_SHAPES = {"default": {}, "strip_d2": {"EVAM_PP_STRIP_D": "2"}, "strip_d3": {"EVAM_PP_STRIP_D": "3"},
+STAGED_SHAPES = {"default": {}, "strip_d1": {"EVAM_PP_STRIP_D": "1"}, "strip_d2": {"EVAM_PP_STRIP_D": "2"},
+                 "strip_d3": {"EVAM_PP_STRIP_D": "3"},
                  "strip_th32": {"EVAM_PP_STRIP_TH": "32"}, "strip_px1": {"EVAM_PP_STRIP_PX": "1"},
                  "strip_xcd": {"EVAM_PP_XCD": "1"},
                  "staged": {"EVAM_PP_STRIP": "0"},

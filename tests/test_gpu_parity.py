@@ -362,7 +362,7 @@ def test_stats_and_timing(evam, O, gpu):
     ((480, 270), (224, 224), "aspect-crop"),        # C5 shape: central crop
 ])
 @pytest.mark.parametrize("variant", ["auto", "wave", "px1", "px2", "noreuse", "staged", "staged_xcd", "staged_r1",
-                                     "staged_wide", "staged_b3", "staged_slot2k", "strip", "strip_d2", "strip_d3",
+                                     "staged_wide", "staged_b3", "staged_slot2k", "strip", "strip_d1", "strip_d2", "strip_d3",
                                      "strip_th5", "strip_nw8", "strip_xcd", "strip_px1", "strip_px2",
                                      "strip_px2_d4_th7"])
 def test_wave_kernel_variants(evam, O, coracle, gpu, fmt, src, dst, resize, variant, monkeypatch):
@@ -381,6 +381,7 @@ def test_wave_kernel_variants(evam, O, coracle, gpu, fmt, src, dst, resize, vari
            "staged_b3": {"EVAM_PP_WAVE": "0", "EVAM_PP_STAGE_NBUF": "3"},
            "staged_slot2k": {"EVAM_PP_WAVE": "0", "EVAM_PP_WIDE_SLOT": "1"},
            "strip": {"EVAM_PP_STRIP": "2"}, "strip_d2": {"EVAM_PP_STRIP": "2", "EVAM_PP_STRIP_D": "2"},
+           "strip_d1": {"EVAM_PP_STRIP": "2", "EVAM_PP_STRIP_D": "1"},
            "strip_d3": {"EVAM_PP_STRIP": "2", "EVAM_PP_STRIP_D": "3"},
            "strip_th5": {"EVAM_PP_STRIP": "2", "EVAM_PP_STRIP_TH": "5"},
            "strip_nw8": {"EVAM_PP_STRIP": "2", "EVAM_PP_STRIP_NW": "8"},
