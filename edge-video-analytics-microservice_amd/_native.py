@@ -12,6 +12,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import sys
 
 LIB_NAME = "libevam_pp.so"
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
@@ -129,7 +130,17 @@ def load_library(path: str | None = None) -> ctypes.CDLL:
         return _LIB
     import torch  # noqa: F401  (binds the library to torch's HIP runtime; see module docstring)
 
-    p = path or os.environ.get("EVAM_PP_LIB") or LIB_PATH  # EVAM_PP_LIB: A/B a variant build
+    p = path or LIB_PATH
+    ab = os.environ.get("EVAM_PP_LIB")
+    if path is None and ab:
+        # A/B runs only: a variant of this library built by tools/build_variant.sh into <repo>/ab/. Anything
+        # else is refused, and the swap is announced, so a stray setting cannot silently replace the product.
+        ab_dir = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(LIB_PATH))), "ab")
+        real = os.path.realpath(ab)
+        if os.path.dirname(real) != os.path.realpath(ab_dir) or not os.path.basename(real).startswith("libevam_pp_"):
+            raise RuntimeError(f"EVAM_PP_LIB={ab}: only variant builds in {ab_dir} (tools/build_variant.sh) are loaded")
+        print(f"[evam_pp] EVAM_PP_LIB: loading the A/B variant {real}", file=sys.stderr)
+        p = real
     if not os.path.exists(p):
         raise RuntimeError(
             f"{LIB_NAME} is not built at {p}: run `python -c 'import __graft_entry__ as g; g.build()'` "

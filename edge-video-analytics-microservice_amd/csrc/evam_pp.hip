@@ -68,6 +68,26 @@ constexpr int kAblate = EVAM_PP_ABLATE;
 #ifndef EVAM_PP_LOAD_AUX
 #define EVAM_PP_LOAD_AUX 0
 #endif
+// Strip-kernel build variants (A/B builds; defaults are the measured best):
+//  * EVAM_PP_STRIP_EARLY 1: a ring entry's next DMA goes out as soon as the row's taps are in registers
+//    (before the row's arithmetic and stores) instead of after the row's stores. Same box: C2 42.2 vs
+//    42.0 us, C4 113.3 vs 110.7 us, C5 equal (profiles/r03i_bench_lines.txt): off.
+//  * EVAM_PP_STRIP_ADJ 1: lane l holds the PX adjacent columns PX l .. (one PX-wide store per channel and
+//    row) instead of columns l, l + 64 (PX dword stores of 256 contiguous bytes).
+//  * EVAM_PP_STRIP_PRIO 1: waves of odd workgroups run at s_setprio 1 (a static stagger of the otherwise
+//    lockstep waves of one SIMD, MI355X_MICROARCH.md "Two waves per SIMD" items 4 and 9).
+#ifndef EVAM_PP_STRIP_EARLY
+#define EVAM_PP_STRIP_EARLY 0
+#endif
+#ifndef EVAM_PP_STRIP_ADJ
+#define EVAM_PP_STRIP_ADJ 0
+#endif
+#ifndef EVAM_PP_STRIP_PRIO
+#define EVAM_PP_STRIP_PRIO 0
+#endif
+constexpr bool kStripEarly = EVAM_PP_STRIP_EARLY != 0;
+constexpr bool kStripAdj = EVAM_PP_STRIP_ADJ != 0;
+constexpr bool kStripPrio = EVAM_PP_STRIP_PRIO != 0;
 
 // OpenCV color_yuv.simd.hpp ITUR_BT_601_*; the -128 chroma bias is folded into the constants.
 constexpr int kCY = 1220542, kCUB = 2116026, kCUG = -409993, kCVG = -852492, kCVR = 1673527;
@@ -1562,9 +1582,10 @@ __global__ __launch_bounds__(kThreads) void evam_pp_wave(const WParams P) {
 // strip kernel (uniform geometry, 4:2:0 sources, no shared source rows between output rows)
 // ------------------------------------------------------------------------------------------------
 constexpr int kMaxStrips = 32;  // per-strip footprints in the kernel arguments: DW <= 2048
-// One staged row segment of the strip kernel: a strip's footprint is at most 64 16-byte chunks (one DMA
-// instruction), so every LDS offset of the ring is a compile-time immediate.
-constexpr int kStripSlot = 1024;
+// One staged row segment of the strip kernel: a strip's footprint is at most one DMA instruction's 64
+// 16-byte chunks, so every LDS offset of the ring is a compile-time immediate. 64-column strips (PX = 1)
+// use half-size slots (footprints <= 512 B, downscales <= ~7.7x): half the LDS per wave.
+constexpr int strip_slot(int px) { return px == 1 ? 512 : 1024; }
 
 struct TParams {
     ItemArg items[kArgItems];
@@ -1576,12 +1597,16 @@ struct TParams {
     int cw, ch, rw, rh, ox, oy;  // the launch's crop size, resized size and placement (uniform)
     int nw;                      // waves (strips) per workgroup
     int TH, tiles_x, tiles_per_item;  // tile = nw strips x TH rows
-    int wave_bytes;              // one wave's ring: D entries of kStripSlot-byte segments
+    int wave_bytes;              // one wave's ring: D entries of strip_slot(PX)-byte segments
     int color_rgb;
     uint32_t fill;
     int xcd_remap;               // 1: consecutive tiles land on one XCD
     int2 sfoot[kMaxStrips];      // per strip: crop-relative source columns of the first visible column's
                                  // first tap and the last visible column's last tap; (-1, -1): padding only
+    // band kernel only: one wave per (item, band of TH rows, strip); LDS rows of one band
+    int nstrips, units;          // strips per row; waves of work in the launch
+    int segY, segC;              // bytes of one staged luma / chroma row (multiples of 16)
+    int nrY;                     // most luma rows of one band (the chroma rows follow at nrY * segY)
 };
 
 // Row-strip kernel for uniform-geometry 4:2:0 batches whose output rows do not share source rows
@@ -1620,6 +1645,7 @@ __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
     asm volatile("" ::"s"(p_nw), "s"(p_tpi), "s"(p_tx), "s"(p_TH), "s"(p_DH), "s"(p_DW), "s"(p_grid), "s"(P.xcd_remap),
                  "s"(P.ox), "s"(P.rw), "s"(P.oy), "s"(P.rh), "s"(P.wave_bytes));
     const int t = P.xcd_remap ? xcd_tile(blockIdx.x, p_grid) : (int)blockIdx.x;
+    if (kStripPrio && (blockIdx.x & 1)) __builtin_amdgcn_s_setprio(1);
     const int item = t / p_tpi;
     const int tile = t - item * p_tpi;
     const int ty = tile / p_tx;
@@ -1657,8 +1683,8 @@ __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
     const __amdgpu_buffer_rsrc_t rsU = __builtin_amdgcn_make_buffer_rsrc((void*)p1, (short)0, 0x7FFFFFFF, 0x00020000);
     const __amdgpu_buffer_rsrc_t rsV = __builtin_amdgcn_make_buffer_rsrc((void*)(NPC == 2 ? p2 : p1), (short)0, 0x7FFFFFFF, 0x00020000);
     uint8_t* const wbuf = smem + wave * P.wave_bytes;
-    // ring entry: [Y tap0][Y tap1][C tap0][C tap1] (+ [V tap0][V tap1] for I420), kStripSlot bytes each
-    constexpr int SY = kStripSlot, SC = kStripSlot, GRP = 2 * SY + 2 * NPC * SC;
+    // ring entry: [Y tap0][Y tap1][C tap0][C tap1] (+ [V tap0][V tap1] for I420), strip_slot(PX) bytes each
+    constexpr int SY = strip_slot(PX), SC = strip_slot(PX), GRP = 2 * SY + 2 * NPC * SC;
     constexpr int segY = SY, segC = SC;
     auto issue = [&](int i, int k) {
         if (kAblate & 16) return;  // diagnostics: no DMA
@@ -1711,7 +1737,7 @@ __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
     const size_t esz = OUT == 1 ? 4 : 1;
 #pragma unroll
     for (int j = 0; j < PX; j++) {
-        const int X = X0 + lane + 64 * j;
+        const int X = kStripAdj ? X0 + PX * lane + j : X0 + lane + 64 * j;
         xin[j] = live && X < p_DW;
         vo[j] = (uint32_t)(xin[j] ? X : 0) * (uint32_t)esz;
         lY[j] = lC0[j] = lC1[j] = wp[j] = 0;
@@ -1736,8 +1762,9 @@ __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
     }
     // some visible lane shows letterbox columns (wave-uniform): only then the per-pixel fill select
     const bool anypad = cols && __builtin_amdgcn_ballot_w64(anyp) != 0;
-    // stores per row of this wave: 3 per pixel column group with any lane inside the output (counted waits)
-    const bool full = X0 + 64 * (PX - 1) < p_DW;
+    // stores per row of this wave: 3 per pixel column group with any lane inside the output (counted waits);
+    // adjacent columns: 3 (one PX-wide store per channel)
+    const bool full = !kStripAdj && X0 + 64 * (PX - 1) < p_DW;
 
     const size_t plane = (size_t)p_DW * p_DH;
     uint8_t* const d0 = reinterpret_cast<uint8_t*>(P.dst) + (size_t)(P.slot_offset + it.index * P.slot_stride) * 3 * plane * esz;
@@ -1814,9 +1841,28 @@ __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
             __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v2, rsO2, vo[j], so, EVAM_PP_STORE_AUX);
         }
     };
-    auto put_fill = [&](int Y) {
+    // a whole row of the lane's PX pixels, vv[c][j] in source channel order
+    auto put_row = [&](int Y, const uint32_t (&vv)[3][PX]) {
+        if constexpr (kStripAdj) {
+            if (!xin[0]) return;  // DW % PX == 0 (host): a lane's pixels are all in or all out
+            if (kAblate & 4) {
+                asm volatile("" ::"v"(vv[0][0]), "v"(vv[1][0]), "v"(vv[2][0]));
+                return;
+            }
+            const uint32_t off = vo[0] + (uint32_t)(Y * p_DW) * (uint32_t)esz;  // soffset 0: wide-store hazard
+            store_off<OUT, PX>(rsO0, off, lutb, vv[0]);
+            store_off<OUT, PX>(rsO1, off, lutb + 1024, vv[1]);
+            store_off<OUT, PX>(rsO2, off, lutb + 2048, vv[2]);
+        } else {
 #pragma unroll
-        for (int j = 0; j < PX; j++) put(Y, j, fill0, fill1, fill2);
+            for (int j = 0; j < PX; j++) put(Y, j, vv[0][j], vv[1][j], vv[2][j]);
+        }
+    };
+    auto put_fill = [&](int Y) {
+        uint32_t vv[3][PX];
+#pragma unroll
+        for (int j = 0; j < PX; j++) { vv[0][j] = fill0; vv[1][j] = fill1; vv[2][j] = fill2; }
+        put_row(Y, vv);
     };
     // letterbox rows above the ring: before its DMA in issue order, so they never enter the counted waits
     const int ra = n ? vr0 : Y1;
@@ -1826,35 +1872,60 @@ __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
     // one output row: row i of the tile's visible rows, ring entry kk (compile-time after unrolling)
     auto row = [&](int i, int kk, auto has_pad) {
         constexpr bool PADC = decltype(has_pad)::value;
-        // row i's DMA landed: after it this wave issued the DMA of rows i+1 .. i+D-1 (>= NMIN each) and
-        // the stores of rows i-D+1 .. i-1 (nst each)
-        if (D == 1) {  // nothing was issued after row i's DMA
+        // row i's DMA landed. Issued after it: the DMA of rows i+1 .. i+D-1 (>= NMIN each) and the stores
+        // of rows i-D+1 .. i-1 (nst each); with the early issue (row j's successor DMA goes out before row
+        // j's stores) also the stores of row i-D.
+        constexpr int SD = kStripEarly ? D : D - 1;
+        if (SD == 0) {  // nothing was issued after row i's DMA
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        } else if (i >= D - 1 && i + D - 1 < n) {
-            if (PX == 1 || !full) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 1) * (NMIN + 3)) : "memory");
-            else asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 1) * (NMIN + 3 * PX)) : "memory");
+        } else if (i >= SD && i + D - 1 < n) {
+            if (PX == 1 || !full) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 1) * NMIN + SD * 3) : "memory");
+            else asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 1) * NMIN + SD * 3 * PX) : "memory");
         } else {
-            vmcnt_exact(NMIN * (min(i + D - 1, n - 1) - i) + nst * min(i, D - 1));
+            vmcnt_exact(NMIN * (min(i + D - 1, n - 1) - i) + nst * min(i, SD));
         }
         const int Y = vr0 + i;
         const uint32_t wb0 = (uint32_t)__builtin_amdgcn_readlane(lb0, i), wb1 = (uint32_t)__builtin_amdgcn_readlane(lb1, i);
         const int ya = __builtin_amdgcn_readlane(lr0, i), yb = __builtin_amdgcn_readlane(lr1, i);
         const bool share = ((y0 + ya) >> 1) == ((y0 + yb) >> 1);
         if (kAblate & 2) {  // diagnostics: no pixel math (no tap reads)
+            if (kStripEarly && i + D < n) issue(i + D, kk);
             put_fill(Y);
         } else {
             const int eo = kk * GRP;  // this entry's offset from entry 0
-            // NV12: U and V of a tap are adjacent bytes of the UV row; I420: the same offset in the U and V slots
-            auto chroma = [&](const uint8_t* a, int o) -> UVs {
-                if constexpr (FMT == kNV12) return uvt(a[o], a[o + 1]);
-                else return uvt(a[o], a[o + 2 * SC]);
+            // raw taps of the entry into registers: luma bytes of both source rows, chroma of the first
+            // chroma row and, when the second source row has its own, of the second
+            uint32_t rY[PX][4], rC[PX][2][2], rE[PX][2][2];
+            auto raw_c = [&](const uint8_t* a, int o, uint32_t (&c)[2]) {
+                c[0] = a[o];
+                c[1] = FMT == kNV12 ? a[o + 1] : a[o + 2 * SC];  // NV12: interleaved UV; I420: the V slot
             };
 #pragma unroll
             for (int j = 0; j < PX; j++) {
                 const uint8_t* ay = aY[j] + eo;
-                const UVs tA = chroma(aC0[j], eo), tB = chroma(aC1[j], eo);
-                const uint32_t yA = luma_term(ay[0]), yB = luma_term(ay[1]);
-                const uint32_t yC = luma_term(ay[SY]), yD = luma_term(ay[SY + 1]);
+                rY[j][0] = ay[0]; rY[j][1] = ay[1]; rY[j][2] = ay[SY]; rY[j][3] = ay[SY + 1];
+                raw_c(aC0[j], eo, rC[j][0]);
+                raw_c(aC1[j], eo, rC[j][1]);
+            }
+            if (!share) {
+#pragma unroll
+                for (int j = 0; j < PX; j++) {
+                    raw_c(aC0[j], eo + SC, rE[j][0]);
+                    raw_c(aC1[j], eo + SC, rE[j][1]);
+                }
+            }
+            if constexpr (kStripEarly) {
+                // the entry's bytes are in registers: its next row's DMA overlaps this row's arithmetic
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                if (i + D < n) issue(i + D, kk);
+                asm volatile("" ::: "memory");
+            }
+            uint32_t vv[3][PX];
+#pragma unroll
+            for (int j = 0; j < PX; j++) {
+                const UVs tA = uvt(rC[j][0][0], rC[j][0][1]), tB = uvt(rC[j][1][0], rC[j][1][1]);
+                const uint32_t yA = luma_term(rY[j][0]), yB = luma_term(rY[j][1]);
+                const uint32_t yC = luma_term(rY[j][2]), yD = luma_term(rY[j][3]);
                 uint32_t h0[3], h1[3];
                 h0[0] = hpass_sat(yA, tA.b, yB, tB.b, wp[j]);
                 h0[1] = hpass_sat(yA, tA.g, yB, tB.g, wp[j]);
@@ -1867,7 +1938,7 @@ __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
                     // tail behind register copies of the chroma terms
                     asm volatile("; strip: shared chroma row" ::"v"(h1[0]), "v"(h1[1]), "v"(h1[2]));
                 } else {
-                    const UVs tC = chroma(aC0[j], eo + SC), tE = chroma(aC1[j], eo + SC);
+                    const UVs tC = uvt(rE[j][0][0], rE[j][0][1]), tE = uvt(rE[j][1][0], rE[j][1][1]);
                     h1[0] = hpass_sat(yC, tC.b, yD, tE.b, wp[j]);
                     h1[1] = hpass_sat(yC, tC.g, yD, tE.g, wp[j]);
                     h1[2] = hpass_sat(yC, tC.r, yD, tE.r, wp[j]);
@@ -1881,11 +1952,16 @@ __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
                     v[1] = padc[j] ? fill1 : v[1];
                     v[2] = padc[j] ? fill2 : v[2];
                 }
-                put(Y, j, v[0], v[1], v[2]);
+                if constexpr (kStripAdj) {
+                    vv[0][j] = v[0]; vv[1][j] = v[1]; vv[2][j] = v[2];
+                } else {
+                    put(Y, j, v[0], v[1], v[2]);
+                }
             }
+            if constexpr (kStripAdj) put_row(Y, vv);
         }
-        asm volatile("" ::: "memory");  // the stores stay ahead of the next DMA (counted waits)
-        if (i + D < n) issue(i + D, kk);  // this entry's reads are done: the stores consumed them
+        asm volatile("" ::: "memory");  // issue order is what the counted waits assume
+        if (!kStripEarly && i + D < n) issue(i + D, kk);  // this entry's reads are done: the stores consumed them
         asm volatile("" ::: "memory");
     };
     auto ring = [&](auto has_pad) {
@@ -1899,6 +1975,263 @@ __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
     else ring(std::false_type{});
     // letterbox rows below the ring
     for (int Y = max(ra, vr1); Y < Y1; Y++) put_fill(Y);
+}
+
+// Band kernel for uniform 4:2:0 batches whose consecutive output rows share source rows (vertical
+// upscales: C1). One wave owns one band of TH output rows of one 64·PX-column strip (lane l: the PX
+// adjacent columns X0 + PX l ..), with no workgroup barrier after the prologue:
+//  * every source row the band reads (luma rows r0(first) .. r1(last), and their chroma rows) is staged
+//    once, in need order, by one LDS-DMA instruction per row segment at the start; output row i then
+//    waits with one counted vmcnt for the rows it needs, so its arithmetic overlaps the later rows' DMA;
+//  * horizontal results stay in registers per source row (HA: row pa, HB: row pb) and the BT.601 chroma
+//    terms per chroma row, so a source row is converted and filtered once however many output rows read
+//    it (~0.84 source rows per output row at 432 -> 512);
+//  * coefficients of the strip's columns (per lane) and of the band's rows (one per lane, v_readlane)
+//    come from the kernels' shared linear_coef: no table loads;
+//  * each channel of a row leaves as one PX-wide store per lane.
+template <int FMT, int OUT, int PX>
+__global__ __launch_bounds__(256) void evam_pp_band(const TParams P) {
+    __shared__ __attribute__((aligned(16))) float lut_s[OUT == 1 ? 768 : 4];
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    static_assert(FMT == kNV12 || FMT == kI420, "4:2:0 sources");
+    static_assert(PX == 1 || PX == 2 || PX == 4, "pixels per lane");
+    constexpr int NPC = FMT == kI420 ? 2 : 1;  // chroma planes
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int p_tpi = P.tiles_per_item, p_ns = P.nstrips, p_TH = P.TH, p_DH = P.DH, p_DW = P.DW;
+    asm volatile("" ::"s"(p_tpi), "s"(p_ns), "s"(p_TH), "s"(p_DH), "s"(p_DW), "s"(P.units), "s"(P.ox), "s"(P.rw),
+                 "s"(P.oy), "s"(P.rh), "s"(P.wave_bytes), "s"(P.segY), "s"(P.segC), "s"(P.nrY));
+    // wave unit u -> (item, band, strip); consecutive waves: neighbouring strips of one band
+    const int u = (int)blockIdx.x * (blockDim.x >> 6) + wave;
+    const bool live = u < P.units;
+    const int uu = live ? u : 0;
+    const int item = uu / p_tpi;
+    const int rem = uu - item * p_tpi;
+    const int band = rem / p_ns;
+    const int strip = rem - band * p_ns;
+    const int Y0 = band * p_TH, Y1 = min(Y0 + p_TH, p_DH);
+    const ItemArg& it = P.items[item];
+    const uint8_t* p0 = it.plane[0];
+    const uint8_t* p1 = it.plane[1];
+    const uint8_t* p2 = it.plane[2];
+    const int pitch0 = it.pitch[0], pitch1 = it.pitch[1], pitch2 = it.pitch[2];
+    const int x0 = it.x0, y0 = it.y0;
+    const int X0 = strip * 64 * PX;
+    const int2 sf = P.sfoot[min(strip, kMaxStrips - 1)];
+    asm volatile("" ::"s"(p0), "s"(p1), "s"(p2), "s"(pitch0), "s"(pitch1), "s"(pitch2), "s"(x0), "s"(y0),
+                 "s"(it.index), "s"(sf.x), "s"(sf.y), "s"(P.dst), "s"(P.slot_offset), "s"(P.slot_stride));
+    const bool cols = live && sf.x >= 0;
+    int fsY = 0, nY = 0, fsC = 0, nC = 0;
+    if (cols) footprint_chunks(FMT, 1, x0 + sf.x, x0 + sf.y, fsY, nY, fsC, nC);
+    const int vr0 = max(Y0, P.oy), vr1 = min(Y1, P.oy + P.rh);
+    const int n = cols && vr1 > vr0 ? vr1 - vr0 : 0;  // visible rows of the band (<= 64)
+
+    // row table, one visible row per lane: source rows relative to the crop, weights << 8
+    int lr0 = 0, lr1 = 0, lb0 = 0, lb1 = 0;
+    if (lane < n) {
+        int sy, b0, b1;
+        linear_coef(vr0 + lane - P.oy, P.scale_y, P.ch, false, sy, b0, b1);
+        lr0 = min(max(sy, 0), P.ch - 1);
+        lr1 = min(max(sy + 1, 0), P.ch - 1);
+        lb0 = b0 << 8;
+        lb1 = b1 << 8;
+    }
+    const __amdgpu_buffer_rsrc_t rsY = __builtin_amdgcn_make_buffer_rsrc((void*)p0, (short)0, 0x7FFFFFFF, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsU = __builtin_amdgcn_make_buffer_rsrc((void*)p1, (short)0, 0x7FFFFFFF, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsV = __builtin_amdgcn_make_buffer_rsrc((void*)(NPC == 2 ? p2 : p1), (short)0, 0x7FFFFFFF, 0x00020000);
+    uint8_t* const wbuf = smem + wave * P.wave_bytes;
+    const int segY = P.segY, segC = P.segC;
+    uint8_t* const cbuf = wbuf + P.nrY * segY;  // chroma rows; I420: V row k at + segC / 2 (segC holds U | V)
+    // source rows of the band (rows are monotonic in the output row): luma [rlo, rhi], chroma [clo, chi]
+    const int rlo = n ? __builtin_amdgcn_readlane(lr0, 0) : 0;
+    const int rhi = n ? __builtin_amdgcn_readlane(lr1, n - 1) : -1;
+    const int clo = (y0 + rlo) >> 1;
+    // fp32: the LUT (3 KB, sections in source channel order) by LDS-DMA ahead of the rows, so no VGPR waits
+    // on it and the rows' counted waits are unaffected (it is older)
+    if constexpr (OUT == 1) {
+        for (int c0 = wave * 64; c0 < 192; c0 += (int)(blockDim.x >> 6) * 64) {
+            const int c = c0 + lane, sec = c >> 6;
+            const int src = ((P.color_rgb ? 2 - sec : sec) * 64 + (c & 63)) * 16;
+            const __amdgpu_buffer_rsrc_t rsL = __builtin_amdgcn_make_buffer_rsrc((void*)P.lut, (short)0, 3072, 0x00020000);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsL, (__attribute__((address_space(3))) void*)((uint8_t*)lut_s + c0 * 16),
+                                                     16, (uint32_t)src, 0, 0, 0);
+        }
+    }
+    // DMA in need order: luma row r, then its chroma row when r is the first row reading it. Instructions
+    // issued up to row r: kd(r) = (r - rlo + 1) + NPC (c(r) - clo + 1).
+    if (n) {
+        const uint32_t vo = (uint32_t)lane * 16u;
+        int cprev = -1;
+        for (int r = rlo; r <= rhi; r++) {
+            const int ya = y0 + r, c = ya >> 1;
+            if (lane < nY)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rsY, (__attribute__((address_space(3))) void*)(wbuf + (r - rlo) * segY),
+                                                         16, vo, ya * pitch0 + fsY, EVAM_PP_LOAD_AUX, 0);
+            if (c != cprev) {
+                uint8_t* cb = cbuf + (c - clo) * segC;
+                if (lane < nC) {
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsU, (__attribute__((address_space(3))) void*)cb, 16, vo,
+                                                             c * pitch1 + fsC, EVAM_PP_LOAD_AUX, 0);
+                    if constexpr (NPC == 2)
+                        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsV, (__attribute__((address_space(3))) void*)(cb + segC / 2),
+                                                                 16, vo, c * pitch2 + fsC, EVAM_PP_LOAD_AUX, 0);
+                }
+                cprev = c;
+            }
+        }
+    }
+    const int kd_total = n ? (rhi - rlo + 1) + NPC * (((y0 + rhi) >> 1) - clo + 1) : 0;
+
+    if constexpr (OUT == 1) {
+        vmcnt_exact(kd_total);  // this wave's LUT pieces landed (issued before every row)
+        __syncthreads();        // ... and every other wave's
+    }
+    if (!live) return;
+
+    // per-lane column state: tap offsets in the staged rows (tap 0 low, tap 1 high half), packed 11-bit
+    // weights, padding columns
+    const int X = X0 + lane * PX;
+    const bool xin = X < p_DW;  // DW % PX == 0: a lane's pixels are all in or all out
+    uint32_t lY[PX], lC[PX], wp[PX];
+    bool padc[PX];
+    bool anyp = false;
+#pragma unroll
+    for (int j = 0; j < PX; j++) {
+        lY[j] = lC[j] = wp[j] = 0;
+        padc[j] = true;
+        const int dx = X + j - P.ox;
+        if (cols && xin && dx >= 0 && dx < P.rw) {
+            int s0, a0, a1;
+            linear_coef(dx, P.scale_x, P.cw, true, s0, a0, a1);
+            const int ca = x0 + s0, cb = x0 + min(s0 + 1, P.cw - 1);
+            lY[j] = (uint32_t)(ca - fsY) | ((uint32_t)(cb - fsY) << 16);
+            if constexpr (FMT == kNV12)
+                lC[j] = (uint32_t)(2 * (ca >> 1) - fsC) | ((uint32_t)(2 * (cb >> 1) - fsC) << 16);
+            else
+                lC[j] = (uint32_t)((ca >> 1) - fsC) | ((uint32_t)((cb >> 1) - fsC) << 16);
+            wp[j] = (uint32_t)a0 | ((uint32_t)a1 << 16);
+            padc[j] = false;
+        }
+        anyp |= xin && padc[j];
+    }
+    const bool anypad = __builtin_amdgcn_ballot_w64(anyp) != 0;
+    const size_t esz = OUT == 1 ? 4 : 1;
+    const uint32_t vo = (uint32_t)(xin ? X : 0) * (uint32_t)esz;
+    const size_t plane = (size_t)p_DW * p_DH;
+    uint8_t* const d0 = reinterpret_cast<uint8_t*>(P.dst) + (size_t)(P.slot_offset + it.index * P.slot_stride) * 3 * plane * esz;
+    uint8_t* const d1 = d0 + plane * esz;
+    uint8_t* const d2 = d1 + plane * esz;
+    const __amdgpu_buffer_rsrc_t rsO0 = __builtin_amdgcn_make_buffer_rsrc((void*)(P.color_rgb ? d2 : d0), (short)0, 0x7FFFFFFF, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsO1 = __builtin_amdgcn_make_buffer_rsrc((void*)d1, (short)0, 0x7FFFFFFF, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsO2 = __builtin_amdgcn_make_buffer_rsrc((void*)(P.color_rgb ? d0 : d2), (short)0, 0x7FFFFFFF, 0x00020000);
+    const uint32_t fq0 = P.fill & 0xFF, fq1 = (P.fill >> 8) & 0xFF, fq2 = (P.fill >> 16) & 0xFF;
+    const uint32_t fsh = OUT == 1 ? 2 : 0;
+    const uint32_t fill0 = (P.color_rgb ? fq2 : fq0) << fsh, fill1 = fq1 << fsh, fill2 = (P.color_rgb ? fq0 : fq2) << fsh;
+    const uint8_t* lutb = reinterpret_cast<const uint8_t*>(lut_s);
+    // one row of the strip: v[c][j] = LUT byte offsets (fp32) or bytes (u8) in source channel order; the
+    // row offset in the VGPR offset (soffset 0: the store-data hazard of wide stores, see evam_pp_wave)
+    auto put = [&](int Y, const uint32_t (&v)[3][PX]) {
+        if (!xin) return;
+        const uint32_t off = vo + (uint32_t)(Y * p_DW) * (uint32_t)esz;
+        store_off<OUT, PX>(rsO0, off, lutb, v[0]);
+        store_off<OUT, PX>(rsO1, off, lutb + 1024, v[1]);
+        store_off<OUT, PX>(rsO2, off, lutb + 2048, v[2]);
+    };
+    auto put_fill = [&](int Y) {
+        uint32_t v[3][PX];
+#pragma unroll
+        for (int j = 0; j < PX; j++) { v[0][j] = fill0; v[1][j] = fill1; v[2][j] = fill2; }
+        put(Y, v);
+    };
+    for (int Y = Y0; Y < (n ? vr0 : Y1); Y++) put_fill(Y);  // letterbox rows above
+
+    uint32_t kb = kKBs, kg = kKGs, kr = kKRs;
+    int cvg = kCVG, cug = kCUG;
+    asm volatile("" : "+v"(kb), "+v"(kg), "+v"(kr), "+s"(cvg), "+s"(cug));
+    auto uvt = [&](uint32_t U, uint32_t V) {
+        int gu = __mul24((int)U, cug) + (int)kg;
+        asm("" : "+v"(gu));
+        return UVs{__umul24(U, (uint32_t)kCUB) + kb, (uint32_t)(__mul24((int)V, cvg) + gu), __umul24(V, (uint32_t)kCVR) + kr};
+    };
+    // chroma terms of the chroma row cc for both taps of every pixel (kept across source rows)
+    UVs tA[PX], tB[PX];
+    int cc = -1;
+    auto chroma_row = [&](int c) {
+        const uint8_t* cb = cbuf + (c - clo) * segC;
+#pragma unroll
+        for (int j = 0; j < PX; j++) {
+            const uint8_t* a0 = cb + (lC[j] & 0xFFFF);
+            const uint8_t* a1 = cb + (lC[j] >> 16);
+            if constexpr (FMT == kNV12) {
+                tA[j] = uvt(a0[0], a0[1]);
+                tB[j] = uvt(a1[0], a1[1]);
+            } else {
+                tA[j] = uvt(a0[0], a0[segC / 2]);
+                tB[j] = uvt(a1[0], a1[segC / 2]);
+            }
+        }
+        cc = c;
+    };
+    // horizontal pass of source row r (crop-relative) into H
+    auto hrow = [&](int r, uint32_t (&H)[PX][3]) {
+        const int c = (y0 + r) >> 1;
+        if (c != cc) chroma_row(c);
+        const uint8_t* yb = wbuf + (r - rlo) * segY;
+#pragma unroll
+        for (int j = 0; j < PX; j++) {
+            const uint32_t yA = luma_term(yb[lY[j] & 0xFFFF]), yB = luma_term(yb[lY[j] >> 16]);
+            H[j][0] = hpass_sat(yA, tA[j].b, yB, tB[j].b, wp[j]);
+            H[j][1] = hpass_sat(yA, tA[j].g, yB, tB[j].g, wp[j]);
+            H[j][2] = hpass_sat(yA, tA[j].r, yB, tB[j].r, wp[j]);
+        }
+    };
+    uint32_t HA[PX][3], HB[PX][3];
+    int pa = -1, pb = -1;
+    const int nst = 3;  // stores per output row (one PX-wide store per channel)
+    for (int i = 0; i < n; i++) {
+        const int ra = __builtin_amdgcn_readlane(lr0, i), rb = __builtin_amdgcn_readlane(lr1, i);
+        // rows up to rb landed: issued after them, the DMA of later rows and the stores of rows 0 .. i-1
+        const int kd = (rb - rlo + 1) + NPC * (((y0 + rb) >> 1) - clo + 1);
+        vmcnt_exact(kd_total - kd + nst * i);
+        const uint32_t wb0 = (uint32_t)__builtin_amdgcn_readlane(lb0, i), wb1 = (uint32_t)__builtin_amdgcn_readlane(lb1, i);
+        // HA <- row ra, HB <- row rb, reusing what the previous output row filtered (wave-uniform branches)
+        if (ra != pa) {
+            if (ra == pb) {
+#pragma unroll
+                for (int j = 0; j < PX; j++)
+#pragma unroll
+                    for (int c = 0; c < 3; c++) HA[j][c] = HB[j][c];
+            } else {
+                hrow(ra, HA);
+            }
+        }
+        if (rb == ra) {
+#pragma unroll
+            for (int j = 0; j < PX; j++)
+#pragma unroll
+                for (int c = 0; c < 3; c++) HB[j][c] = HA[j][c];
+        } else if (rb != pb || ra == pb) {  // HB was overwritten into HA above, or holds another row
+            hrow(rb, HB);
+        }
+        pa = ra;
+        pb = rb;
+        uint32_t v[3][PX];
+#pragma unroll
+        for (int j = 0; j < PX; j++)
+#pragma unroll
+            for (int c = 0; c < 3; c++) v[c][j] = vfinal<OUT>(HA[j][c], HB[j][c], wb0, wb1);
+        if (anypad) {
+#pragma unroll
+            for (int j = 0; j < PX; j++) {
+                v[0][j] = padc[j] ? fill0 : v[0][j];
+                v[1][j] = padc[j] ? fill1 : v[1][j];
+                v[2][j] = padc[j] ? fill2 : v[2][j];
+            }
+        }
+        put(vr0 + i, v);
+        asm volatile("" ::: "memory");  // issue order is what the counted waits assume
+    }
+    for (int Y = max(n ? vr1 : Y1, Y0); Y < Y1; Y++) put_fill(Y);  // letterbox rows below
 }
 
 static_assert(sizeof(evam_roi) == 20, "evam_roi layout");
@@ -2434,8 +2767,12 @@ struct Knobs {
     int roi_nbuf = 2;                              // ROI staging buffers (3: two groups of DMA in flight)
     int strip = 1, strip_th = -1, strip_d = -1, strip_nw = -1, strip_px = 0;  // strip kernel: allowed (2: forced),
                                                                               // rows per tile, ring depth, waves, px
+    int strip_waves = 16;                          // strip / band kernels: resident waves per CU the tiles are sized for
+    int band = 1, band_px = 0;                     // band kernel: allowed (2: forced), pixels per lane
     void read() {
+        band = env_int("EVAM_PP_BAND", band); band_px = env_int("EVAM_PP_BAND_PX", band_px);
         strip = env_int("EVAM_PP_STRIP", strip); strip_th = env_int("EVAM_PP_STRIP_TH", strip_th);
+        strip_waves = env_int("EVAM_PP_STRIP_WAVES", strip_waves);
         strip_d = env_int("EVAM_PP_STRIP_D", strip_d); strip_nw = env_int("EVAM_PP_STRIP_NW", strip_nw);
         strip_px = env_int("EVAM_PP_STRIP_PX", strip_px);
         staged = env_int("EVAM_PP_STAGED", staged); wave = env_int("EVAM_PP_WAVE", wave);
@@ -2788,9 +3125,10 @@ const void* strip_fn(int f, int out, int d, int px) {
 //    the strip pattern's data movement alone is 3 us faster at 128 columns than at 64
 //    (profiles/r03c_strip_bw.txt).
 //  * Waves per workgroup: 4..8 strips with the fewest idle waves.
-//  * Tile height: about 16 waves per CU over the whole launch (the data-movement microbenchmark's best:
-//    fewer, longer-lived waves beat a full 32), at most 64 rows (the lane-held row table).
-//  * Ring depth D: the deepest (<= 4) whose LDS still admits those workgroups.
+//  * Tile height: about EVAM_PP_STRIP_WAVES (16) waves per CU over the whole launch (the data-movement
+//    microbenchmark's best: fewer, longer-lived waves beat a full 32), at most 64 rows (the lane-held row
+//    table).
+//  * Ring depth D: 2 (D 3 / 4 measured slower on C2, D 1 slower on C2 and C5).
 // Returns false when the geometry does not suit it: outputs wider than kMaxStrips strips, footprints over
 // 1 KB per strip, or consecutive output rows that share source rows (vertical upscales: the wave kernel's
 // REUSE path).
@@ -2815,13 +3153,15 @@ bool plan_strip(int f, const Geom& g, int DW, int DH, int count, int out_dtype, 
         // 128-column strips, the second 3/4 full) runs 13.0 us in four 64-column strips and 15.6 us in
         // two 128-column ones (profiles/r03g_c5_px.txt)
         if (cand == 2 && (DW + 127) / 128 < 4 && kn.strip_px != 2) continue;
+        if (kStripAdj && DW % cand) continue;  // adjacent columns: a lane's pixels all in or all out
         wave_segments(f, g.ox, g.rw, DW, xt, x0_mask, 64 * cand, mY, mC);
-        if (mY <= 64 && mC <= 64) { px = cand; break; }
+        const int cap = strip_slot(cand) / 16;  // chunks of one slot
+        if (mY <= cap && mC <= cap) { px = cand; break; }
     }
     if (!px) return false;
     const int nstrips = (DW + 64 * px - 1) / (64 * px);
     if (nstrips > kMaxStrips) return false;
-    const int grp_bytes = (2 + 2 * npc) * kStripSlot;  // one ring entry: 2 luma + 2 x npc chroma segments
+    const int grp_bytes = (2 + 2 * npc) * strip_slot(px);  // one ring entry: 2 luma + 2 x npc chroma segments
     int nw = 4, best = 1 << 30;
     for (int c = 4; c <= 8; c++) {
         const int idle = (nstrips + c - 1) / c * c - nstrips;
@@ -2832,12 +3172,8 @@ bool plan_strip(int f, const Geom& g, int DW, int DH, int count, int out_dtype, 
     p.nw = nw;
     p.tiles_x = (nstrips + nw - 1) / nw;
     const int lut_static = out_dtype == EVAM_DTYPE_F32 ? kLutBytes : 16;  // the kernel's static LDS
-    const int wg_target = std::max(1, 16 / nw);
-    D = 2;
-    for (int d : {4, 3, 2}) {
-        const int need = lut_static + nw * d * grp_bytes + 16;
-        if (need <= std::min(64 * 1024, (160 * 1024) / wg_target)) { D = d; break; }
-    }
+    const int wg_target = std::max(1, std::min(32, kn.strip_waves) / nw);
+    D = 2;  // deeper rings measured slower (profiles/r03f_bench_lines.txt: C2 D 3 +2.7 us)
     if (kn.strip_d >= 1 && kn.strip_d <= 4) D = kn.strip_d;
     p.wave_bytes = D * grp_bytes;
     lds = nw * p.wave_bytes + 16;  // dynamic LDS; + 16: a right-edge tap reads past its footprint (weight 0)
@@ -2885,6 +3221,116 @@ hipError_t launch_strip(int f, int out, int d, int px, const TParams& p, int gri
     case (kI420 * 2 + 0) * 2 + 1: return launch_strip_t<kI420, 0, 2>(d, p, grid, lds, s);
     case (kI420 * 2 + 1) * 2: return launch_strip_t<kI420, 1, 1>(d, p, grid, lds, s);
     default: return launch_strip_t<kI420, 1, 2>(d, p, grid, lds, s);
+    }
+}
+
+template <int FMT, int OUT>
+const void* band_fn_t(int px) {
+    return px == 4 ? (const void*)evam_pp_band<FMT, OUT, 4>
+         : px == 2 ? (const void*)evam_pp_band<FMT, OUT, 2> : (const void*)evam_pp_band<FMT, OUT, 1>;
+}
+const void* band_fn(int f, int out, int px) {
+    switch (f * 2 + out) {
+    case kNV12 * 2 + 0: return band_fn_t<kNV12, 0>(px);
+    case kNV12 * 2 + 1: return band_fn_t<kNV12, 1>(px);
+    case kI420 * 2 + 0: return band_fn_t<kI420, 0>(px);
+    default: return band_fn_t<kI420, 1>(px);
+    }
+}
+
+// Band-kernel plan for a uniform 4:2:0 group whose consecutive output rows share source rows (vertical
+// upscales, C1). Fills the geometry, strips, bands and LDS fields of TParams (not items, LUT, output,
+// colour).
+//  * PX: the widest of 4 / 2 / 1 adjacent columns per lane that divides DW and whose strip footprint fits
+//    one DMA instruction (64 chunks) per row.
+//  * Band height TH: about EVAM_PP_STRIP_WAVES (16) waves per CU over the launch (one round), at most 64
+//    (the lane-held row table), lowered until the band's staged rows fit the LDS.
+//  * LDS per wave: the most luma rows any band reads (nrY, from the host's row table) and the chroma rows
+//    they can span at either crop-origin parity (nrY / 2 + 1).
+// Returns false for geometries it does not suit (fewer than 1 in 8 rows sharing source rows, footprints
+// over 1 KB, outputs wider than kMaxStrips strips).
+bool plan_band(int f, const Geom& g, int DW, int DH, int count, int out_dtype, int n_cu, const XTab* xt,
+               const YTab* yt, uint32_t x0_mask, const Knobs& kn, TParams& p, int& px, int& nw, int& lds) {
+    if (f != kNV12 && f != kI420) return false;
+    int shared = 0, vis = 0;
+    for (int Y = 0; Y + 1 < DH; Y++) {
+        const bool pad0 = (yt[Y].b0 | yt[Y].b1) == 0, pad1 = (yt[Y + 1].b0 | yt[Y + 1].b1) == 0;
+        if (pad0 || pad1) continue;
+        vis++;
+        shared += yt[Y + 1].r0 <= yt[Y].r1;
+    }
+    if (kn.band != 2 && shared * 8 <= vis) return false;
+    if (!x0_mask) x0_mask = 1u << (g.x0 & 31);
+    const int npc = f == kI420 ? 2 : 1;
+    int mY = 0, mC = 0;
+    px = 0;
+    for (int cand : {4, 2, 1}) {
+        if (kn.band_px > 0 && cand != kn.band_px) continue;
+        if (DW % cand) continue;
+        wave_segments(f, g.ox, g.rw, DW, xt, x0_mask, 64 * cand, mY, mC);
+        if (mY <= 64 && mC <= 64) { px = cand; break; }
+    }
+    if (!px) return false;
+    const int nstrips = (DW + 64 * px - 1) / (64 * px);
+    if (nstrips > kMaxStrips) return false;
+    p.segY = 16 * std::max(1, mY);
+    p.segC = 16 * std::max(1, mC) * npc;  // I420: the U and V rows side by side
+    const int lut_static = out_dtype == EVAM_DTYPE_F32 ? kLutBytes : 16;
+    const int per_launch = std::min(count, kArgItems);
+    const int64_t want = (int64_t)std::max(1, std::min(64, kn.strip_waves)) * n_cu;
+    int th = (int)std::max<int64_t>(2, ((int64_t)per_launch * nstrips * DH + want - 1) / want);
+    if (kn.strip_th > 0) th = kn.strip_th;
+    th = std::max(1, std::min(std::min(DH, 64), th));
+    for (;; th--) {
+        int nrY = 1;
+        for (int Y0 = 0; Y0 < DH; Y0 += th) {
+            int lo = -1, hi = -1;
+            for (int Y = Y0; Y < std::min(DH, Y0 + th); Y++) {
+                if ((yt[Y].b0 | yt[Y].b1) == 0) continue;  // letterbox row
+                if (lo < 0) lo = yt[Y].r0;
+                hi = yt[Y].r1;
+            }
+            if (lo >= 0) nrY = std::max(nrY, hi - lo + 1);
+        }
+        p.nrY = nrY;
+        p.wave_bytes = nrY * p.segY + (nrY / 2 + 1) * p.segC;
+        nw = 4;
+        lds = nw * p.wave_bytes + 16;  // + 16: a right-edge tap reads past its footprint (weight 0)
+        if (lds + lut_static <= 64 * 1024) break;
+        if (th == 1) return false;
+    }
+    p.TH = th;
+    p.nstrips = nstrips;
+    p.tiles_per_item = nstrips * ((DH + th - 1) / th);  // wave units per item
+    p.DW = DW; p.DH = DH;
+    p.cw = g.cw; p.ch = g.ch; p.rw = g.rw; p.rh = g.rh; p.ox = g.ox; p.oy = g.oy;
+    p.scale_x = 1. / ((double)g.rw / g.cw);
+    p.scale_y = 1. / ((double)g.rh / g.ch);
+    p.nw = nw;
+    p.tiles_x = nstrips;
+    p.xcd_remap = 0;
+    const int sw = 64 * px;
+    for (int s = 0; s < kMaxStrips; s++) {
+        const int Xv0 = std::max(s * sw, g.ox), Xv1 = std::min(std::min(s * sw + sw, DW), g.ox + g.rw) - 1;
+        p.sfoot[s] = s < nstrips && Xv0 <= Xv1 ? int2{xt[Xv0].s0, xt[Xv1].s1} : int2{-1, -1};
+    }
+    return (int64_t)per_launch * p.tiles_per_item <= 0x7FFFFFFF;
+}
+
+template <int FMT, int OUT>
+hipError_t launch_band_t(int px, const TParams& p, int grid, int nw, int lds, hipStream_t s) {
+    const dim3 blk(64 * nw);
+    if (px == 4) hipLaunchKernelGGL((evam_pp_band<FMT, OUT, 4>), dim3(grid), blk, lds, s, p);
+    else if (px == 2) hipLaunchKernelGGL((evam_pp_band<FMT, OUT, 2>), dim3(grid), blk, lds, s, p);
+    else hipLaunchKernelGGL((evam_pp_band<FMT, OUT, 1>), dim3(grid), blk, lds, s, p);
+    return hipGetLastError();
+}
+hipError_t launch_band(int f, int out, int px, const TParams& p, int grid, int nw, int lds, hipStream_t s) {
+    switch (f * 2 + out) {
+    case kNV12 * 2 + 0: return launch_band_t<kNV12, 0>(px, p, grid, nw, lds, s);
+    case kNV12 * 2 + 1: return launch_band_t<kNV12, 1>(px, p, grid, nw, lds, s);
+    case kI420 * 2 + 0: return launch_band_t<kI420, 0>(px, p, grid, nw, lds, s);
+    default: return launch_band_t<kI420, 1>(px, p, grid, nw, lds, s);
     }
 }
 
@@ -3583,6 +4029,30 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
                         launches++;
                     }
                     (void)grid;
+                    continue;
+                }
+            }
+            if (kn.band && kn.wave != 2 && kn.strip != 2) {
+                TParams* tp = &h->sc_tparams;
+                int bpx = 0, nw = 0, lds = 0;
+                const XTab* hx = reinterpret_cast<const XTab*>(h->h_block.data() + tab_off[f]);
+                if (plan_band(f, g0, DW, DH, count[f], cfg->out_dtype, h->n_cu, hx, reinterpret_cast<const YTab*>(hx + DW),
+                              x0_mask[f], kn, *tp, bpx, nw, lds)) {
+                    tp->lut = lut_d;
+                    tp->dst = dst->data;
+                    tp->slot_offset = dst->slot_offset;
+                    tp->slot_stride = dst->slot_stride;
+                    tp->color_rgb = color_rgb;
+                    tp->fill = fill;
+                    for (int m0 = mfirst[f]; m0 < mfirst[f + 1]; m0 += kArgItems) {
+                        const int nm = std::min(kArgItems, mfirst[f + 1] - m0);
+                        fill_args(tp->items, m0, nm);
+                        tp->units = nm * tp->tiles_per_item;
+                        const int gr = (tp->units + nw - 1) / nw;
+                        hipError_t e = launch_band(f, cfg->out_dtype, bpx, *tp, gr, nw, lds, h->stream);
+                        if (e != hipSuccess) return fail(EVAM_PP_ERR_HIP, "kernel launch failed: %s", hipGetErrorString(e));
+                        launches++;
+                    }
                     continue;
                 }
             }

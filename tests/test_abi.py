@@ -98,3 +98,19 @@ def test_transform_inverse(evam):
                        pad_x=0, pad_y=140, resized_w=640, resized_h=360)
     x, y = t.tensor_to_source(320, 320)
     assert abs(x - 1920) < 1e-6 and abs(y - 1080) < 1e-6
+
+
+def test_variant_library_override_is_confined(evam, monkeypatch, tmp_path):
+    """EVAM_PP_LIB (A/B runs) loads only a tools/build_variant.sh build from <repo>/ab/; a stray setting
+    pointing anywhere else is refused instead of silently replacing the product library."""
+    from importlib import import_module
+
+    native = import_module(evam.__name__ + "._native")
+    stray = tmp_path / "libevam_pp_x.so"
+    stray.write_bytes(b"")
+    monkeypatch.setattr(native, "_LIB", None)
+    monkeypatch.setenv("EVAM_PP_LIB", str(stray))
+    with pytest.raises(RuntimeError, match="only variant builds"):
+        native.load_library()
+    monkeypatch.delenv("EVAM_PP_LIB")
+    assert native.load_library() is not None

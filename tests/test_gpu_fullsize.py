@@ -33,9 +33,15 @@ def oracle_items(O, coracle, frames, items, out_shape, dtype, info, slot=lambda 
     return ref
 
 
-def test_c1_bench_batch(evam, O, coracle, gpu):
-    """C1: 32 x 768x432 NV12 -> 32x3x512x512 u8 (the wave kernel's REUSE path), bench frames."""
+@pytest.mark.parametrize("shape", ["default", "band_px2", "band_th16", "wave"])
+def test_c1_bench_batch(evam, O, coracle, gpu, shape, monkeypatch):
+    """C1: 32 x 768x432 NV12 -> 32x3x512x512 u8, bench frames: the band kernel (default; 2 pixels per lane;
+    16-row bands) and the wave kernel's REUSE path (EVAM_PP_WAVE=2)."""
     import torch
+
+    for k, v in {"default": {}, "band_px2": {"EVAM_PP_BAND_PX": "2"}, "band_th16": {"EVAM_PP_STRIP_TH": "16"},
+                 "wave": {"EVAM_PP_WAVE": "2"}}[shape].items():
+        monkeypatch.setenv(k, v)
 
     wl = bench.WORKLOADS["c1"]
     imgs = bench.device_frames(evam, torch, wl, 32, gpu, seed=1234)

@@ -364,13 +364,14 @@ def test_stats_and_timing(evam, O, gpu):
 @pytest.mark.parametrize("variant", ["auto", "wave", "px1", "px2", "noreuse", "staged", "staged_xcd", "staged_r1",
                                      "staged_wide", "staged_b3", "staged_slot2k", "strip", "strip_d1", "strip_d2", "strip_d3",
                                      "strip_th5", "strip_nw8", "strip_xcd", "strip_px1", "strip_px2",
-                                     "strip_px2_d4_th7"])
+                                     "strip_px2_d4_th7", "band", "band_px1", "band_px2", "band_th5", "band_th64"])
 def test_wave_kernel_variants(evam, O, coracle, gpu, fmt, src, dst, resize, variant, monkeypatch):
     """Uniform-geometry batches through the default kernel choice, the wave-row kernel forced
     (EVAM_PP_WAVE=2; every PX / REUSE choice), the staged kernel (EVAM_PP_WAVE=0 EVAM_PP_STRIP=0; with the
     XCD-contiguous tile order forced on small, non-multiple-of-8 grids: EVAM_PP_XCD=1) and the strip kernel
     (EVAM_PP_STRIP=2: forced even where output rows share source rows; every ring depth, an odd tile height,
-    8 waves per workgroup, XCD order, 1 and 2 pixels per lane), RGB order, fp32 with normalisation and u8."""
+    8 waves per workgroup, XCD order, 1 and 2 pixels per lane) and the band kernel (EVAM_PP_BAND=2: forced
+    on downscales too, every PX, short and 64-row bands), RGB order, fp32 with normalisation and u8."""
     import torch
 
     env = {"wave": {"EVAM_PP_WAVE": "2"}, "px1": {"EVAM_PP_WAVE": "2", "EVAM_PP_PX": "1"},
@@ -389,8 +390,12 @@ def test_wave_kernel_variants(evam, O, coracle, gpu, fmt, src, dst, resize, vari
            "strip_px1": {"EVAM_PP_STRIP": "2", "EVAM_PP_STRIP_PX": "1"},
            "strip_px2": {"EVAM_PP_STRIP": "2", "EVAM_PP_STRIP_PX": "2"},
            "strip_px2_d4_th7": {"EVAM_PP_STRIP": "2", "EVAM_PP_STRIP_PX": "2", "EVAM_PP_STRIP_D": "4",
-                                "EVAM_PP_STRIP_TH": "7"}}.get(variant, {})
-    if variant.startswith("staged"):
+                                "EVAM_PP_STRIP_TH": "7"},
+           "band": {"EVAM_PP_BAND": "2"}, "band_px1": {"EVAM_PP_BAND": "2", "EVAM_PP_BAND_PX": "1"},
+           "band_px2": {"EVAM_PP_BAND": "2", "EVAM_PP_BAND_PX": "2"},
+           "band_th5": {"EVAM_PP_BAND": "2", "EVAM_PP_STRIP_TH": "5"},
+           "band_th64": {"EVAM_PP_BAND": "2", "EVAM_PP_STRIP_TH": "64"}}.get(variant, {})
+    if variant.startswith(("staged", "band")):
         env["EVAM_PP_STRIP"] = "0"
     for k, v in env.items():
         monkeypatch.setenv(k, v)

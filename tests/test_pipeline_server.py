@@ -375,6 +375,65 @@ def test_hub_batches_across_pipelines(ps, evam, model_dir, gpu, O):
     ps.PipelineServer.stop()
 
 
+@pytest.mark.gpu
+def test_streams_partitioned_over_devices(ps, evam, model_dir, gpu, O):
+    """Option ``devices``: pipeline k runs on devices[(k - 1) mod G] (the reference starts one
+    pipeline per source, evas/manager.py:129-141). Two logical devices on the one GPU of the box: pipelines
+    1, 3 batch through hub 0 and 2, 4 through hub 1, each hub with its own pre-processing handle and stream,
+    and every classifier input row is bit-exact with the oracle (so with a one-device run)."""
+    import torch
+
+    cls_inputs = []
+
+    def detector(t):
+        n = t.shape[0]
+        out = torch.full((n, 3, 7), -1.0)
+        out[:, 0] = torch.tensor([0, 1, 0.9, 0.25, 0.25, 0.5, 0.75])     # car
+        return out
+
+    def classifier(t):
+        cls_inputs.append(t.detach().cpu().numpy().copy())
+        m = t.mean(dim=(1, 2, 3))
+        return {"color": torch.stack([1 - m, m], 1)}
+
+    ps.PipelineServer.start({"pipeline_dir": PIPES, "model_dir": model_dir, "devices": [0, 0], "batch_target": 2,
+                             "batch_wait_ms": 20000})
+    assert ps.PipelineServer.devices() == [0, 0]
+    ps.PipelineServer.register_model("det_alias/det_ver", ps.InferenceModel(detector, (64, 64), name="det"))
+    ps.PipelineServer.register_model("cls_alias/cls_ver", ps.InferenceModel(classifier, (24, 24), name="cls"))
+    rng = np.random.default_rng(29)
+    frames = [O.random_frame(rng, O.NV12, 320, 180) for _ in range(4)]
+    pipes = []
+    for f in frames:
+        qin = queue.Queue()
+        qin.put({"fourcc": f.fourcc, "width": f.width, "height": f.height, "planes": f.planes})
+        qin.put(None)
+        p = ps.PipelineServer.pipeline("detect_classify", "hip")
+        p.start(source={"type": "application", "input": qin},
+                destination={"metadata": {"type": "application", "output": queue.Queue(), "mode": "json"}})
+        pipes.append(p)
+    assert [p.slot for p in pipes] == [0, 1, 0, 1] and [p.device for p in pipes] == [0, 0, 0, 0]
+    for p in pipes:
+        st = p.wait(120)
+        assert st["state"] == "COMPLETED", st
+    h0, h1 = ps.PipelineServer.hub(0), ps.PipelineServer.hub(1)
+    assert h0 is not h1
+    # each hub served its two streams: one 2-frame detection launch and one 2-ROI classification launch
+    assert sorted(b[1:] for b in h0.batches) == [(2, 2), (2, 2)]
+    assert sorted(b[1:] for b in h1.batches) == [(2, 2), (2, 2)]
+    info = ps.InferenceModel(None, (24, 24), json.load(open(os.path.join(
+        model_dir, "cls_alias", "cls_ver", "cls_alias-cls_ver.json")))).preproc_info()
+    c = O.COracle()
+    ref = np.zeros((4, 3, 24, 24), np.float32)
+    for i, f in enumerate(frames):
+        c.preprocess_item(f, (80, 45, 80, 90), ref, i, color_rgb=True, lut=O.np_norm_lut(1, info.range))
+    rows = [r for t in cls_inputs for r in t]
+    assert len(rows) == 4
+    matched = sorted(next(j for j in range(4) if np.array_equal(r, ref[j])) for r in rows)
+    assert matched == [0, 1, 2, 3]
+    ps.PipelineServer.stop()
+
+
 @pytest.mark.parametrize("per_call", [1, 7, 4])
 def test_classify_reclassify_interval(ps, evam, per_call):
     """gvaclassify reclassify-interval (pipelines/object_classification/vehicle_attributes/pipeline.json:68-71):

@@ -1,8 +1,9 @@
 #!/bin/bash
-# Round-3 GPU session: the GPU parity suite, then bench lines of the strip kernel (default) against the
-# staged kernel (EVAM_PP_STRIP=0) on C2 / C4 / C5, then a rocprofv3 kernel-trace summary of C2.
+# Round-3 GPU session: the GPU parity suite, then bench lines of the default build on C2 / C4 / C5 and of
+# each A/B setting given (env assignments, e.g. EVAM_PP_STRIP=0 or EVAM_PP_LIB=ab/libevam_pp_X.so),
+# then a rocprofv3 kernel-trace summary of C2.
 # Every GPU step has its own time limit; the first failure ends the script.
-#   tools/gpu_r03.sh TAG [tests|notests] ["env settings for extra C2 A/B lines", ...]
+#   tools/gpu_r03.sh TAG [tests|notests] ["env settings of an A/B arm", ...]
 set -euo pipefail
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 OUT="$ROOT/gpurun_out"
@@ -34,14 +35,16 @@ print(f"{sys.argv[2]:>18}: {b['value']:>12.1f} f/s  step {b['ms_per_step']*1e3:7
 EOF
 }
 line c2_strip -- --steps 300 --warmup 50
-line c2_staged EVAM_PP_STRIP=0 -- --steps 300 --warmup 50
-for e in "$@"; do
-  line "c2_$(echo "$e" | tr ' =' '_-')" $e -- --steps 300 --warmup 50
-done
 line c4_strip -- --config c4 --steps 150 --warmup 30
-line c4_staged EVAM_PP_STRIP=0 -- --config c4 --steps 150 --warmup 30
 line c5_strip -- --config c5 --steps 300 --warmup 50
-line c5_staged EVAM_PP_STRIP=0 -- --config c5 --steps 300 --warmup 50
+line c1 -- --config c1 --steps 300 --warmup 50
+for e in "$@"; do
+  tag="$(echo "$e" | sed 's/[ =\/]/_/g')"
+  line "c2_$tag" $e -- --steps 300 --warmup 50
+  line "c4_$tag" $e -- --config c4 --steps 150 --warmup 30
+  line "c5_$tag" $e -- --config c5 --steps 300 --warmup 50
+  line "c1_$tag" $e -- --config c1 --steps 300 --warmup 50
+done
 echo "[r03] rocprofv3 C2"; date
 export TMPDIR=/tmp
 cd /tmp
