@@ -2274,7 +2274,7 @@ struct QParams {
 // 100 MHz constant clock at entry / after the record and geometry / after the setup / at the end,
 // written by lane 0 with a vector store. Product builds compile no stamp.
 #ifdef EVAM_PP_TRACE
-constexpr int kTraceWGs = 16384, kTraceSlots = 8;
+constexpr int kTraceWGs = 16384, kTraceSlots = 12;
 __device__ unsigned long long g_evam_trace[kTraceWGs * kTraceSlots];
 #define EVAM_STAMP(k)                                                                                  \
     do {                                                                                               \
@@ -2448,6 +2448,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(96))) void
     const uint32_t mY = nY > 1 ? (uint32_t)((0x100000000ull + nY - 1) / nY) : 0u;
     const uint32_t mC = nC > 1 ? (uint32_t)((0x100000000ull + nC - 1) / nC) : 0u;
     __syncthreads();  // row table (and on the first unit the LUT) visible
+    EVAM_STAMP(8);
     // One plane region of group grp: chunk q -> (segment, chunk) -> (row, tap) -> source offset.
     // Returns the number of DMA instructions this wave issued (wave-uniform: an instruction with no active
     // lane is skipped), for the counted waits of the three-buffer pipeline.
@@ -2504,6 +2505,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(96))) void
         xt[X] = e;
     }
     __syncthreads();  // column table visible to the per-lane setup
+    EVAM_STAMP(9);
     // fill in source channel order (P.fill is in output plane order); fp32: LUT byte offsets
     const uint32_t fsh = OUT == 1 ? 2 : 0;
     const uint32_t fq0 = P.fill & 0xFF, fq1 = (P.fill >> 8) & 0xFF, fq2 = (P.fill >> 16) & 0xFF;
@@ -2657,6 +2659,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(96))) void
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();  // every wave's DMA for grp landed; every wave done reading grp-1
+        if (grp == 0) EVAM_STAMP(10);
         if (grp + 1 < ngroups) issue(grp + 1, (grp & 1) ? buf0 : buf1);
         asm volatile("" ::: "memory");  // the next group's DMA stays ahead of this group's stores
         compute(grp, (grp & 1) ? buf1 : buf0);

@@ -54,15 +54,16 @@ def main():
         pp.convert(sets[t % 5], outs[t % 5], info, rois=rois[t % len(rois)])
     torch.cuda.synchronize()
     cap = 4096
-    buf = (ctypes.c_ulonglong * (8 * cap))()
+    buf = (ctypes.c_ulonglong * (12 * cap))()
     rc = lib.evam_pp_debug_trace(ctypes.cast(buf, ctypes.c_void_p), cap)
     if rc:
         raise SystemExit(f"evam_pp_debug_trace: {rc}")
-    tr = np.frombuffer(buf, dtype=np.uint64).reshape(cap, 8)
+    tr = np.frombuffer(buf, dtype=np.uint64).reshape(cap, 12)
     tr = tr[tr[:, 3] != 0]  # the traced launch's workgroups
     nwg = len(tr)
-    t = tr[:, :4].astype(np.int64)
-    t = (t - t[:, 0].min()) * 10 / 1000.0  # us from the first workgroup's entry
+    t0 = tr[:, 0].astype(np.int64).min()
+    t = (tr[:, :4].astype(np.int64) - t0) * 10 / 1000.0  # us from the first workgroup's entry
+    s8, s9, s10 = ((tr[:, k].astype(np.int64) - t0) * 10 / 1000.0 for k in (8, 9, 10))
     cw, ch = (tr[:, 4] & 0xFFFFFFFF).astype(int), (tr[:, 4] >> 32).astype(int)
     ng, R = (tr[:, 5] & 0xFFFFFFFF).astype(int), (tr[:, 5] >> 32).astype(int)
     xcc = (tr[:, 6] & 0xFFFFFFFF).astype(int)
@@ -80,7 +81,9 @@ def main():
         "config": a.config, "workgroups": int(nwg),
         "phase_us_p0_p10_p50_p90_p100": {
             "entry": dist(t[:, 0]), "record+geometry": dist(t[:, 1] - t[:, 0]),
-            "setup": dist(t[:, 2] - t[:, 1]), "loop": dist(loop), "end": dist(end)},
+            "setup": dist(t[:, 2] - t[:, 1]), "loop": dist(loop), "end": dist(end),
+            "setup: row table + LUT barrier": dist(s8 - t[:, 1]), "setup: column table barrier": dist(s9 - s8),
+            "setup: per-lane state": dist(t[:, 2] - s9), "loop: group 0 DMA wait + barrier": dist(s10 - t[:, 2])},
         "groups_per_roi": dist(ng), "rows_per_group": dist(R), "us_per_group": dist(per_group),
         "last_10_to_finish": [{"end": round(float(end[i]), 2), "cw": int(cw[i]), "ch": int(ch[i]),
                                "groups": int(ng[i]), "R": int(R[i]), "nY": int(nY[i]),
