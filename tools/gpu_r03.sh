@@ -38,12 +38,14 @@ line c2_strip -- --steps 300 --warmup 50
 line c4_strip -- --config c4 --steps 150 --warmup 30
 line c5_strip -- --config c5 --steps 300 --warmup 50
 line c1 -- --config c1 --steps 300 --warmup 50
+line c3 -- --config c3 --steps 300 --warmup 50
 for e in "$@"; do
   tag="$(echo "$e" | sed 's/[ =\/]/_/g')"
   line "c2_$tag" $e -- --steps 300 --warmup 50
   line "c4_$tag" $e -- --config c4 --steps 150 --warmup 30
   line "c5_$tag" $e -- --config c5 --steps 300 --warmup 50
   line "c1_$tag" $e -- --config c1 --steps 300 --warmup 50
+  line "c3_$tag" $e -- --config c3 --steps 300 --warmup 50
 done
 echo "[r03] rocprofv3 C2"; date
 export TMPDIR=/tmp
