@@ -68,26 +68,6 @@ constexpr int kAblate = EVAM_PP_ABLATE;
 #ifndef EVAM_PP_LOAD_AUX
 #define EVAM_PP_LOAD_AUX 0
 #endif
-// Strip-kernel build variants (A/B builds; defaults are the measured best):
-//  * EVAM_PP_STRIP_EARLY 1: a ring entry's next DMA goes out as soon as the row's taps are in registers
-//    (before the row's arithmetic and stores) instead of after the row's stores. Same box: C2 42.2 vs
-//    42.0 us, C4 113.3 vs 110.7 us, C5 equal (profiles/r03i_bench_lines.txt): off.
-//  * EVAM_PP_STRIP_ADJ 1: lane l holds the PX adjacent columns PX l .. (one PX-wide store per channel and
-//    row) instead of columns l, l + 64 (PX dword stores of 256 contiguous bytes).
-//  * EVAM_PP_STRIP_PRIO 1: waves of odd workgroups run at s_setprio 1 (a static stagger of the otherwise
-//    lockstep waves of one SIMD, MI355X_MICROARCH.md "Two waves per SIMD" items 4 and 9).
-#ifndef EVAM_PP_STRIP_EARLY
-#define EVAM_PP_STRIP_EARLY 0
-#endif
-#ifndef EVAM_PP_STRIP_ADJ
-#define EVAM_PP_STRIP_ADJ 0
-#endif
-#ifndef EVAM_PP_STRIP_PRIO
-#define EVAM_PP_STRIP_PRIO 0
-#endif
-constexpr bool kStripEarly = EVAM_PP_STRIP_EARLY != 0;
-constexpr bool kStripAdj = EVAM_PP_STRIP_ADJ != 0;
-constexpr bool kStripPrio = EVAM_PP_STRIP_PRIO != 0;
 
 // OpenCV color_yuv.simd.hpp ITUR_BT_601_*; the -128 chroma bias is folded into the constants.
 constexpr int kCY = 1220542, kCUB = 2116026, kCUG = -409993, kCVG = -852492, kCVR = 1673527;
@@ -1648,15 +1628,7 @@ struct TParams {
     int nstrips, units;          // strips per row; waves of work in the launch
     int segY, segC;              // bytes of one staged luma / chroma row (multiples of 16)
     int nrY;                     // most luma rows of one band (the chroma rows follow at nrY * segY)
-    // queue strip kernel only: units (item, band of TH rows) of each strip, drawn by its waves
-    unsigned* qcnt;              // this launch's counters: strip s, range r at qcnt[(s * 8 + r) * kQStride]
-    unsigned* qzero;             // a later launch's counter slot, zeroed by this launch (kQSlotWords words)
-    int qunits;                  // units per strip (items x bands)
-    int qks;                     // static units per wave: wave (x, y) takes units y, y + WY, ... (< qks of them)
 };
-constexpr int kQStride = 16;                          // one counter per 64 bytes
-constexpr int kQSlotWords = kMaxStrips * 8 * kQStride;  // one launch's counters
-constexpr int kQSlots = 64, kQAhead = 32;             // counter slots per handle; zeroed this many launches ahead
 
 // Row-strip kernel for uniform-geometry 4:2:0 batches whose output rows do not share source rows
 // (downscales: C2, C4, C5). Every wave owns one strip of 64 x PX output columns of a tile (lane l holds
@@ -1695,7 +1667,6 @@ __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
     asm volatile("" ::"s"(p_nw), "s"(p_tpi), "s"(p_tx), "s"(p_TH), "s"(p_DH), "s"(p_DW), "s"(p_grid), "s"(P.xcd_remap),
                  "s"(P.ox), "s"(P.rw), "s"(P.oy), "s"(P.rh), "s"(P.wave_bytes));
     const int t = P.xcd_remap ? xcd_tile(blockIdx.x, p_grid) : (int)blockIdx.x;
-    if (kStripPrio && (blockIdx.x & 1)) __builtin_amdgcn_s_setprio(1);
     const int item = t / p_tpi;
     const int tile = t - item * p_tpi;
     const int ty = tile / p_tx;
@@ -1790,7 +1761,7 @@ __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
     const size_t esz = OUT == 1 ? 4 : 1;
 #pragma unroll
     for (int j = 0; j < PX; j++) {
-        const int X = kStripAdj ? X0 + PX * lane + j : X0 + lane + 64 * j;
+        const int X = X0 + lane + 64 * j;
         xin[j] = live && X < p_DW;
         vo[j] = (uint32_t)(xin[j] ? X : 0) * (uint32_t)esz;
         lY[j] = lC0[j] = lC1[j] = wp[j] = 0;
@@ -1815,9 +1786,8 @@ __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
     }
     // some visible lane shows letterbox columns (wave-uniform): only then the per-pixel fill select
     const bool anypad = cols && __builtin_amdgcn_ballot_w64(anyp) != 0;
-    // stores per row of this wave: 3 per pixel column group with any lane inside the output (counted waits);
-    // adjacent columns: 3 (one PX-wide store per channel)
-    const bool full = !kStripAdj && X0 + 64 * (PX - 1) < p_DW;
+    // stores per row of this wave: 3 per pixel column group with any lane inside the output (counted waits)
+    const bool full = X0 + 64 * (PX - 1) < p_DW;
 
     const size_t plane = (size_t)p_DW * p_DH;
     uint8_t* const d0 = reinterpret_cast<uint8_t*>(P.dst) + (size_t)(P.slot_offset + it.index * P.slot_stride) * 3 * plane * esz;
@@ -1895,28 +1865,9 @@ __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
             __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v2, rsO2, vo[j], so, EVAM_PP_STORE_AUX);
         }
     };
-    // a whole row of the lane's PX pixels, vv[c][j] in source channel order
-    auto put_row = [&](int Y, const uint32_t (&vv)[3][PX]) {
-        if constexpr (kStripAdj) {
-            if (!xin[0]) return;  // DW % PX == 0 (host): a lane's pixels are all in or all out
-            if (kAblate & 4) {
-                asm volatile("" ::"v"(vv[0][0]), "v"(vv[1][0]), "v"(vv[2][0]));
-                return;
-            }
-            const uint32_t off = vo[0] + (uint32_t)(Y * p_DW) * (uint32_t)esz;  // soffset 0: wide-store hazard
-            store_off<OUT, PX>(rsO0, off, lutb, vv[0]);
-            store_off<OUT, PX>(rsO1, off, lutb + 1024, vv[1]);
-            store_off<OUT, PX>(rsO2, off, lutb + 2048, vv[2]);
-        } else {
-#pragma unroll
-            for (int j = 0; j < PX; j++) put(Y, j, vv[0][j], vv[1][j], vv[2][j]);
-        }
-    };
     auto put_fill = [&](int Y) {
-        uint32_t vv[3][PX];
 #pragma unroll
-        for (int j = 0; j < PX; j++) { vv[0][j] = fill0; vv[1][j] = fill1; vv[2][j] = fill2; }
-        put_row(Y, vv);
+        for (int j = 0; j < PX; j++) put(Y, j, fill0, fill1, fill2);
     };
     // letterbox rows above the ring: before its DMA in issue order, so they never enter the counted waits
     const int ra = n ? vr0 : Y1;
@@ -1927,9 +1878,8 @@ __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
     auto row = [&](int i, int kk, auto has_pad) {
         constexpr bool PADC = decltype(has_pad)::value;
         // row i's DMA landed. Issued after it: the DMA of rows i+1 .. i+D-1 (>= NMIN each) and the stores
-        // of rows i-D+1 .. i-1 (nst each); with the early issue (row j's successor DMA goes out before row
-        // j's stores) also the stores of row i-D.
-        constexpr int SD = kStripEarly ? D : D - 1;
+        // of rows i-D+1 .. i-1 (nst each)
+        constexpr int SD = D - 1;
         if (SD == 0) {  // nothing was issued after row i's DMA
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         } else if (i >= SD && i + D - 1 < n) {
@@ -1946,7 +1896,6 @@ __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
         const int ya = __builtin_amdgcn_readlane(lr0, i), yb = __builtin_amdgcn_readlane(lr1, i);
         const bool share = ((y0 + ya) >> 1) == ((y0 + yb) >> 1);
         if (kAblate & 2) {  // diagnostics: no pixel math (no tap reads)
-            if (kStripEarly && i + D < n) issue(i + D, kk);
             put_fill(Y);
         } else {
             const int eo = kk * GRP;  // this entry's offset from entry 0
@@ -1971,13 +1920,6 @@ __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
                     raw_c(aC1[j], eo + SC, rE[j][1]);
                 }
             }
-            if constexpr (kStripEarly) {
-                // the entry's bytes are in registers: its next row's DMA overlaps this row's arithmetic
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                if (i + D < n) issue(i + D, kk);
-                asm volatile("" ::: "memory");
-            }
-            uint32_t vv[3][PX];
 #pragma unroll
             for (int j = 0; j < PX; j++) {
                 const UVs tA = uvt(rC[j][0][0], rC[j][0][1]), tB = uvt(rC[j][1][0], rC[j][1][1]);
@@ -2009,16 +1951,11 @@ __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
                     v[1] = padc[j] ? fill1 : v[1];
                     v[2] = padc[j] ? fill2 : v[2];
                 }
-                if constexpr (kStripAdj) {
-                    vv[0][j] = v[0]; vv[1][j] = v[1]; vv[2][j] = v[2];
-                } else {
-                    put(Y, j, v[0], v[1], v[2]);
-                }
+                put(Y, j, v[0], v[1], v[2]);
             }
-            if constexpr (kStripAdj) put_row(Y, vv);
         }
         asm volatile("" ::: "memory");  // issue order is what the counted waits assume
-        if (!kStripEarly && i + D < n) issue(i + D, kk);  // this entry's reads are done: the stores consumed them
+        if (i + D < n) issue(i + D, kk);  // this entry's reads are done: the stores consumed them
         asm volatile("" ::: "memory");
     };
     auto ring = [&](auto has_pad) {
@@ -2041,328 +1978,6 @@ __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
         EVAM_WTRACE_VAL(6, (unsigned long long)xcc);
     }
 #endif
-}
-
-// Queue strip kernel: the strip kernel's per-row work (ring of D row entries fed by LDS-DMA, counted
-// waits, the same per-pixel arithmetic) with the tail of the rows handed out dynamically. A wave keeps one
-// strip of 64 x PX columns for the whole launch and walks a sequence of units (item, band of TH rows) of that
-// strip: first its static units (wy, wy + WY, ...: about EVAM_PP_STRIPQ_STATIC % of the rows), then
-// dynamic ones from a per-(strip, range) counter, one relaxed device-scope atomic per unit, issued one unit
-// ahead. A static one-wave-per-tile grid ends with a long tail: on C2 the waves' end times spread over
-// 23-40 us, because waves share a SIMD's issue unequally (profiles/r03l_wave_timeline_c2.json); the
-// dynamic tail lets the fast waves take the slow ones' last rows. The atomics come only from waves that
-// finished their static rows, so they are spread over the tail (drawing every unit dynamically put 4,096
-// atomics on 32 counters at once and made every row wait behind them: profiles/r03m_bench_lines.txt).
-// The ring runs on across units: the last D rows of a unit issue the DMA of the next unit's first rows, and
-// the next unit's state (item, planes, footprint, row table) is loaded when the current one starts. Waits
-// count every VMEM operation the wave issued since the row's DMA (marks in SGPRs), so they stay exact however
-// units, rows and atomics interleave. Groups without letterbox rows or columns only.
-template <int FMT, int OUT, int D, int PX>
-__global__ __launch_bounds__(512) void evam_pp_stripq(const TParams P) {
-#if defined(__HIP_DEVICE_COMPILE__)  // the host pass rejects this body (its launch stub needs only the signature)
-    __shared__ __attribute__((aligned(16))) float lut_s[OUT == 1 ? 768 : 4];
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    static_assert(FMT == kNV12 || FMT == kI420, "4:2:0 sources");
-    static_assert(D >= 1 && D <= 2, "ring depth");
-    static_assert(PX == 1 || PX == 2, "pixels per lane");
-    constexpr int NPC = FMT == kI420 ? 2 : 1;
-    constexpr int NMIN = 2 + NPC;
-    constexpr int SY = strip_slot(PX), SC = strip_slot(PX), GRP = 2 * SY + 2 * NPC * SC;
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    EVAM_WSTAMP(0);
-    const int p_nw = P.nw, p_bands = P.tiles_per_item, p_TH = P.TH, p_DH = P.DH, p_DW = P.DW, p_U = P.qunits;
-    const int p_ks = P.qks;
-    asm volatile("" ::"s"(p_nw), "s"(p_bands), "s"(p_TH), "s"(p_DH), "s"(p_DW), "s"(p_U), "s"(p_ks), "s"(P.oy),
-                 "s"(P.ch), "s"(P.wave_bytes), "s"(P.qcnt), "s"(P.qzero), "s"(P.dst), "s"(P.slot_offset),
-                 "s"(P.slot_stride), "s"(P.ox), "s"(P.cw));
-    const int strip = (int)blockIdx.x * p_nw + wave;
-    const int X0 = strip * 64 * PX;
-    const bool live = X0 < p_DW;
-    const int2 sf = P.sfoot[min(strip, kMaxStrips - 1)];
-    const int WY = (int)gridDim.y, wy = (int)blockIdx.y;
-    // dynamic units of this strip: [KS WY, U) split into NP ranges with a counter each (spreads the atomics),
-    // range wy mod NP: every range has workgroups of every strip column whatever the placement
-    const int S = p_ks * WY;
-    const int NP = min(8, WY);
-    const int part = wy % NP;
-    const int dyn = max(p_U - S, 0);
-    const int q_lo = S + (int)((int64_t)dyn * part / NP), q_hi = S + (int)((int64_t)dyn * (part + 1) / NP);
-    unsigned* const cnt = P.qcnt + ((size_t)min(strip, kMaxStrips - 1) * 8 + part) * kQStride;
-    // zero a later launch's counters (one workgroup)
-    if (P.qzero && blockIdx.x == 0 && wy == 0)
-        for (int k = threadIdx.x; k < kQSlotWords; k += blockDim.x)
-            __hip_atomic_store(P.qzero + k, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-
-    int ops = 0;  // VMEM operations this wave issued since here (counted waits)
-    // the LUT by LDS-DMA ahead of everything (no VGPR waits on it): 192 chunks over the workgroup's waves
-    if constexpr (OUT == 1) {
-        const __amdgpu_buffer_rsrc_t rsL = __builtin_amdgcn_make_buffer_rsrc((void*)P.lut, (short)0, 3072, 0x00020000);
-        for (int c0 = wave * 64; c0 < 192; c0 += p_nw * 64) {
-            const int c = c0 + lane, sec = c >> 6;
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsL, (__attribute__((address_space(3))) void*)((uint8_t*)lut_s + c0 * 16), 16,
-                                                     (uint32_t)(((P.color_rgb ? 2 - sec : sec) * 64 + (c & 63)) * 16), 0, 0, 0);
-            ops++;
-        }
-    }
-    const int ops_lut = ops;
-    const size_t esz = OUT == 1 ? 4 : 1;
-    const size_t plane = (size_t)p_DW * p_DH;
-
-    // a unit: item, its band of rows, planes, footprint, output base, the band's row table (one row per lane)
-    struct Unit {
-        int u, n, Y0, y0, x0, fsY, nY, fsC, nC, pitch0, pitch1, pitch2;
-        const uint8_t *p0, *p1, *p2;
-        uint8_t* d0;
-        int lr0, lr1, lb0, lb1;  // lanes
-    };
-    auto load_unit = [&](Unit& U, int u) {
-        U.u = u;
-        U.n = 0;
-        if (u < 0 || u >= p_U || !live) return;
-        const int item = u / p_bands, band = u - item * p_bands;
-        U.Y0 = band * p_TH;
-        U.n = min(p_TH, p_DH - U.Y0);
-        const ItemArg& it = P.items[item];
-        U.p0 = it.plane[0]; U.p1 = it.plane[1]; U.p2 = it.plane[2];
-        U.pitch0 = it.pitch[0]; U.pitch1 = it.pitch[1]; U.pitch2 = it.pitch[2];
-        U.x0 = it.x0; U.y0 = it.y0;
-        U.d0 = reinterpret_cast<uint8_t*>(P.dst) + (size_t)(P.slot_offset + it.index * P.slot_stride) * 3 * plane * esz;
-        footprint_chunks(FMT, 1, U.x0 + sf.x, U.x0 + sf.y, U.fsY, U.nY, U.fsC, U.nC);
-        U.lr0 = U.lr1 = U.lb0 = U.lb1 = 0;
-        if (lane < U.n) {
-            int sy, b0, b1;
-            linear_coef(U.Y0 + lane - P.oy, P.scale_y, P.ch, false, sy, b0, b1);
-            U.lr0 = min(max(sy, 0), P.ch - 1);
-            U.lr1 = min(max(sy + 1, 0), P.ch - 1);
-            U.lb0 = b0 << 8;
-            U.lb1 = b1 << 8;
-        }
-    };
-    uint8_t* const wbuf = smem + wave * P.wave_bytes;
-    int mark[D];  // ops count right after each ring entry's DMA
-    // DMA of row i of unit U into ring entry k
-    auto issue = [&](const Unit& U, int i, int k) {
-        const int ya = U.y0 + __builtin_amdgcn_readlane(U.lr0, i), yb = U.y0 + __builtin_amdgcn_readlane(U.lr1, i);
-        const __amdgpu_buffer_rsrc_t rsY = __builtin_amdgcn_make_buffer_rsrc((void*)U.p0, (short)0, 0x7FFFFFFF, 0x00020000);
-        const __amdgpu_buffer_rsrc_t rsU = __builtin_amdgcn_make_buffer_rsrc((void*)U.p1, (short)0, 0x7FFFFFFF, 0x00020000);
-        const __amdgpu_buffer_rsrc_t rsV = __builtin_amdgcn_make_buffer_rsrc((void*)(NPC == 2 ? U.p2 : U.p1), (short)0, 0x7FFFFFFF, 0x00020000);
-        uint8_t* e = wbuf + k * GRP;
-        const uint32_t v = (uint32_t)lane * 16u;
-        if (lane < U.nY) {
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsY, (__attribute__((address_space(3))) void*)e, 16, v,
-                                                     ya * U.pitch0 + U.fsY, EVAM_PP_LOAD_AUX, 0);
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsY, (__attribute__((address_space(3))) void*)(e + SY), 16, v,
-                                                     yb * U.pitch0 + U.fsY, EVAM_PP_LOAD_AUX, 0);
-        }
-        const int ca = ya >> 1, cb = yb >> 1;
-        if (lane < U.nC) {
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsU, (__attribute__((address_space(3))) void*)(e + 2 * SY), 16, v,
-                                                     ca * U.pitch1 + U.fsC, EVAM_PP_LOAD_AUX, 0);
-            if constexpr (NPC == 2)
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(rsV, (__attribute__((address_space(3))) void*)(e + 2 * SY + 2 * SC),
-                                                         16, v, ca * U.pitch2 + U.fsC, EVAM_PP_LOAD_AUX, 0);
-        }
-        int cntd = NMIN;
-        if (ca != cb) {
-            if (lane < U.nC) {
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(rsU, (__attribute__((address_space(3))) void*)(e + 2 * SY + SC), 16, v,
-                                                         cb * U.pitch1 + U.fsC, EVAM_PP_LOAD_AUX, 0);
-                if constexpr (NPC == 2)
-                    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsV, (__attribute__((address_space(3))) void*)(e + 2 * SY + 3 * SC),
-                                                             16, v, cb * U.pitch2 + U.fsC, EVAM_PP_LOAD_AUX, 0);
-            }
-            cntd += NPC;
-        }
-        ops += cntd;
-        mark[k] = ops;
-    };
-    // a dynamic unit's id: relaxed device-scope atomic on this strip's counter of its range (lane 0)
-    int qres = 0, qmark = -1;
-    auto fetch = [&]() {
-        if (lane == 0) qres = (int)__hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        ops++;
-        qmark = ops;
-    };
-    auto fetched = [&]() {  // the atomic's result (waits for it and everything issued before it)
-        vmcnt_exact(ops - qmark);
-        const int r = q_lo + __builtin_amdgcn_readfirstlane(qres);
-        return r < q_hi ? r : -1;
-    };
-    // unit j of this wave's sequence: static for j < KS (its id known), else dynamic (-2: fetched on first need)
-    int jn = 0;  // index of the next unit of the sequence to set up
-    auto next_unit = [&](Unit& U) {
-        if (jn < p_ks) {
-            load_unit(U, wy + jn * WY);
-        } else {
-            U.u = -2;
-            U.n = 0;
-            fetch();
-        }
-        jn++;
-    };
-
-    Unit A, B;  // the current unit and the next one
-    A.n = 0;
-    B.u = -1; B.n = 0;
-    int ia = 0, ib = 0;  // rows of A / B issued
-    if (live) {
-        next_unit(A);
-        if (A.u == -2) load_unit(A, fetched());  // no static unit (more waves than KS x WY units)
-        for (; ia < min(A.n, D); ia++) issue(A, ia, ia);
-        if (A.n) next_unit(B);
-    }
-    EVAM_WSTAMP(1);
-
-    // per-lane column state of the strip: first tap, packed 11-bit weights, store offset (x0-independent)
-    bool xin[PX];
-    int s0c[PX];
-    uint32_t wp[PX], vo[PX];
-#pragma unroll
-    for (int j = 0; j < PX; j++) {
-        const int X = X0 + lane + 64 * j;
-        xin[j] = live && X < p_DW;
-        vo[j] = (uint32_t)(xin[j] ? X : 0) * (uint32_t)esz;
-        s0c[j] = 0; wp[j] = 0;
-        if (xin[j]) {
-            int s0, a0, a1;
-            linear_coef(X - P.ox, P.scale_x, P.cw, true, s0, a0, a1);
-            s0c[j] = s0;
-            wp[j] = (uint32_t)a0 | ((uint32_t)a1 << 16);
-        }
-    }
-    const bool full = X0 + 64 * (PX - 1) < p_DW;
-    const int nst = full ? 3 * PX : 3;
-    // per-lane tap offsets of the current unit (x0 and footprint dependent)
-    uint32_t lY[PX], lC0[PX], lC1[PX];
-    auto taps = [&](const Unit& U) {
-#pragma unroll
-        for (int j = 0; j < PX; j++) {
-            const int ca = U.x0 + s0c[j];  // tap 1 reads ca + 1: at the right edge its weight is 0
-            lY[j] = (uint32_t)(ca - U.fsY);
-            if constexpr (FMT == kNV12) {
-                lC0[j] = (uint32_t)(2 * (ca >> 1) - U.fsC);
-                lC1[j] = (uint32_t)(2 * ((ca + 1) >> 1) - U.fsC);
-            } else {
-                lC0[j] = (uint32_t)((ca >> 1) - U.fsC);
-                lC1[j] = (uint32_t)(((ca + 1) >> 1) - U.fsC);
-            }
-        }
-    };
-    if (live) taps(A);
-    if constexpr (OUT == 1) {
-        vmcnt_exact(ops - ops_lut);  // this wave's LUT pieces landed (issued before everything else)
-        __syncthreads();             // ... and every other wave's
-    }
-    EVAM_WSTAMP(2);
-    if (!live) return;
-
-    const uint8_t* lutb = reinterpret_cast<const uint8_t*>(lut_s);
-    uint32_t kb = kKBs, kg = kKGs, kr = kKRs;
-    int cvg = kCVG, cug = kCUG;
-    asm volatile("" : "+v"(kb), "+v"(kg), "+v"(kr), "+s"(cvg), "+s"(cug));
-    auto uvt = [&](uint32_t U, uint32_t V) {
-        int gu = __mul24((int)U, cug) + (int)kg;
-        asm("" : "+v"(gu));
-        return UVs{__umul24(U, (uint32_t)kCUB) + kb, (uint32_t)(__mul24((int)V, cvg) + gu), __umul24(V, (uint32_t)kCVR) + kr};
-    };
-    // the stream's next row to issue after row i of A: row i + D of A, else a row of B (a dynamic B's id is
-    // taken from its atomic on first need)
-    auto issue_next = [&](int k) {
-        if (ia < A.n) {
-            issue(A, ia++, k);
-            return;
-        }
-        if (B.u == -2) load_unit(B, fetched());
-        if (ib < B.n) issue(B, ib++, k);
-    };
-    int g = 0;  // rows of the stream computed (ring entry g % D)
-    for (;;) {
-        for (int i = 0; i < A.n; i++, g++) {
-            const int kk = D == 1 ? 0 : (g & 1);
-            // row i of A landed: everything issued after its DMA may stay in flight
-            vmcnt_exact(ops - mark[kk]);
-#ifdef EVAM_PP_TRACE
-            if (g == 0) EVAM_WSTAMP(3);
-#endif
-            const int Y = A.Y0 + i;
-            const uint32_t wb0 = (uint32_t)__builtin_amdgcn_readlane(A.lb0, i), wb1 = (uint32_t)__builtin_amdgcn_readlane(A.lb1, i);
-            const int ya = __builtin_amdgcn_readlane(A.lr0, i), yb = __builtin_amdgcn_readlane(A.lr1, i);
-            const bool share = ((A.y0 + ya) >> 1) == ((A.y0 + yb) >> 1);
-            const uint8_t* eb = wbuf + kk * GRP;
-            const __amdgpu_buffer_rsrc_t rsO0 = __builtin_amdgcn_make_buffer_rsrc((void*)(P.color_rgb ? A.d0 + 2 * plane * esz : A.d0), (short)0, 0x7FFFFFFF, 0x00020000);
-            const __amdgpu_buffer_rsrc_t rsO1 = __builtin_amdgcn_make_buffer_rsrc((void*)(A.d0 + plane * esz), (short)0, 0x7FFFFFFF, 0x00020000);
-            const __amdgpu_buffer_rsrc_t rsO2 = __builtin_amdgcn_make_buffer_rsrc((void*)(P.color_rgb ? A.d0 : A.d0 + 2 * plane * esz), (short)0, 0x7FFFFFFF, 0x00020000);
-            const int so = (int)((uint32_t)(Y * p_DW) * (uint32_t)esz);
-#pragma unroll
-            for (int j = 0; j < PX; j++) {
-                const uint8_t* ay = eb + lY[j];
-                const uint8_t* c0 = eb + 2 * SY + lC0[j];
-                const uint8_t* c1 = eb + 2 * SY + lC1[j];
-                auto chroma = [&](const uint8_t* a, int o) -> UVs {
-                    if constexpr (FMT == kNV12) return uvt(a[o], a[o + 1]);
-                    else return uvt(a[o], a[o + 2 * SC]);
-                };
-                const UVs tA = chroma(c0, 0), tB = chroma(c1, 0);
-                const uint32_t yA = luma_term(ay[0]), yB = luma_term(ay[1]);
-                const uint32_t yC = luma_term(ay[SY]), yD = luma_term(ay[SY + 1]);
-                uint32_t h0[3], h1[3];
-                h0[0] = hpass_sat(yA, tA.b, yB, tB.b, wp[j]);
-                h0[1] = hpass_sat(yA, tA.g, yB, tB.g, wp[j]);
-                h0[2] = hpass_sat(yA, tA.r, yB, tB.r, wp[j]);
-                if (share) {
-                    h1[0] = hpass_sat(yC, tA.b, yD, tB.b, wp[j]);
-                    h1[1] = hpass_sat(yC, tA.g, yD, tB.g, wp[j]);
-                    h1[2] = hpass_sat(yC, tA.r, yD, tB.r, wp[j]);
-                    asm volatile("; stripq: shared chroma row" ::"v"(h1[0]), "v"(h1[1]), "v"(h1[2]));
-                } else {
-                    const UVs tC = chroma(c0, SC), tE = chroma(c1, SC);
-                    h1[0] = hpass_sat(yC, tC.b, yD, tE.b, wp[j]);
-                    h1[1] = hpass_sat(yC, tC.g, yD, tE.g, wp[j]);
-                    h1[2] = hpass_sat(yC, tC.r, yD, tE.r, wp[j]);
-                    asm volatile("; stripq: two chroma rows" ::"v"(h1[0]), "v"(h1[1]), "v"(h1[2]));
-                }
-                uint32_t v[3];
-#pragma unroll
-                for (int c = 0; c < 3; c++) v[c] = vfinal<OUT>(h0[c], h1[c], wb0, wb1);
-                if (xin[j]) {
-                    if constexpr (OUT == 1) {
-                        __builtin_amdgcn_raw_buffer_store_b32(*reinterpret_cast<const uint32_t*>(lutb + v[0]), rsO0, vo[j], so, EVAM_PP_STORE_AUX);
-                        __builtin_amdgcn_raw_buffer_store_b32(*reinterpret_cast<const uint32_t*>(lutb + 1024 + v[1]), rsO1, vo[j], so, EVAM_PP_STORE_AUX);
-                        __builtin_amdgcn_raw_buffer_store_b32(*reinterpret_cast<const uint32_t*>(lutb + 2048 + v[2]), rsO2, vo[j], so, EVAM_PP_STORE_AUX);
-                    } else {
-                        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v[0], rsO0, vo[j], so, EVAM_PP_STORE_AUX);
-                        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v[1], rsO1, vo[j], so, EVAM_PP_STORE_AUX);
-                        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v[2], rsO2, vo[j], so, EVAM_PP_STORE_AUX);
-                    }
-                }
-            }
-            ops += nst;
-            asm volatile("" ::: "memory");  // the stores stay ahead of the next DMA (counted waits)
-            issue_next(kk);                 // this entry's reads are done: the stores consumed them
-            asm volatile("" ::: "memory");
-        }
-        // A is done: B becomes current
-        if (B.u == -2) load_unit(B, fetched());
-        if (B.n == 0) break;
-        A = B;
-        ia = ib;
-        ib = 0;
-        for (; ia < min(A.n, D); ia++) issue(A, ia, (g + ia) % D);  // top up when A had fewer rows ahead
-        next_unit(B);
-        taps(A);
-    }
-#ifdef EVAM_PP_TRACE
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    EVAM_WSTAMP(4);
-    EVAM_WTRACE_VAL(5, (unsigned long long)g << 48);
-    {
-        unsigned xcc;
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-        EVAM_WTRACE_VAL(6, (unsigned long long)xcc);
-    }
-#endif
-#endif  // __HIP_DEVICE_COMPILE__
 }
 
 // Band kernel for uniform 4:2:0 batches whose consecutive output rows share source rows (vertical
@@ -3140,10 +2755,7 @@ struct Knobs {
                                                                               // rows per tile, ring depth, waves, px
     int strip_waves = 16;                          // strip / band kernels: resident waves per CU the tiles are sized for
     int band = 1, band_px = 0;                     // band kernel: allowed (2: forced), pixels per lane
-    int stripq = 0, stripq_th = 4, stripq_static = 75;  // queue strip kernel: used (1), rows per unit, % static
     void read() {
-        stripq = env_int("EVAM_PP_STRIPQ", stripq); stripq_th = env_int("EVAM_PP_STRIPQ_TH", stripq_th);
-        stripq_static = env_int("EVAM_PP_STRIPQ_STATIC", stripq_static);
         band = env_int("EVAM_PP_BAND", band); band_px = env_int("EVAM_PP_BAND_PX", band_px);
         strip = env_int("EVAM_PP_STRIP", strip); strip_th = env_int("EVAM_PP_STRIP_TH", strip_th);
         strip_waves = env_int("EVAM_PP_STRIP_WAVES", strip_waves);
@@ -3527,7 +3139,6 @@ bool plan_strip(int f, const Geom& g, int DW, int DH, int count, int out_dtype, 
         // 128-column strips, the second 3/4 full) runs 13.0 us in four 64-column strips and 15.6 us in
         // two 128-column ones (profiles/r03g_c5_px.txt)
         if (cand == 2 && (DW + 127) / 128 < 4 && kn.strip_px != 2) continue;
-        if (kStripAdj && DW % cand) continue;  // adjacent columns: a lane's pixels all in or all out
         wave_segments(f, g.ox, g.rw, DW, xt, x0_mask, 64 * cand, mY, mC);
         const int cap = strip_slot(cand) / 16;  // chunks of one slot
         if (mY <= cap && mC <= cap) { px = cand; break; }
@@ -3573,43 +3184,6 @@ bool plan_strip(int f, const Geom& g, int DW, int DH, int count, int out_dtype, 
     if (gr > 0x7FFFFFFF) return false;
     grid = (int)gr;
     return true;
-}
-
-template <int FMT, int OUT, int PX>
-const void* stripq_fn_p(int d) {
-    return d == 2 ? (const void*)evam_pp_stripq<FMT, OUT, 2, PX> : (const void*)evam_pp_stripq<FMT, OUT, 1, PX>;
-}
-const void* stripq_fn(int f, int out, int d, int px) {
-    switch ((f * 2 + out) * 2 + (px == 2)) {
-    case (kNV12 * 2 + 0) * 2: return stripq_fn_p<kNV12, 0, 1>(d);
-    case (kNV12 * 2 + 0) * 2 + 1: return stripq_fn_p<kNV12, 0, 2>(d);
-    case (kNV12 * 2 + 1) * 2: return stripq_fn_p<kNV12, 1, 1>(d);
-    case (kNV12 * 2 + 1) * 2 + 1: return stripq_fn_p<kNV12, 1, 2>(d);
-    case (kI420 * 2 + 0) * 2: return stripq_fn_p<kI420, 0, 1>(d);
-    case (kI420 * 2 + 0) * 2 + 1: return stripq_fn_p<kI420, 0, 2>(d);
-    case (kI420 * 2 + 1) * 2: return stripq_fn_p<kI420, 1, 1>(d);
-    default: return stripq_fn_p<kI420, 1, 2>(d);
-    }
-}
-
-template <int FMT, int OUT, int PX>
-hipError_t launch_stripq_t(int d, const TParams& p, dim3 grid, int lds, hipStream_t s) {
-    const dim3 blk(64 * p.nw);
-    if (d == 2) hipLaunchKernelGGL((evam_pp_stripq<FMT, OUT, 2, PX>), grid, blk, lds, s, p);
-    else hipLaunchKernelGGL((evam_pp_stripq<FMT, OUT, 1, PX>), grid, blk, lds, s, p);
-    return hipGetLastError();
-}
-hipError_t launch_stripq(int f, int out, int d, int px, const TParams& p, dim3 grid, int lds, hipStream_t s) {
-    switch ((f * 2 + out) * 2 + (px == 2)) {
-    case (kNV12 * 2 + 0) * 2: return launch_stripq_t<kNV12, 0, 1>(d, p, grid, lds, s);
-    case (kNV12 * 2 + 0) * 2 + 1: return launch_stripq_t<kNV12, 0, 2>(d, p, grid, lds, s);
-    case (kNV12 * 2 + 1) * 2: return launch_stripq_t<kNV12, 1, 1>(d, p, grid, lds, s);
-    case (kNV12 * 2 + 1) * 2 + 1: return launch_stripq_t<kNV12, 1, 2>(d, p, grid, lds, s);
-    case (kI420 * 2 + 0) * 2: return launch_stripq_t<kI420, 0, 1>(d, p, grid, lds, s);
-    case (kI420 * 2 + 0) * 2 + 1: return launch_stripq_t<kI420, 0, 2>(d, p, grid, lds, s);
-    case (kI420 * 2 + 1) * 2: return launch_stripq_t<kI420, 1, 1>(d, p, grid, lds, s);
-    default: return launch_stripq_t<kI420, 1, 2>(d, p, grid, lds, s);
-    }
 }
 
 template <int FMT, int OUT, int PX>
@@ -3894,8 +3468,6 @@ struct evam_pp {
     std::vector<Geom> sc_geo;
     std::vector<int> sc_units;     // ROI work units: (item, row0, row1, cost)
     TParams sc_tparams;            // strip-kernel arguments (3.5 KB: kept off the stack)
-    unsigned* qcnt = nullptr;      // queue strip kernel: kQSlots launch slots of unit counters (device)
-    uint64_t qseq = 0;             // launches of the queue strip kernel so far (slot = qseq % kQSlots)
 };
 
 namespace {
@@ -3989,10 +3561,6 @@ void evam_pp_destroy(evam_pp* h) {
     HipRings b;
     h->ring.release(b);
     h->pin.release(b);
-    if (h->qcnt) {
-        (void)hipStreamSynchronize(h->stream);
-        (void)hipFree(h->qcnt);
-    }
     if (h->ev_switch) (void)hipEventDestroy(h->ev_switch);
     if (h->ev0) (void)hipEventDestroy(h->ev0);
     if (h->ev1) (void)hipEventDestroy(h->ev1);
@@ -4433,40 +4001,6 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
                     tp->slot_stride = dst->slot_stride;
                     tp->color_rgb = color_rgb;
                     tp->fill = fill;
-                    // Queue strip kernel where every output row and column is visible (no letterbox): the
-                    // same row work with short units handed out dynamically (evam_pp_stripq)
-                    const bool q = kn.stripq && kn.xcd <= 0 && g0.ox <= 0 && g0.ox + g0.rw >= DW && g0.oy <= 0 &&
-                                   g0.oy + g0.rh >= DH;
-                    if (q) {
-                        if (!h->qcnt) {
-                            const size_t qb = sizeof(unsigned) * (size_t)kQSlots * kQSlotWords;
-                            HIP_TRY(hipMalloc((void**)&h->qcnt, qb));
-                            HIP_TRY(hipMemsetAsync(h->qcnt, 0, qb, h->stream));
-                        }
-                        const int dq = std::min(D, 2);
-                        const int thq = std::max(dq, std::min(std::min(DH, 64), kn.stripq_th > 0 ? kn.stripq_th : 4));
-                        tp->TH = thq;
-                        tp->tiles_per_item = (DH + thq - 1) / thq;  // bands per item
-                        // waves per CU: EVAM_PP_STRIP_WAVES (16), at most what registers and LDS admit
-                        const int res = resident_per_cu(stripq_fn(f, cfg->out_dtype, dq, spx), lds) * tp->nw;
-                        const int wpc = std::max(1, std::min(std::min(32, kn.strip_waves), std::max(res, tp->nw)));
-                        const int wy = std::max(1, (wpc * h->n_cu) / (tp->tiles_x * tp->nw));
-                        for (int m0 = mfirst[f]; m0 < mfirst[f + 1]; m0 += kArgItems) {
-                            const int nm = std::min(kArgItems, mfirst[f + 1] - m0);
-                            fill_args(tp->items, m0, nm);
-                            tp->qunits = nm * tp->tiles_per_item;
-                            const int wyq = std::min(wy, tp->qunits);
-                            tp->qks = (int)((int64_t)tp->qunits * std::max(0, std::min(100, kn.stripq_static)) / 100 / wyq);
-                            tp->qcnt = h->qcnt + (size_t)(h->qseq % kQSlots) * kQSlotWords;
-                            tp->qzero = h->qcnt + (size_t)((h->qseq + kQAhead) % kQSlots) * kQSlotWords;
-                            h->qseq++;
-                            const dim3 gq((unsigned)tp->tiles_x, (unsigned)wyq);
-                            hipError_t e = launch_stripq(f, cfg->out_dtype, dq, spx, *tp, gq, lds, h->stream);
-                            if (e != hipSuccess) return fail(EVAM_PP_ERR_HIP, "kernel launch failed: %s", hipGetErrorString(e));
-                            launches++;
-                        }
-                        continue;
-                    }
                     for (int m0 = mfirst[f]; m0 < mfirst[f + 1]; m0 += kArgItems) {
                         const int nm = std::min(kArgItems, mfirst[f + 1] - m0);
                         fill_args(tp->items, m0, nm);

@@ -57,16 +57,12 @@ def test_c1_bench_batch(evam, O, coracle, gpu, shape, monkeypatch):
 
 # kernel shapes forced on the full-size workloads: the default choice (the strip kernel for C2 / C4 / C5),
 # the strip kernel's other ring depths and tile heights, and the staged kernel's pipeline shapes
-STAGED_SHAPES = {"default": {}, "stripq": {"EVAM_PP_STRIPQ": "1"}, "stripq_th8": {"EVAM_PP_STRIPQ": "1", "EVAM_PP_STRIPQ_TH": "8"},
-                 "stripq_w2": {"EVAM_PP_STRIPQ": "1", "EVAM_PP_STRIP_WAVES": "2", "EVAM_PP_STRIPQ_TH": "3"},
-                 "stripq_d1_px1": {"EVAM_PP_STRIPQ": "1", "EVAM_PP_STRIP_D": "1", "EVAM_PP_STRIP_PX": "1"},
-                 "stripq_dyn": {"EVAM_PP_STRIPQ": "1", "EVAM_PP_STRIPQ_STATIC": "0"}, "stripq_static": {"EVAM_PP_STRIPQ": "1", "EVAM_PP_STRIPQ_STATIC": "100"},
-                 "strip": {"EVAM_PP_STRIPQ": "0"},
-                 "strip_d1": {"EVAM_PP_STRIPQ": "0", "EVAM_PP_STRIP_D": "1"},
-                 "strip_d2": {"EVAM_PP_STRIPQ": "0", "EVAM_PP_STRIP_D": "2"},
-                 "strip_d3": {"EVAM_PP_STRIPQ": "0", "EVAM_PP_STRIP_D": "3"},
-                 "strip_th32": {"EVAM_PP_STRIPQ": "0", "EVAM_PP_STRIP_TH": "32"},
-                 "strip_px1": {"EVAM_PP_STRIPQ": "0", "EVAM_PP_STRIP_PX": "1"},
+STAGED_SHAPES = {"default": {},
+                 "strip_d1": {"EVAM_PP_STRIP_D": "1"},
+                 "strip_d2": {"EVAM_PP_STRIP_D": "2"},
+                 "strip_d3": {"EVAM_PP_STRIP_D": "3"},
+                 "strip_th32": {"EVAM_PP_STRIP_TH": "32"},
+                 "strip_px1": {"EVAM_PP_STRIP_PX": "1"},
                  "strip_xcd": {"EVAM_PP_XCD": "1"},
                  "staged": {"EVAM_PP_STRIP": "0"},
                  "r2": {"EVAM_PP_STRIP": "0", "EVAM_PP_STAGE_R": "2", "EVAM_PP_NSEGX": "4"},

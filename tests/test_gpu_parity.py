@@ -364,8 +364,7 @@ def test_stats_and_timing(evam, O, gpu):
 @pytest.mark.parametrize("variant", ["auto", "wave", "px1", "px2", "noreuse", "staged", "staged_xcd", "staged_r1",
                                      "staged_wide", "staged_b3", "staged_slot2k", "strip", "strip_d1", "strip_d2", "strip_d3",
                                      "strip_th5", "strip_nw8", "strip_xcd", "strip_px1", "strip_px2",
-                                     "strip_px2_d4_th7", "stripq_th3", "stripq_th64", "stripq_d1", "stripq_px1",
-                                     "stripq_w1", "stripq_dyn", "band", "band_px1", "band_px2", "band_th5", "band_th64"])
+                                     "strip_px2_d4_th7", "band", "band_px1", "band_px2", "band_th5", "band_th64"])
 def test_wave_kernel_variants(evam, O, coracle, gpu, fmt, src, dst, resize, variant, monkeypatch):
     """Uniform-geometry batches through the default kernel choice, the wave-row kernel forced
     (EVAM_PP_WAVE=2; every PX / REUSE choice), the staged kernel (EVAM_PP_WAVE=0 EVAM_PP_STRIP=0; with the
@@ -392,20 +391,12 @@ def test_wave_kernel_variants(evam, O, coracle, gpu, fmt, src, dst, resize, vari
            "strip_px2": {"EVAM_PP_STRIP": "2", "EVAM_PP_STRIP_PX": "2"},
            "strip_px2_d4_th7": {"EVAM_PP_STRIP": "2", "EVAM_PP_STRIP_PX": "2", "EVAM_PP_STRIP_D": "4",
                                 "EVAM_PP_STRIP_TH": "7"},
-           "stripq_th3": {"EVAM_PP_STRIPQ": "1", "EVAM_PP_STRIP": "2", "EVAM_PP_STRIPQ_TH": "3"},
-           "stripq_th64": {"EVAM_PP_STRIPQ": "1", "EVAM_PP_STRIP": "2", "EVAM_PP_STRIPQ_TH": "64"},
-           "stripq_d1": {"EVAM_PP_STRIPQ": "1", "EVAM_PP_STRIP": "2", "EVAM_PP_STRIP_D": "1"},
-           "stripq_px1": {"EVAM_PP_STRIPQ": "1", "EVAM_PP_STRIP": "2", "EVAM_PP_STRIP_PX": "1", "EVAM_PP_STRIPQ_TH": "2"},
-           "stripq_w1": {"EVAM_PP_STRIPQ": "1", "EVAM_PP_STRIP": "2", "EVAM_PP_STRIP_WAVES": "1", "EVAM_PP_STRIPQ_TH": "2"},
-           "stripq_dyn": {"EVAM_PP_STRIPQ": "1", "EVAM_PP_STRIP": "2", "EVAM_PP_STRIPQ_STATIC": "0", "EVAM_PP_STRIPQ_TH": "2"},
            "band": {"EVAM_PP_BAND": "2"}, "band_px1": {"EVAM_PP_BAND": "2", "EVAM_PP_BAND_PX": "1"},
            "band_px2": {"EVAM_PP_BAND": "2", "EVAM_PP_BAND_PX": "2"},
            "band_th5": {"EVAM_PP_BAND": "2", "EVAM_PP_STRIP_TH": "5"},
            "band_th64": {"EVAM_PP_BAND": "2", "EVAM_PP_STRIP_TH": "64"}}.get(variant, {})
     if variant.startswith(("staged", "band")):
         env["EVAM_PP_STRIP"] = "0"
-    if variant.startswith("strip_"):  # the static strip kernel (the queue kernel takes groups without letterbox)
-        env["EVAM_PP_STRIPQ"] = "0"
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     if variant == "px2" and dst[0] % 2:
