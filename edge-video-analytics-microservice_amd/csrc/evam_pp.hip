@@ -1584,12 +1584,12 @@ __device__ unsigned long long g_evam_trace[kTraceWGs * kTraceSlots];
         __builtin_amdgcn_sched_barrier(0);                                                             \
         asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");               \
         __builtin_amdgcn_sched_barrier(0);                                                             \
-        const unsigned w_ = (blockIdx.y * gridDim.x + blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);  \
+        const unsigned w_ = ((blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6); \
         if ((threadIdx.x & 63) == 0 && w_ < (unsigned)kTraceWGs) g_evam_trace[w_ * kTraceSlots + (k)] = t_; \
     } while (0)
 #define EVAM_WTRACE_VAL(k, v)                                                                          \
     do {                                                                                               \
-        const unsigned w_ = (blockIdx.y * gridDim.x + blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);  \
+        const unsigned w_ = ((blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6); \
         if ((threadIdx.x & 63) == 0 && w_ < (unsigned)kTraceWGs) g_evam_trace[w_ * kTraceSlots + (k)] = (v); \
     } while (0)
 #else
@@ -1603,6 +1603,7 @@ __device__ unsigned long long g_evam_trace[kTraceWGs * kTraceSlots];
 // strip kernel (uniform geometry, 4:2:0 sources, no shared source rows between output rows)
 // ------------------------------------------------------------------------------------------------
 constexpr int kMaxStrips = 32;  // per-strip footprints in the kernel arguments: DW <= 2048
+constexpr int kSfoot = 64;      // footprint entries: strip kernel tile column x 8 + wave (<= 8 columns)
 // One staged row segment of the strip kernel: a strip's footprint is at most one DMA instruction's 64
 // 16-byte chunks, so every LDS offset of the ring is a compile-time immediate. 64-column strips (PX = 1)
 // use half-size slots (footprints <= 512 B, downscales <= ~7.7x): half the LDS per wave.
@@ -1622,8 +1623,9 @@ struct TParams {
     int color_rgb;
     uint32_t fill;
     int xcd_remap;               // 1: consecutive tiles land on one XCD
-    int2 sfoot[kMaxStrips];      // per strip: crop-relative source columns of the first visible column's
+    int2 sfoot[kSfoot];          // per strip: crop-relative source columns of the first visible column's
                                  // first tap and the last visible column's last tap; (-1, -1): padding only
+                                 // (band kernel: per strip; strip kernel: per tile column x 8 + wave)
     // band kernel only: one wave per (item, band of TH rows, strip); LDS rows of one band
     int nstrips, units;          // strips per row; waves of work in the launch
     int segY, segC;              // bytes of one staged luma / chroma row (multiples of 16)
@@ -1662,27 +1664,24 @@ __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (kAblate & 128) return;  // diagnostics: launch cost only
     EVAM_WSTAMP(0);
-    const int p_nw = P.nw, p_tpi = P.tiles_per_item, p_tx = P.tiles_x, p_TH = P.TH, p_DH = P.DH, p_DW = P.DW;
-    const int p_grid = gridDim.x;
-    asm volatile("" ::"s"(p_nw), "s"(p_tpi), "s"(p_tx), "s"(p_TH), "s"(p_DH), "s"(p_DW), "s"(p_grid), "s"(P.xcd_remap),
-                 "s"(P.ox), "s"(P.rw), "s"(P.oy), "s"(P.rh), "s"(P.wave_bytes));
-    const int t = P.xcd_remap ? xcd_tile(blockIdx.x, p_grid) : (int)blockIdx.x;
-    const int item = t / p_tpi;
-    const int tile = t - item * p_tpi;
-    const int ty = tile / p_tx;
-    const int strip = (tile - ty * p_tx) * p_nw + wave;
-    const int Y0 = ty * p_TH, Y1 = min(Y0 + p_TH, p_DH);
+    // grid (tile column, tile row, item): every kernel-argument load of the prologue has an address known at
+    // entry, so they all go out in one batch (one round trip before the first DMA)
+    const int item = blockIdx.z, ty = blockIdx.y;
     const ItemArg& it = P.items[item];
+    const int2 sf = P.sfoot[min((int)blockIdx.x * 8 + wave, kSfoot - 1)];
+    const int p_nw = P.nw, p_TH = P.TH, p_DH = P.DH, p_DW = P.DW;
     const uint8_t* p0 = it.plane[0];
     const uint8_t* p1 = it.plane[1];
     const uint8_t* p2 = it.plane[2];
     const int pitch0 = it.pitch[0], pitch1 = it.pitch[1], pitch2 = it.pitch[2];
     const int x0 = it.x0, y0 = it.y0;
+    asm volatile("" ::"s"(p_nw), "s"(p_TH), "s"(p_DH), "s"(p_DW), "s"(P.ox), "s"(P.rw), "s"(P.oy), "s"(P.rh),
+                 "s"(P.wave_bytes), "s"(p0), "s"(p1), "s"(p2), "s"(pitch0), "s"(pitch1), "s"(pitch2), "s"(x0), "s"(y0),
+                 "s"(it.index), "s"(sf.x), "s"(sf.y), "s"(P.dst), "s"(P.slot_offset), "s"(P.slot_stride));
+    const int strip = (int)blockIdx.x * p_nw + wave;
+    const int Y0 = ty * p_TH, Y1 = min(Y0 + p_TH, p_DH);
     const int X0 = strip * 64 * PX;
     const bool live = X0 < p_DW;  // a wave past the last strip only joins the LUT barrier
-    const int2 sf = P.sfoot[min(strip, kMaxStrips - 1)];
-    asm volatile("" ::"s"(p0), "s"(p1), "s"(p2), "s"(pitch0), "s"(pitch1), "s"(pitch2), "s"(x0), "s"(y0),
-                 "s"(it.index), "s"(sf.x), "s"(sf.y), "s"(P.dst), "s"(P.slot_offset), "s"(P.slot_stride));
     const bool cols = live && sf.x >= 0;
     int fsY = 0, nY = 0, fsC = 0, nC = 0;
     if (cols) footprint_chunks(FMT, 1, x0 + sf.x, x0 + sf.y, fsY, nY, fsC, nC);
@@ -1992,6 +1991,7 @@ __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
 //  * coefficients of the strip's columns (per lane) and of the band's rows (one per lane, v_readlane)
 //    come from the kernels' shared linear_coef: no table loads;
 //  * each channel of a row leaves as one PX-wide store per lane.
+// Workgroups of up to four waves: the strips of one band of one item.
 template <int FMT, int OUT, int PX>
 __global__ __launch_bounds__(256) void evam_pp_band(const TParams P) {
     __shared__ __attribute__((aligned(16))) float lut_s[OUT == 1 ? 768 : 4];
@@ -2001,28 +2001,25 @@ __global__ __launch_bounds__(256) void evam_pp_band(const TParams P) {
     constexpr int NPC = FMT == kI420 ? 2 : 1;  // chroma planes
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int p_tpi = P.tiles_per_item, p_ns = P.nstrips, p_TH = P.TH, p_DH = P.DH, p_DW = P.DW;
-    asm volatile("" ::"s"(p_tpi), "s"(p_ns), "s"(p_TH), "s"(p_DH), "s"(p_DW), "s"(P.units), "s"(P.ox), "s"(P.rw),
-                 "s"(P.oy), "s"(P.rh), "s"(P.wave_bytes), "s"(P.segY), "s"(P.segC), "s"(P.nrY));
-    // wave unit u -> (item, band, strip); consecutive waves: neighbouring strips of one band
-    const int u = (int)blockIdx.x * (blockDim.x >> 6) + wave;
-    const bool live = u < P.units;
-    const int uu = live ? u : 0;
-    const int item = uu / p_tpi;
-    const int rem = uu - item * p_tpi;
-    const int band = rem / p_ns;
-    const int strip = rem - band * p_ns;
-    const int Y0 = band * p_TH, Y1 = min(Y0 + p_TH, p_DH);
+    // grid (strip group, band, item): every kernel-argument load of the prologue has an address known at entry,
+    // so they all go out in one batch (one round trip before the first DMA)
+    const int item = blockIdx.z, band = blockIdx.y;
     const ItemArg& it = P.items[item];
+    const int2 sf = P.sfoot[min((int)blockIdx.x * 8 + wave, kSfoot - 1)];
+    const int p_nw = P.nw, p_ns = P.nstrips, p_TH = P.TH, p_DH = P.DH, p_DW = P.DW;
     const uint8_t* p0 = it.plane[0];
     const uint8_t* p1 = it.plane[1];
     const uint8_t* p2 = it.plane[2];
     const int pitch0 = it.pitch[0], pitch1 = it.pitch[1], pitch2 = it.pitch[2];
     const int x0 = it.x0, y0 = it.y0;
+    asm volatile("" ::"s"(p_nw), "s"(p_ns), "s"(p_TH), "s"(p_DH), "s"(p_DW), "s"(P.ox), "s"(P.rw), "s"(P.oy), "s"(P.rh),
+                 "s"(P.wave_bytes), "s"(P.segY), "s"(P.segC), "s"(P.nrY), "s"(p0), "s"(p1), "s"(p2), "s"(pitch0),
+                 "s"(pitch1), "s"(pitch2), "s"(x0), "s"(y0), "s"(it.index), "s"(sf.x), "s"(sf.y), "s"(P.dst),
+                 "s"(P.slot_offset), "s"(P.slot_stride));
+    const int strip = (int)blockIdx.x * p_nw + wave;
+    const bool live = strip < p_ns;
+    const int Y0 = band * p_TH, Y1 = min(Y0 + p_TH, p_DH);
     const int X0 = strip * 64 * PX;
-    const int2 sf = P.sfoot[min(strip, kMaxStrips - 1)];
-    asm volatile("" ::"s"(p0), "s"(p1), "s"(p2), "s"(pitch0), "s"(pitch1), "s"(pitch2), "s"(x0), "s"(y0),
-                 "s"(it.index), "s"(sf.x), "s"(sf.y), "s"(P.dst), "s"(P.slot_offset), "s"(P.slot_stride));
     const bool cols = live && sf.x >= 0;
     int fsY = 0, nY = 0, fsC = 0, nC = 0;
     if (cols) footprint_chunks(FMT, 1, x0 + sf.x, x0 + sf.y, fsY, nY, fsC, nC);
@@ -3176,10 +3173,12 @@ bool plan_strip(int f, const Geom& g, int DW, int DH, int count, int out_dtype, 
     p.scale_x = 1. / ((double)g.rw / g.cw);
     p.scale_y = 1. / ((double)g.rh / g.ch);
     const int sw = 64 * px;
-    for (int s = 0; s < kMaxStrips; s++) {
+    for (int k = 0; k < kSfoot; k++) {  // entry tile column x 8 + wave (nw <= 8, tiles_x <= 8)
+        const int tx = k >> 3, w = k & 7, s = tx * nw + w;
         const int Xv0 = std::max(s * sw, g.ox), Xv1 = std::min(std::min(s * sw + sw, DW), g.ox + g.rw) - 1;
-        p.sfoot[s] = s < nstrips && Xv0 <= Xv1 ? int2{xt[Xv0].s0, xt[Xv1].s1} : int2{-1, -1};
+        p.sfoot[k] = w < nw && s < nstrips && Xv0 <= Xv1 ? int2{xt[Xv0].s0, xt[Xv1].s1} : int2{-1, -1};
     }
+    if ((p.tiles_x - 1) * 8 + nw > kSfoot) return false;
     const int64_t gr = (int64_t)std::min(count, kArgItems) * p.tiles_per_item;
     if (gr > 0x7FFFFFFF) return false;
     grid = (int)gr;
@@ -3187,16 +3186,16 @@ bool plan_strip(int f, const Geom& g, int DW, int DH, int count, int out_dtype, 
 }
 
 template <int FMT, int OUT, int PX>
-hipError_t launch_strip_t(int d, const TParams& p, int grid, int lds, hipStream_t s) {
+hipError_t launch_strip_t(int d, const TParams& p, dim3 grid, int lds, hipStream_t s) {
     const dim3 blk(64 * p.nw);
-    if (d == 4) hipLaunchKernelGGL((evam_pp_strip<FMT, OUT, 4, PX>), dim3(grid), blk, lds, s, p);
-    else if (d == 3) hipLaunchKernelGGL((evam_pp_strip<FMT, OUT, 3, PX>), dim3(grid), blk, lds, s, p);
-    else if (d == 2) hipLaunchKernelGGL((evam_pp_strip<FMT, OUT, 2, PX>), dim3(grid), blk, lds, s, p);
-    else hipLaunchKernelGGL((evam_pp_strip<FMT, OUT, 1, PX>), dim3(grid), blk, lds, s, p);
+    if (d == 4) hipLaunchKernelGGL((evam_pp_strip<FMT, OUT, 4, PX>), grid, blk, lds, s, p);
+    else if (d == 3) hipLaunchKernelGGL((evam_pp_strip<FMT, OUT, 3, PX>), grid, blk, lds, s, p);
+    else if (d == 2) hipLaunchKernelGGL((evam_pp_strip<FMT, OUT, 2, PX>), grid, blk, lds, s, p);
+    else hipLaunchKernelGGL((evam_pp_strip<FMT, OUT, 1, PX>), grid, blk, lds, s, p);
     return hipGetLastError();
 }
 
-hipError_t launch_strip(int f, int out, int d, int px, const TParams& p, int grid, int lds, hipStream_t s) {
+hipError_t launch_strip(int f, int out, int d, int px, const TParams& p, dim3 grid, int lds, hipStream_t s) {
     switch ((f * 2 + out) * 2 + (px == 2)) {
     case (kNV12 * 2 + 0) * 2: return launch_strip_t<kNV12, 0, 1>(d, p, grid, lds, s);
     case (kNV12 * 2 + 0) * 2 + 1: return launch_strip_t<kNV12, 0, 2>(d, p, grid, lds, s);
@@ -3279,7 +3278,7 @@ bool plan_band(int f, const Geom& g, int DW, int DH, int count, int out_dtype, i
         }
         p.nrY = nrY;
         p.wave_bytes = nrY * p.segY + (nrY / 2 + 1) * p.segC;
-        nw = 4;
+        nw = std::min(4, nstrips);  // a workgroup: up to four strips of one band
         lds = nw * p.wave_bytes + 16;  // + 16: a right-edge tap reads past its footprint (weight 0)
         if (lds + lut_static <= 64 * 1024) break;
         if (th == 1) return false;
@@ -3292,25 +3291,27 @@ bool plan_band(int f, const Geom& g, int DW, int DH, int count, int out_dtype, i
     p.scale_x = 1. / ((double)g.rw / g.cw);
     p.scale_y = 1. / ((double)g.rh / g.ch);
     p.nw = nw;
-    p.tiles_x = nstrips;
+    p.tiles_x = (nstrips + nw - 1) / nw;  // strip groups
     p.xcd_remap = 0;
+    if ((p.tiles_x - 1) * 8 + nw > kSfoot) return false;
     const int sw = 64 * px;
-    for (int s = 0; s < kMaxStrips; s++) {
+    for (int k = 0; k < kSfoot; k++) {  // entry strip group x 8 + wave
+        const int w = k & 7, s = (k >> 3) * nw + w;
         const int Xv0 = std::max(s * sw, g.ox), Xv1 = std::min(std::min(s * sw + sw, DW), g.ox + g.rw) - 1;
-        p.sfoot[s] = s < nstrips && Xv0 <= Xv1 ? int2{xt[Xv0].s0, xt[Xv1].s1} : int2{-1, -1};
+        p.sfoot[k] = w < nw && s < nstrips && Xv0 <= Xv1 ? int2{xt[Xv0].s0, xt[Xv1].s1} : int2{-1, -1};
     }
     return (int64_t)per_launch * p.tiles_per_item <= 0x7FFFFFFF;
 }
 
 template <int FMT, int OUT>
-hipError_t launch_band_t(int px, const TParams& p, int grid, int nw, int lds, hipStream_t s) {
+hipError_t launch_band_t(int px, const TParams& p, dim3 grid, int nw, int lds, hipStream_t s) {
     const dim3 blk(64 * nw);
-    if (px == 4) hipLaunchKernelGGL((evam_pp_band<FMT, OUT, 4>), dim3(grid), blk, lds, s, p);
-    else if (px == 2) hipLaunchKernelGGL((evam_pp_band<FMT, OUT, 2>), dim3(grid), blk, lds, s, p);
-    else hipLaunchKernelGGL((evam_pp_band<FMT, OUT, 1>), dim3(grid), blk, lds, s, p);
+    if (px == 4) hipLaunchKernelGGL((evam_pp_band<FMT, OUT, 4>), grid, blk, lds, s, p);
+    else if (px == 2) hipLaunchKernelGGL((evam_pp_band<FMT, OUT, 2>), grid, blk, lds, s, p);
+    else hipLaunchKernelGGL((evam_pp_band<FMT, OUT, 1>), grid, blk, lds, s, p);
     return hipGetLastError();
 }
-hipError_t launch_band(int f, int out, int px, const TParams& p, int grid, int nw, int lds, hipStream_t s) {
+hipError_t launch_band(int f, int out, int px, const TParams& p, dim3 grid, int nw, int lds, hipStream_t s) {
     switch (f * 2 + out) {
     case kNV12 * 2 + 0: return launch_band_t<kNV12, 0>(px, p, grid, nw, lds, s);
     case kNV12 * 2 + 1: return launch_band_t<kNV12, 1>(px, p, grid, nw, lds, s);
@@ -4004,12 +4005,12 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
                     for (int m0 = mfirst[f]; m0 < mfirst[f + 1]; m0 += kArgItems) {
                         const int nm = std::min(kArgItems, mfirst[f + 1] - m0);
                         fill_args(tp->items, m0, nm);
-                        const int64_t gr = (int64_t)nm * tp->tiles_per_item;
-                        // Dispatch order, not XCD-contiguous: the C2 data movement in the strip pattern takes
-                        // 1.7 us longer with each XCD on its own run of tiles (profiles/r03c_strip_bw.txt);
-                        // EVAM_PP_XCD=1 forces that order
-                        tp->xcd_remap = kn.xcd > 0 ? 1 : 0;
-                        hipError_t e = launch_strip(f, cfg->out_dtype, D, spx, *tp, (int)gr, lds, h->stream);
+                        // grid (tile column, tile row, item), dispatched in that order (the C2 data movement in
+                        // the strip pattern takes 1.7 us longer with each XCD on its own run of tiles,
+                        // profiles/r03c_strip_bw.txt)
+                        tp->xcd_remap = 0;
+                        const dim3 gr((unsigned)tp->tiles_x, (unsigned)((DH + tp->TH - 1) / tp->TH), (unsigned)nm);
+                        hipError_t e = launch_strip(f, cfg->out_dtype, D, spx, *tp, gr, lds, h->stream);
                         if (e != hipSuccess) return fail(EVAM_PP_ERR_HIP, "kernel launch failed: %s", hipGetErrorString(e));
                         launches++;
                     }
@@ -4033,7 +4034,7 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
                         const int nm = std::min(kArgItems, mfirst[f + 1] - m0);
                         fill_args(tp->items, m0, nm);
                         tp->units = nm * tp->tiles_per_item;
-                        const int gr = (tp->units + nw - 1) / nw;
+                        const dim3 gr((unsigned)tp->tiles_x, (unsigned)((DH + tp->TH - 1) / tp->TH), (unsigned)nm);
                         hipError_t e = launch_band(f, cfg->out_dtype, bpx, *tp, gr, nw, lds, h->stream);
                         if (e != hipSuccess) return fail(EVAM_PP_ERR_HIP, "kernel launch failed: %s", hipGetErrorString(e));
                         launches++;
