@@ -65,6 +65,9 @@ def main():
     t0 = tr[:, 0].astype(np.int64).min()
     t = (tr[:, :5].astype(np.int64) - t0) * 10 / 1000.0  # us from the first wave's entry
     rows = (tr[:, 5] >> 48).astype(int)
+    idx = np.nonzero(np.frombuffer(buf, dtype=np.uint64).reshape(cap, SLOTS)[:, 4] != 0)[0]
+    n_cu = torch.cuda.get_device_properties(0).multi_processor_count
+    rank = (idx // 4) // n_cu  # workgroups of 4 waves (C2 / C4 / C5 strip tiles)
     xcc = (tr[:, 6] & 0xFFFFFFFF).astype(int)
 
     def dist(v):
@@ -85,6 +88,11 @@ def main():
             "end (absolute)": dist(end)},
         "us_per_row_after_first": dist(loop / np.maximum(rows, 1)),
         "end_by_xcc": {int(x): round(float(end[xcc == x].max()), 2) for x in sorted(set(xcc.tolist()))},
+        # dispatch-order rank of the wave's workgroup on its CU (linear workgroup index // CUs): the older
+        # waves of a SIMD win its issue arbitration (MI355X_MICROARCH.md, Two waves per SIMD, item 2)
+        "end_by_dispatch_rank": {int(r): dist(end[rank == r]) for r in sorted(set(rank.tolist()))},
+        "us_per_row_by_dispatch_rank": {int(r): dist((loop / np.maximum(rows, 1))[rank == r])
+                                        for r in sorted(set(rank.tolist()))},
         "active_waves_by_us": [int(((t[:, 0] <= u) & (end > u)).sum()) for u in np.arange(0, float(end.max()) + 1, 1.0)],
     }
     print(json.dumps(res), flush=True)
