@@ -2001,6 +2001,7 @@ __global__ __launch_bounds__(256) void evam_pp_band(const TParams P) {
     constexpr int NPC = FMT == kI420 ? 2 : 1;  // chroma planes
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    EVAM_WSTAMP(0);
     // grid (strip group, band, item): every kernel-argument load of the prologue has an address known at entry,
     // so they all go out in one batch (one round trip before the first DMA)
     const int item = blockIdx.z, band = blockIdx.y;
@@ -2081,6 +2082,8 @@ __global__ __launch_bounds__(256) void evam_pp_band(const TParams P) {
         }
     }
     const int kd_total = n ? (rhi - rlo + 1) + NPC * (((y0 + rhi) >> 1) - clo + 1) : 0;
+    EVAM_WSTAMP(1);
+    EVAM_WTRACE_VAL(5, (unsigned long long)n << 48);
 
     if constexpr (OUT == 1) {
         vmcnt_exact(kd_total);  // this wave's LUT pieces landed (issued before every row)
@@ -2193,6 +2196,12 @@ __global__ __launch_bounds__(256) void evam_pp_band(const TParams P) {
         // rows up to rb landed: issued after them, the DMA of later rows and the stores of rows 0 .. i-1
         const int kd = (rb - rlo + 1) + NPC * (((y0 + rb) >> 1) - clo + 1);
         vmcnt_exact(kd_total - kd + nst * i);
+#ifdef EVAM_PP_TRACE
+        if (i == 0) {
+            EVAM_WSTAMP(2);
+            EVAM_WSTAMP(3);
+        }
+#endif
         const uint32_t wb0 = (uint32_t)__builtin_amdgcn_readlane(lb0, i), wb1 = (uint32_t)__builtin_amdgcn_readlane(lb1, i);
         // HA <- row ra, HB <- row rb, reusing what the previous output row filtered (wave-uniform branches)
         if (ra != pa) {
@@ -2232,6 +2241,15 @@ __global__ __launch_bounds__(256) void evam_pp_band(const TParams P) {
         asm volatile("" ::: "memory");  // issue order is what the counted waits assume
     }
     for (int Y = max(n ? vr1 : Y1, Y0); Y < Y1; Y++) put_fill(Y);  // letterbox rows below
+#ifdef EVAM_PP_TRACE
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    EVAM_WSTAMP(4);
+    {
+        unsigned xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        EVAM_WTRACE_VAL(6, (unsigned long long)xcc);
+    }
+#endif
 }
 
 static_assert(sizeof(evam_roi) == 20, "evam_roi layout");

@@ -1,12 +1,13 @@
 #!/usr/bin/env python3
-"""Per-wave timeline of one strip-kernel launch (diagnostic; needs the trace build).
+"""Per-wave timeline of one strip- or band-kernel launch (diagnostic; needs the trace build).
 
 Build:  tools/build_variant.sh trace "-DEVAM_PP_TRACE=1"      (ab/libevam_pp_trace.so)
 Run:    EVAM_PP_LIB=ab/libevam_pp_trace.so EVAM_PP_DIAGNOSTIC_BUILD_OK=1 python tools/wave_timeline.py --config c2
 
 Runs bench.py's own workload (pooled frame sets, device-resident), then reads the stamps every wave of the
 last launch wrote on the 100 MHz constant clock (10 ns): entry, first DMA issued, LUT barrier passed, first
-row's DMA landed, end (last stores retired). Prints phase distributions, the active waves over time and
+row's DMA landed, end (last stores retired). The band kernel (C1) stamps its first row's landing as both the
+LUT barrier and the landing, and its workgroups hold two waves (the dispatch rank assumes four). Prints phase distributions, the active waves over time and
 per-XCD end times, as one JSON object.
 """
 import argparse
@@ -25,7 +26,7 @@ SLOTS = 12  # kTraceSlots of the trace build
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--config", default="c2", choices=["c2", "c4", "c5"])
+    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c4", "c5"])
     ap.add_argument("--steps", type=int, default=40)
     a = ap.parse_args()
     if "trace" not in os.environ.get("EVAM_PP_LIB", ""):
@@ -42,7 +43,8 @@ def main():
     info = bench.make_info(evam, wl)
     DW, DH = wl["dst"]
     sets = [evam.ImageBatch(bench.device_frames(evam, torch, wl, n, dev, seed=1234 + 7919 * k)) for k in range(5)]
-    outs = [torch.empty((n * (ring or 1), 3, DH, DW), dtype=torch.float32, device=dev) for _ in range(1 if ring else 5)]
+    dt = torch.float32 if wl["dtype"] == "f32" else torch.uint8
+    outs = [torch.empty((n * (ring or 1), 3, DH, DW), dtype=dt, device=dev) for _ in range(1 if ring else 5)]
     pp = evam.HipPreProcessor(device=0)
     lib = evam.native.load_library()
     lib.evam_pp_debug_trace.argtypes = [ctypes.c_void_p, ctypes.c_int]
