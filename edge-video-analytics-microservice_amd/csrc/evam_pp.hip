@@ -734,6 +734,14 @@ struct LaneRows {
 // takes an immediate, so n is rounded DOWN to one of a few levels (always safe: it only waits longer) by
 // a short ladder of scalar compares; a full 64-way switch cost more SALU and branch issue per row group
 // than it saved.
+// Workgroup barrier for data written to LDS by ds_write only: lgkmcnt(0) and a raw s_barrier. __syncthreads()
+// also waits vmcnt(0), which drains every LDS-DMA in flight (cdna_hip_programming.md, Pipelining across barriers).
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
 __device__ __forceinline__ void vmcnt_at_most(int n) {
     n = __builtin_amdgcn_readfirstlane(n);
     if (n >= 24) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
@@ -1815,6 +1823,8 @@ __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
             for (int idx = threadIdx.x; idx < 768; idx += nthr)
                 lut_s[idx] = P.lut[P.color_rgb ? 512 - (idx & ~255) + (idx & 255) : idx];
         }
+        // (an lds_barrier() here measured equal: the compiler already waits vmcnt(0) before the LUT's ds_writes,
+        // which may alias the ring's LDS-DMA destinations; profiles/r03x_barrier_tail_ab.txt)
         __syncthreads();
     }
     EVAM_WSTAMP(2);
@@ -2445,7 +2455,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(96))) void
     // q / n for q < 2^16 by one mul_hi: m = ceil(2^32 / n) is exact there (n = 1: the identity).
     const uint32_t mY = nY > 1 ? (uint32_t)((0x100000000ull + nY - 1) / nY) : 0u;
     const uint32_t mC = nC > 1 ? (uint32_t)((0x100000000ull + nC - 1) / nC) : 0u;
-    __syncthreads();  // row table (and on the first unit the LUT) visible
+    // Row table visible: LDS writes only (lgkmcnt) and a raw barrier. __syncthreads() would add vmcnt(0) and
+    // hold every wave until the LUT's LDS-DMA landed; group 0's wait below covers the LUT instead.
+    lds_barrier();
     EVAM_STAMP(8);
     // One plane region of group grp: chunk q -> (segment, chunk) -> (row, tap) -> source offset.
     // Returns the number of DMA instructions this wave issued (wave-uniform: an instruction with no active
@@ -2502,7 +2514,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(96))) void
         }
         xt[X] = e;
     }
-    __syncthreads();  // column table visible to the per-lane setup
+    lds_barrier();  // column table visible to the per-lane setup; group 0's DMA stays in flight
     EVAM_STAMP(9);
     // fill in source channel order (P.fill is in output plane order); fp32: LUT byte offsets
     const uint32_t fsh = OUT == 1 ? 2 : 0;
@@ -2766,6 +2778,7 @@ struct Knobs {
     int roi_th = -1, roi_buf = -1, roi_px = 1, roi_sort = 1, roi_xcd = 0;  // roi_buf -1: sized for one round
     int roi_unit = 0;                              // ROI work-unit size in row groups (0: one unit per base tile)
     int roi_nbuf = 2;                              // ROI staging buffers (3: two groups of DMA in flight)
+    int roi_tail = 4;                              // row tiles per ROI of the uneven tail over the CUs (1: no split)
     int strip = 1, strip_th = -1, strip_d = -1, strip_nw = -1, strip_px = 0;  // strip kernel: allowed (2: forced),
                                                                               // rows per tile, ring depth, waves, px
     int strip_waves = 16;                          // strip / band kernels: resident waves per CU the tiles are sized for
@@ -2786,7 +2799,7 @@ struct Knobs {
         roi_th = env_int("EVAM_PP_ROI_TH", roi_th); roi_buf = env_int("EVAM_PP_ROI_BUF", roi_buf);
         roi_px = env_int("EVAM_PP_ROI_PX", roi_px); roi_sort = env_int("EVAM_PP_ROI_SORT", roi_sort);
         roi_xcd = env_int("EVAM_PP_ROI_XCD", roi_xcd); roi_unit = env_int("EVAM_PP_ROI_UNIT", roi_unit);
-        roi_nbuf = env_int("EVAM_PP_ROI_NBUF", roi_nbuf);
+        roi_nbuf = env_int("EVAM_PP_ROI_NBUF", roi_nbuf); roi_tail = env_int("EVAM_PP_ROI_TAIL", roi_tail);
     }
 };
 
@@ -3808,6 +3821,9 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
             const int64_t per = qbase[f] == 1 && kn.roi_unit > 0
                                     ? std::min<int64_t>(DH, (DH + kn.roi_unit - 1) / kn.roi_unit) : qbase[f];
             dyn_bytes += sizeof(RoiRec) * (size_t)count[f] * (size_t)per;
+            // tail split: up to n_cu ROIs become kn.roi_tail row tiles each
+            if (qbase[f] == 1 && kn.roi_unit <= 0 && kn.roi_tail > 1)
+                dyn_bytes += sizeof(RoiRec) * (size_t)std::min(count[f], h->n_cu) * (size_t)(kn.roi_tail - 1);
         }
     }
     h->h_block.resize(nbytes);
@@ -3910,14 +3926,31 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
             if (base == 1 && gt <= 0) {
                 // one unit per ROI (the default): no row split, no 64-bit divisions (this loop runs per ROI
                 // on the host for every call: 1,600 ROIs in C3)
-                un.resize(4 * ord.size());
+                // Tail split: every ROI does the same pixel work (DW x DH), so when the ROIs do not divide
+                // evenly over the CUs the last `tail` ROIs in launch order land as one extra workgroup on
+                // `tail` CUs, whose SIMDs then convert 1 / floor(count / n_cu) more pixels than the others and
+                // end the launch (profiles/r03s_c3_roi_timeline_lut_dma.json: the last workgroups to finish
+                // are those narrow, compute-dense crops). Splitting those ROIs into kn.roi_tail row tiles —
+                // as long as every unit stays resident — gives each of the CUs a fraction of an ROI instead.
+                const int n = (int)ord.size();
+                const int tail = n % h->n_cu;
+                int ts = 1;
+                if (kn.roi_tail > 1 && tail > 0 && DH >= 2)
+                    ts = (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)kn.roi_tail, (int64_t)DH,
+                                                                      (qslots[f] - (n - tail)) / tail}));
+                const int nsplit = ts > 1 ? tail : 0;
+                un.resize(4 * ((size_t)n + (size_t)nsplit * (ts - 1)));
                 int* u4 = un.data();
-                for (size_t p = 0; p < ord.size(); p++, u4 += 4) {
+                for (int p = 0; p < n; p++) {
                     const int i = ord[p];
                     const int R = std::max(1, std::min(std::min(q.buf_bytes / row_bytes_bound(f, geo[i].cw), rcap), DH));
-                    const int cost = (DH + R - 1) / R;
-                    maxcost = std::max(maxcost, cost);
-                    u4[0] = i; u4[1] = 0; u4[2] = DH; u4[3] = cost;
+                    const int nt = p >= n - nsplit ? ts : 1;
+                    for (int t = 0; t < nt; t++, u4 += 4) {
+                        const int y0 = DH * t / nt, y1 = DH * (t + 1) / nt;
+                        const int cost = (y1 - y0 + R - 1) / R;
+                        maxcost = std::max(maxcost, cost);
+                        u4[0] = i; u4[1] = y0; u4[2] = y1; u4[3] = cost;
+                    }
                 }
             } else
             for (size_t p = 0; p < ord.size(); p++) {

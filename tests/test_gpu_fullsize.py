@@ -93,11 +93,15 @@ def test_c2_bench_batch(evam, O, coracle, gpu, shape, monkeypatch):
     pp.close()
 
 
+@pytest.mark.parametrize("tail", ["1", "4"])
 @pytest.mark.parametrize("seed", [0, 3])
-def test_c3_bench_roi_set(evam, O, coracle, gpu, seed):
+def test_c3_bench_roi_set(evam, O, coracle, gpu, seed, tail, monkeypatch):
     """C3: bench.py's seeded ROI set (50 per frame, w 24..400, h 24..300) on 32 bench 1080p NV12 frames ->
-    1600x3x72x72 fp32 through the ROI kernel."""
+    1600x3x72x72 fp32 through the ROI kernel, with and without the tail split (EVAM_PP_ROI_TAIL: the 64 ROIs
+    beyond 6 per CU as row tiles)."""
     import torch
+
+    monkeypatch.setenv("EVAM_PP_ROI_TAIL", tail)
 
     wl = bench.WORKLOADS["c3"]
     imgs = bench.device_frames(evam, torch, wl, 32, gpu, seed=1234)

@@ -605,6 +605,28 @@ def test_roi_work_units(evam, O, coracle, gpu, unit, monkeypatch):
     assert_same(got, ref, f"roi units {unit}")
 
 
+@pytest.mark.parametrize("tail", ["1", "2", "4", "7"])
+@pytest.mark.parametrize("dst", [(72, 72), (37, 29)])
+def test_roi_tail_split(evam, O, coracle, gpu, tail, dst, monkeypatch):
+    """ROI batches whose uneven tail over the CUs is split into row tiles (EVAM_PP_ROI_TAIL): with fewer ROIs
+    than CUs every ROI is in the tail, so each becomes `tail` row tiles (any DH, including heights that do not
+    divide evenly) and every tile lands in its own rows of the ROI's slot."""
+    import torch
+
+    monkeypatch.setenv("EVAM_PP_ROI_TAIL", tail)
+    rng = np.random.default_rng(zlib.crc32(f"tail{tail}{dst}".encode()))
+    W, H = 640, 360
+    frames = [O.random_frame(rng, O.NV12, W, H, pattern="gradient" if i else "uniform") for i in range(2)]
+    rois = [(int(rng.integers(0, 2)), int(rng.integers(0, W - 8)), int(rng.integers(0, H - 8)),
+             int(rng.integers(8, 400)), int(rng.integers(8, 300))) for _ in range(40)]
+    info = evam.PreProcInfo(range=(0.0, 1.0), mean=(0.1, 0.2, 0.3), std=(0.3, 0.2, 0.1))
+    shape = (len(rois), 3, dst[1], dst[0])
+    got, _ = run_hip(evam, torch, upload(evam, frames, gpu), shape, torch.float32, info,
+                     rois=[evam.Roi(*r) for r in rois])
+    ref, _ = run_oracle(O, coracle, frames, shape, "f32", info, rois=rois)
+    assert_same(got, ref, f"roi tail split {tail} {dst}")
+
+
 @pytest.mark.parametrize("fmt", FORMATS)
 @pytest.mark.parametrize("buf", ["0", "1024", "3072"])
 def test_roi_kernel_three_buffers(evam, O, coracle, gpu, fmt, buf, monkeypatch):
