@@ -1742,16 +1742,16 @@ __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
         }
     };
 
-    // LUT loads first (oldest VMEM: the first row's wait covers them), then the ring's first D rows.
-    float lutv[3];
+    // The LUT first (oldest VMEM: the first row's wait covers it), then the ring's first D rows. With four or
+    // more waves, waves 0-2 each bring one 1 KB section by LDS-DMA (source section swapped for RGB): no ds_write
+    // follows the ring's DMA, so nothing makes the compiler drain the ring before the LUT barrier.
     const int nthr = p_nw * 64;
-    const bool lut_early = nthr >= 256;  // three LUT entries per thread cover the 768
+    const bool lut_early = nthr >= 256;
     if constexpr (OUT == 1) {
-        if (lut_early)
-#pragma unroll
-        for (int q = 0; q < 3; q++) {
-            const int idx = threadIdx.x + q * nthr;
-            lutv[q] = idx < 768 ? P.lut[P.color_rgb ? 512 - (idx & ~255) + (idx & 255) : idx] : 0.f;
+        if (lut_early && wave < 3) {
+            const __amdgpu_buffer_rsrc_t rsL = __builtin_amdgcn_make_buffer_rsrc((void*)P.lut, (short)0, 3072, 0x00020000);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsL, (__attribute__((address_space(3))) void*)(lut_s + wave * 256), 16,
+                                                     (uint32_t)lane * 16u, (P.color_rgb ? 2 - wave : wave) * 1024, 0, 0);
         }
     }
     const int npro = min(n, D);
@@ -1811,21 +1811,16 @@ __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
 
     if constexpr (OUT == 1) {
         if (lut_early) {
-            // the LUT loads landed once at most the ring's DMA instructions are outstanding
+            // this wave's LUT section landed once at most the ring's DMA instructions are outstanding; the
+            // barrier then needs no vmcnt(0): each wave waits for its own ring rows in the loop
             if (npro == D) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NMIN * D) : "memory");
             else vmcnt_exact(NMIN * npro);
-#pragma unroll
-            for (int q = 0; q < 3; q++) {
-                const int idx = threadIdx.x + q * nthr;
-                if (idx < 768) lut_s[idx] = lutv[q];
-            }
+            lds_barrier();
         } else {  // workgroups of 1-3 waves (outputs narrower than 64 x PX x 3 + 1 columns)
             for (int idx = threadIdx.x; idx < 768; idx += nthr)
                 lut_s[idx] = P.lut[P.color_rgb ? 512 - (idx & ~255) + (idx & 255) : idx];
+            __syncthreads();
         }
-        // (an lds_barrier() here measured equal: the compiler already waits vmcnt(0) before the LUT's ds_writes,
-        // which may alias the ring's LDS-DMA destinations; profiles/r03x_barrier_tail_ab.txt)
-        __syncthreads();
     }
     EVAM_WSTAMP(2);
     if (!live) return;
