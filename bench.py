@@ -405,16 +405,24 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    e0.record(stream)
+    # Launch-time events: e0 goes on the stream after step 0's launch, so e0 -> e1 spans launches 1 .. K-1 back
+    # to back. Recorded before step 0, e0 also timed the idle GPU while the host enqueued step 0 (~20 us after
+    # the synchronize: ~1 us per step of a 20-step run, profiles/r03y_bench_lines.txt). The wall clock (value)
+    # still covers all K steps.
+    ev_from = 1 if args.steps > 1 else 0
+    if ev_from == 0:
+        e0.record(stream)
     for t in range(args.steps):
         step(t)
+        if t == 0 and ev_from == 1:
+            e0.record(stream)
     t_submit = time.perf_counter() - t0  # host time to enqueue the K steps (≈ wall when host-bound)
     e1.record(stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     wall = time.perf_counter() - t0
-    kern_ms = e0.elapsed_time(e1) / args.steps  # one launch per step
+    kern_ms = e0.elapsed_time(e1) / (args.steps - ev_from)  # one launch per step
     # Per-launch spread (median, p10 / p90), measured after the timed region: one event
     # pair around each of up to 200 extra steps, so the timed loop above carries no per-step events.
     n_dist = min(args.steps, 200)
@@ -479,6 +487,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "algorithmic_bytes_per_launch": alg_bytes, "mean_launch_ms": round(kern_ms, 5),
+                         "event_launches": args.steps - ev_from,
                          "launch_ms_p10_p50_p90": [pct[10], pct[50], pct[90]], "resident": resident},
         }
         valu = load_pmc_valu(args.config, n, P) if args.config in VALU_BOUND_CONFIGS else None
@@ -491,7 +500,7 @@ def main():
             res["roofline"] = {"bound": "valu", "achieved": round(g, 1), "peak": VALU_PEAK_GINST,
                                "unit": "G wave64-VALU-inst/s", "frac": round(g / VALU_PEAK_GINST, 4),
                                "traffic": r["traffic"], "valu_insts_per_launch": valu, "hbm": hbm,
-                               **{k: r[k] for k in ("algorithmic_bytes_per_launch", "mean_launch_ms",
+                               **{k: r[k] for k in ("algorithmic_bytes_per_launch", "mean_launch_ms", "event_launches",
                                                     "launch_ms_p10_p50_p90", "resident")}}
         if feed is not None:
             res["h2d"] = {"bytes_per_step": feed.bytes_per_batch,
