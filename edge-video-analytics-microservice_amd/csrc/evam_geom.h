@@ -260,4 +260,19 @@ inline void roi_largest_first(const int* idx, int n, const Geom* geo, int DH, bo
 
 }  // namespace evam
 
+// ROI tail split (evam_pp_run's one-unit-per-ROI plan): every ROI does the same DW x DH pixel work, so when n ROIs
+// do not divide evenly over n_cu CUs, the last n % n_cu in launch order are cut into row tiles — up to roi_tail
+// each, at most DH, and only as many as keep all units within the resident slots. Returns the tiles per split ROI
+// (1: no split) and sets nsplit to the number of ROIs split (the last nsplit of the launch order).
+inline int roi_tail_tiles(int n, int n_cu, int64_t slots, int roi_tail, int DH, int& nsplit) {
+    nsplit = 0;
+    if (n <= 0 || n_cu <= 0) return 1;
+    const int tail = n % n_cu;
+    if (roi_tail <= 1 || tail == 0 || DH < 2) return 1;
+    const int64_t fit = (slots - (int64_t)(n - tail)) / tail;
+    const int ts = (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)roi_tail, (int64_t)DH, fit}));
+    nsplit = ts > 1 ? tail : 0;
+    return ts;
+}
+
 #endif  // EVAM_GEOM_H

@@ -3928,12 +3928,8 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
                 // are those narrow, compute-dense crops). Splitting those ROIs into kn.roi_tail row tiles —
                 // as long as every unit stays resident — gives each of the CUs a fraction of an ROI instead.
                 const int n = (int)ord.size();
-                const int tail = n % h->n_cu;
-                int ts = 1;
-                if (kn.roi_tail > 1 && tail > 0 && DH >= 2)
-                    ts = (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)kn.roi_tail, (int64_t)DH,
-                                                                      (qslots[f] - (n - tail)) / tail}));
-                const int nsplit = ts > 1 ? tail : 0;
+                int nsplit = 0;
+                const int ts = roi_tail_tiles(n, h->n_cu, qslots[f], kn.roi_tail, DH, nsplit);
                 un.resize(4 * ((size_t)n + (size_t)nsplit * (ts - 1)));
                 int* u4 = un.data();
                 for (int p = 0; p < n; p++) {

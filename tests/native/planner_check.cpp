@@ -252,7 +252,37 @@ static void check_oracle_bounds() {
     printf("oracle: %d random items pre-processed on tight allocations\n", runs);
 }
 
+// ROI tail split: the C3 case, fewer ROIs than CUs, an even split, and for random sizes: the units never exceed the
+// resident slots, the split ROIs are the tail beyond a whole number per CU, and the row tiles cover [0, DH) exactly.
+static void check_roi_tail() {
+    int ns = -1;
+    CHECK(roi_tail_tiles(1600, 256, 1792, 4, 72, ns) == 4 && ns == 64, "tail split n=%d", ns);
+    CHECK(roi_tail_tiles(1536, 256, 1792, 4, 72, ns) == 1 && ns == 0, "tail split n=%d", ns);
+    CHECK(roi_tail_tiles(40, 256, 1792, 4, 72, ns) == 4 && ns == 40, "tail split n=%d", ns);
+    CHECK(roi_tail_tiles(1600, 256, 1792, 1, 72, ns) == 1 && ns == 0, "tail split n=%d", ns);
+    CHECK(roi_tail_tiles(1700, 256, 1792, 4, 72, ns) == 1 && ns == 0, "tail split n=%d", ns);  // 1536 + 164 x 2 > 1792: no room
+    CHECK(roi_tail_tiles(10, 256, 1792, 7, 3, ns) == 3 && ns == 10, "tail split n=%d", ns);      // at most DH tiles
+    for (int it = 0; it < 20000; it++) {
+        const int n_cu = uni(1, 300), per = uni(1, 8), n = uni(1, 3000);
+        const int64_t slots = (int64_t)n_cu * per;
+        const int DH = uni(1, 100), rt = uni(0, 8);
+        const int ts = roi_tail_tiles(n, n_cu, slots, rt, DH, ns);
+        CHECK(ts >= 1 && ts <= std::max(1, std::min(rt, DH)), "tail split n=%d", ns);
+        CHECK(ns == (ts > 1 ? n % n_cu : 0), "tail split n=%d", ns);
+        if (ts > 1) CHECK((int64_t)n + (int64_t)ns * (ts - 1) <= slots, "tail split n=%d", ns);
+        int covered = 0, prev = 0;
+        for (int t = 0; t < ts; t++) {
+            const int y0 = DH * t / ts, y1 = DH * (t + 1) / ts;
+            CHECK(y0 == prev && y1 > y0, "tail split n=%d", ns);
+            covered += y1 - y0;
+            prev = y1;
+        }
+        CHECK(covered == DH, "tail split n=%d", ns);
+    }
+}
+
 int main() {
+    check_roi_tail();
     check_geometry();
     check_linear_tables();
     check_footprints();
