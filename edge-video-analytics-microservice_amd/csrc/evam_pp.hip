@@ -1686,6 +1686,12 @@ __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
     asm volatile("" ::"s"(p_nw), "s"(p_TH), "s"(p_DH), "s"(p_DW), "s"(P.ox), "s"(P.rw), "s"(P.oy), "s"(P.rh),
                  "s"(P.wave_bytes), "s"(p0), "s"(p1), "s"(p2), "s"(pitch0), "s"(pitch1), "s"(pitch2), "s"(x0), "s"(y0),
                  "s"(it.index), "s"(sf.x), "s"(sf.y), "s"(P.dst), "s"(P.slot_offset), "s"(P.slot_stride));
+    // the row table's and the LUT DMA's parameters in the same batch, as opaque values the compiler cannot reload:
+    // loaded where first used, they were one or two more dependent kernel-argument round trips before the first DMA
+    double k_scale_y = P.scale_y;
+    int k_ch = P.ch, k_rgb = P.color_rgb;
+    const float* k_lut = P.lut;
+    asm volatile("" : "+s"(k_scale_y), "+s"(k_ch), "+s"(k_lut), "+s"(k_rgb));
     const int strip = (int)blockIdx.x * p_nw + wave;
     const int Y0 = ty * p_TH, Y1 = min(Y0 + p_TH, p_DH);
     const int X0 = strip * 64 * PX;
@@ -1701,9 +1707,9 @@ __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
     int lr0 = 0, lr1 = 0, lb0 = 0, lb1 = 0;
     if (lane < n) {
         int sy, b0, b1;
-        linear_coef(vr0 + lane - P.oy, P.scale_y, P.ch, false, sy, b0, b1);
-        lr0 = min(max(sy, 0), P.ch - 1);
-        lr1 = min(max(sy + 1, 0), P.ch - 1);
+        linear_coef(vr0 + lane - P.oy, k_scale_y, k_ch, false, sy, b0, b1);
+        lr0 = min(max(sy, 0), k_ch - 1);
+        lr1 = min(max(sy + 1, 0), k_ch - 1);
         lb0 = b0 << 8;
         lb1 = b1 << 8;
     }
@@ -1749,9 +1755,9 @@ __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
     const bool lut_early = nthr >= 256;
     if constexpr (OUT == 1) {
         if (lut_early && wave < 3) {
-            const __amdgpu_buffer_rsrc_t rsL = __builtin_amdgcn_make_buffer_rsrc((void*)P.lut, (short)0, 3072, 0x00020000);
+            const __amdgpu_buffer_rsrc_t rsL = __builtin_amdgcn_make_buffer_rsrc((void*)k_lut, (short)0, 3072, 0x00020000);
             __builtin_amdgcn_raw_ptr_buffer_load_lds(rsL, (__attribute__((address_space(3))) void*)(lut_s + wave * 256), 16,
-                                                     (uint32_t)lane * 16u, (P.color_rgb ? 2 - wave : wave) * 1024, 0, 0);
+                                                     (uint32_t)lane * 16u, (k_rgb ? 2 - wave : wave) * 1024, 0, 0);
         }
     }
     const int npro = min(n, D);
@@ -1801,13 +1807,13 @@ __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
     uint8_t* const d1 = d0 + plane * esz;
     uint8_t* const d2 = d1 + plane * esz;
     // output planes in source channel order (B, G, R): planes 0 and 2 exchanged for RGB
-    const __amdgpu_buffer_rsrc_t rsO0 = __builtin_amdgcn_make_buffer_rsrc((void*)(P.color_rgb ? d2 : d0), (short)0, 0x7FFFFFFF, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsO0 = __builtin_amdgcn_make_buffer_rsrc((void*)(k_rgb ? d2 : d0), (short)0, 0x7FFFFFFF, 0x00020000);
     const __amdgpu_buffer_rsrc_t rsO1 = __builtin_amdgcn_make_buffer_rsrc((void*)d1, (short)0, 0x7FFFFFFF, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rsO2 = __builtin_amdgcn_make_buffer_rsrc((void*)(P.color_rgb ? d0 : d2), (short)0, 0x7FFFFFFF, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsO2 = __builtin_amdgcn_make_buffer_rsrc((void*)(k_rgb ? d0 : d2), (short)0, 0x7FFFFFFF, 0x00020000);
     // fill in source channel order (P.fill is in output plane order)
     const uint32_t fq0 = P.fill & 0xFF, fq1 = (P.fill >> 8) & 0xFF, fq2 = (P.fill >> 16) & 0xFF;
     const uint32_t fsh = OUT == 1 ? 2 : 0;
-    const uint32_t fill0 = (P.color_rgb ? fq2 : fq0) << fsh, fill1 = fq1 << fsh, fill2 = (P.color_rgb ? fq0 : fq2) << fsh;
+    const uint32_t fill0 = (k_rgb ? fq2 : fq0) << fsh, fill1 = fq1 << fsh, fill2 = (k_rgb ? fq0 : fq2) << fsh;
 
     if constexpr (OUT == 1) {
         if (lut_early) {
@@ -1818,7 +1824,7 @@ __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
             lds_barrier();
         } else {  // workgroups of 1-3 waves (outputs narrower than 64 x PX x 3 + 1 columns)
             for (int idx = threadIdx.x; idx < 768; idx += nthr)
-                lut_s[idx] = P.lut[P.color_rgb ? 512 - (idx & ~255) + (idx & 255) : idx];
+                lut_s[idx] = k_lut[k_rgb ? 512 - (idx & ~255) + (idx & 255) : idx];
             __syncthreads();
         }
     }
@@ -2012,16 +2018,24 @@ __global__ __launch_bounds__(256) void evam_pp_band(const TParams P) {
     const int item = blockIdx.z, band = blockIdx.y;
     const ItemArg& it = P.items[item];
     const int2 sf = P.sfoot[min((int)blockIdx.x * 8 + wave, kSfoot - 1)];
-    const int p_nw = P.nw, p_ns = P.nstrips, p_TH = P.TH, p_DH = P.DH, p_DW = P.DW;
+    const int p_nw = P.nw, p_TH = P.TH, p_DH = P.DH, p_DW = P.DW;
+    int p_ns = P.nstrips, k_wb = P.wave_bytes;
     const uint8_t* p0 = it.plane[0];
     const uint8_t* p1 = it.plane[1];
     const uint8_t* p2 = it.plane[2];
     const int pitch0 = it.pitch[0], pitch1 = it.pitch[1], pitch2 = it.pitch[2];
     const int x0 = it.x0, y0 = it.y0;
-    asm volatile("" ::"s"(p_nw), "s"(p_ns), "s"(p_TH), "s"(p_DH), "s"(p_DW), "s"(P.ox), "s"(P.rw), "s"(P.oy), "s"(P.rh),
-                 "s"(P.wave_bytes), "s"(P.segY), "s"(P.segC), "s"(P.nrY), "s"(p0), "s"(p1), "s"(p2), "s"(pitch0),
-                 "s"(pitch1), "s"(pitch2), "s"(x0), "s"(y0), "s"(it.index), "s"(sf.x), "s"(sf.y), "s"(P.dst),
-                 "s"(P.slot_offset), "s"(P.slot_stride));
+    // The row table's and the LUT DMA's parameters join the batch as opaque values the compiler cannot reload
+    // (loaded where first used, they were two more dependent kernel-argument round trips before the first DMA);
+    // one statement, so every load goes out before the one wait (30 operands at most: the output's
+    // parameters, first needed at the first store, are left out).
+    double k_scale_y = P.scale_y;
+    int k_ch = P.ch, k_rgb = P.color_rgb;
+    const float* k_lut = P.lut;
+    asm volatile("" : "+s"(k_scale_y), "+s"(k_ch), "+s"(k_lut), "+s"(k_rgb), "+s"(p_ns), "+s"(k_wb)
+                 : "s"(p_nw), "s"(p_TH), "s"(p_DH), "s"(p_DW), "s"(P.ox), "s"(P.rw), "s"(P.oy), "s"(P.rh),
+                   "s"(P.segY), "s"(P.segC), "s"(P.nrY), "s"(p0), "s"(p1), "s"(p2), "s"(pitch0),
+                   "s"(pitch1), "s"(pitch2), "s"(x0), "s"(y0), "s"(it.index), "s"(sf.x), "s"(sf.y));
     const int strip = (int)blockIdx.x * p_nw + wave;
     const bool live = strip < p_ns;
     const int Y0 = band * p_TH, Y1 = min(Y0 + p_TH, p_DH);
@@ -2036,16 +2050,16 @@ __global__ __launch_bounds__(256) void evam_pp_band(const TParams P) {
     int lr0 = 0, lr1 = 0, lb0 = 0, lb1 = 0;
     if (lane < n) {
         int sy, b0, b1;
-        linear_coef(vr0 + lane - P.oy, P.scale_y, P.ch, false, sy, b0, b1);
-        lr0 = min(max(sy, 0), P.ch - 1);
-        lr1 = min(max(sy + 1, 0), P.ch - 1);
+        linear_coef(vr0 + lane - P.oy, k_scale_y, k_ch, false, sy, b0, b1);
+        lr0 = min(max(sy, 0), k_ch - 1);
+        lr1 = min(max(sy + 1, 0), k_ch - 1);
         lb0 = b0 << 8;
         lb1 = b1 << 8;
     }
     const __amdgpu_buffer_rsrc_t rsY = __builtin_amdgcn_make_buffer_rsrc((void*)p0, (short)0, 0x7FFFFFFF, 0x00020000);
     const __amdgpu_buffer_rsrc_t rsU = __builtin_amdgcn_make_buffer_rsrc((void*)p1, (short)0, 0x7FFFFFFF, 0x00020000);
     const __amdgpu_buffer_rsrc_t rsV = __builtin_amdgcn_make_buffer_rsrc((void*)(NPC == 2 ? p2 : p1), (short)0, 0x7FFFFFFF, 0x00020000);
-    uint8_t* const wbuf = smem + wave * P.wave_bytes;
+    uint8_t* const wbuf = smem + wave * k_wb;
     const int segY = P.segY, segC = P.segC;
     uint8_t* const cbuf = wbuf + P.nrY * segY;  // chroma rows; I420: V row k at + segC / 2 (segC holds U | V)
     // source rows of the band (rows are monotonic in the output row): luma [rlo, rhi], chroma [clo, chi]
@@ -2057,8 +2071,8 @@ __global__ __launch_bounds__(256) void evam_pp_band(const TParams P) {
     if constexpr (OUT == 1) {
         for (int c0 = wave * 64; c0 < 192; c0 += (int)(blockDim.x >> 6) * 64) {
             const int c = c0 + lane, sec = c >> 6;
-            const int src = ((P.color_rgb ? 2 - sec : sec) * 64 + (c & 63)) * 16;
-            const __amdgpu_buffer_rsrc_t rsL = __builtin_amdgcn_make_buffer_rsrc((void*)P.lut, (short)0, 3072, 0x00020000);
+            const int src = ((k_rgb ? 2 - sec : sec) * 64 + (c & 63)) * 16;
+            const __amdgpu_buffer_rsrc_t rsL = __builtin_amdgcn_make_buffer_rsrc((void*)k_lut, (short)0, 3072, 0x00020000);
             __builtin_amdgcn_raw_ptr_buffer_load_lds(rsL, (__attribute__((address_space(3))) void*)((uint8_t*)lut_s + c0 * 16),
                                                      16, (uint32_t)src, 0, 0, 0);
         }
@@ -2129,12 +2143,12 @@ __global__ __launch_bounds__(256) void evam_pp_band(const TParams P) {
     uint8_t* const d0 = reinterpret_cast<uint8_t*>(P.dst) + (size_t)(P.slot_offset + it.index * P.slot_stride) * 3 * plane * esz;
     uint8_t* const d1 = d0 + plane * esz;
     uint8_t* const d2 = d1 + plane * esz;
-    const __amdgpu_buffer_rsrc_t rsO0 = __builtin_amdgcn_make_buffer_rsrc((void*)(P.color_rgb ? d2 : d0), (short)0, 0x7FFFFFFF, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsO0 = __builtin_amdgcn_make_buffer_rsrc((void*)(k_rgb ? d2 : d0), (short)0, 0x7FFFFFFF, 0x00020000);
     const __amdgpu_buffer_rsrc_t rsO1 = __builtin_amdgcn_make_buffer_rsrc((void*)d1, (short)0, 0x7FFFFFFF, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rsO2 = __builtin_amdgcn_make_buffer_rsrc((void*)(P.color_rgb ? d0 : d2), (short)0, 0x7FFFFFFF, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsO2 = __builtin_amdgcn_make_buffer_rsrc((void*)(k_rgb ? d0 : d2), (short)0, 0x7FFFFFFF, 0x00020000);
     const uint32_t fq0 = P.fill & 0xFF, fq1 = (P.fill >> 8) & 0xFF, fq2 = (P.fill >> 16) & 0xFF;
     const uint32_t fsh = OUT == 1 ? 2 : 0;
-    const uint32_t fill0 = (P.color_rgb ? fq2 : fq0) << fsh, fill1 = fq1 << fsh, fill2 = (P.color_rgb ? fq0 : fq2) << fsh;
+    const uint32_t fill0 = (k_rgb ? fq2 : fq0) << fsh, fill1 = fq1 << fsh, fill2 = (k_rgb ? fq0 : fq2) << fsh;
     const uint8_t* lutb = reinterpret_cast<const uint8_t*>(lut_s);
     // one row of the strip: v[c][j] = LUT byte offsets (fp32) or bytes (u8) in source channel order; the
     // row offset in the VGPR offset (soffset 0: the store-data hazard of wide stores, see evam_pp_wave)
