@@ -62,6 +62,21 @@ WORKLOADS = {
                     "slot t%16 of a [32,16,3,224,224] clip ring", fourcc="NV12", src=(1920, 1080), frames=32,
                dst=(224, 224), dtype="f32", norm=False, mode="aspect-ratio", crop="central", ring=16),
 }
+# Format and batch variants of the configs: I420 is avdec_h264's output, i.e. the CPU
+# decodebin path of pipelines/object_detection/vehicle/pipeline.json:4; BGRx is the action-recognition
+# template's input (pipelines/action_recognition/general/pipeline.json:3, videoconvert ! BGRx) at the
+# reference run's 768x432 (charts/README.md:117-119); C1 at batch 1 is the reference run's own shape
+# (one stream, gvadetect at its default batch, pipelines/object_detection/vehicle/pipeline.json:5).
+WORKLOADS.update({
+    "c1_i420": dict(WORKLOADS["c1"], desc="C1/I420: 768x432 I420 -> 512x512 u8 BGR NCHW", fourcc="I420"),
+    "c2_i420": dict(WORKLOADS["c2"], desc="C2/I420: 32x 1920x1080 I420 -> 32x3x512x512 fp32 NCHW, range [0,1] + "
+                                          "mean/std", fourcc="I420"),
+    "c5_bgrx": dict(WORKLOADS["c5"], desc="C5/BGRx: 32 streams x 768x432 BGRx -> aspect(max) 398x224 -> central crop "
+                                          "224x224 fp32, slot t%16 of a [32,16,3,224,224] clip ring", fourcc="BGRX",
+                    src=(768, 432)),
+    "c1_b1": dict(WORKLOADS["c1"], desc="C1 batch 1: one 768x432 NV12 frame -> 1x3x512x512 u8 per launch (latency)",
+                  frames=1),
+})
 
 
 def seed_rois(n_per_frame, n_frames, W, H, seed=0):
@@ -434,6 +449,20 @@ def main():
     torch.cuda.synchronize()
     per = np.sort(np.array([a.elapsed_time(b) for a, b in evs])) if n_dist else np.zeros(1)
     pct = {q: round(float(np.percentile(per, q)), 5) for q in (10, 50, 90)}
+    # Latency of one batch on an idle device: host enqueue -> kernel done, synchronised per step (the shape a
+    # single camera stream sees; the throughput loop above keeps the device busy instead).
+    n_lat = min(args.steps, 200)
+    lat = []
+    for t in range(n_lat):
+        torch.cuda.synchronize()
+        s0 = time.perf_counter()
+        step(t)
+        torch.cuda.synchronize()
+        lat.append(time.perf_counter() - s0)
+    lat_ms = np.array(lat) * 1e3 if lat else np.zeros(1)
+    latency = {"items": n_items, "steps": n_lat,
+               "ms_p10_p50_p90": [round(float(np.percentile(lat_ms, q)), 4) for q in (10, 50, 90)],
+               "note": "host enqueue to kernel completion per launch, device idle before each"}
     # Secondary: the same launches re-reading ONE set (frames and output resident in the Infinity Cache
     # when they fit), for comparison with the pooled headline.
     resident = None
@@ -489,6 +518,7 @@ def main():
                          "algorithmic_bytes_per_launch": alg_bytes, "mean_launch_ms": round(kern_ms, 5),
                          "event_launches": args.steps - ev_from,
                          "launch_ms_p10_p50_p90": [pct[10], pct[50], pct[90]], "resident": resident},
+            "latency": latency,
         }
         valu = load_pmc_valu(args.config, n, P) if args.config in VALU_BOUND_CONFIGS else None
         if valu:

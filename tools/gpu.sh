@@ -1,0 +1,79 @@
+#!/bin/bash
+# One parameterised GPU session (replaces the per-round one-off scripts). Every GPU step runs under its own
+# time limit and the first failure ends the script.
+#
+#   tools/gpu.sh TAG STEP [STEP ...]
+#
+# Steps:
+#   test              pytest -m gpu (one process)                      -> gpurun_out/pytest_gpu_TAG.log
+#   smoke             __graft_entry__.smoke()                          -> gpurun_out/smoke_TAG.txt
+#   driver            the driver's own bench command (C2, CPU baseline) -> gpurun_out/bench_TAG_driver.json
+#   bench:c1,c2,...   one bench line per config (BENCH_STEPS, default 1000; CPU baseline unless CPU=0)
+#   prof:c1,c2,...    rocprofv3 --kernel-trace --stats per config (tools/prof_configs.sh, 200 steps)
+#   pmc:c2,c3,...     FETCH_SIZE / WRITE_SIZE passes per config (tools/pmc.sh) -> pmc_traffic_TAG_<cfg>.json
+#   valu:c1,...       SQ_INSTS_VALU pass per config (tools/pmc.sh)
+#   ab:CFG:SET1|SET2  same-box alternating env A/B (tools/gpu_env_ab.sh)
+#   dist              bench.py under torch.distributed.run, 2 ranks sharing the GPU over gloo
+#
+# Every output is stamped with EVAM_SHA (pass `EVAM_SHA=$(git rev-parse HEAD)` from the container: the box has
+# no .git) and with the sha256 of the kernel source and bench.py as they were on the box.
+set -euo pipefail
+ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
+OUT="$ROOT/gpurun_out"; mkdir -p "$OUT"
+cd "$ROOT"
+TAG="$1"; shift
+SRC_SHA=$(cat edge-video-analytics-microservice_amd/csrc/*.hip edge-video-analytics-microservice_amd/csrc/*.h | sha256sum | cut -c1-16)
+BENCH_SHA=$(sha256sum bench.py | cut -c1-16)
+echo "{\"tag\": \"$TAG\", \"git_head\": \"${EVAM_SHA:-unknown}\", \"kernel_src_sha16\": \"$SRC_SHA\", \"bench_py_sha16\": \"$BENCH_SHA\", \"date\": \"$(date -u +%FT%TZ)\"}" \
+  | tee "$OUT/stamp_$TAG.json"
+CPUARG=""; [ "${CPU:-1}" = "0" ] && CPUARG="--no-cpu-baseline"
+for st in "$@"; do
+  kind="${st%%:*}"; arg="${st#*:}"; cfgs="${arg//,/ }"
+  echo "[gpu.sh] $st"; date
+  case "$kind" in
+    test)
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
+        > "$OUT/pytest_gpu_$TAG.log" 2>&1 || { tail -40 "$OUT/pytest_gpu_$TAG.log"; exit 1; }
+      tail -1 "$OUT/pytest_gpu_$TAG.log" ;;
+    smoke)
+      timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke_$TAG.txt" 2>&1 \
+        || { tail -20 "$OUT/smoke_$TAG.txt"; exit 1; }
+      tail -1 "$OUT/smoke_$TAG.txt" ;;
+    driver)
+      timeout -k 10 240 python3 bench.py --gpus 1 --steps 20 --warmup 5 > "$OUT/bench_${TAG}_driver.json" \
+        2> "$OUT/bench_${TAG}_driver.err" || { tail -20 "$OUT/bench_${TAG}_driver.err"; exit 1; }
+      tail -1 "$OUT/bench_${TAG}_driver.json" ;;
+    bench)
+      for c in $cfgs; do
+        timeout -k 10 300 python3 bench.py --config "$c" --steps "${BENCH_STEPS:-1000}" --warmup 100 $CPUARG \
+          ${BENCH_ARGS:-} > "$OUT/bench_${TAG}_$c.json" 2> "$OUT/bench_${TAG}_$c.err" || { tail -20 "$OUT/bench_${TAG}_$c.err"; exit 1; }
+        python3 - "$OUT/bench_${TAG}_$c.json" "$c" <<'PY' | tee -a "$OUT/bench_$TAG.txt"
+import json, sys
+d = json.loads(open(sys.argv[1]).read().splitlines()[-1]); r = d["roofline"]; cb = d.get("cpu_baseline") or {}
+print(sys.argv[2], d["value"], "f/s", d["ms_per_step"], "ms/step", r["bound"], r["frac"], "hbm", r.get("hbm", {}).get("frac"),
+      "p10/50/90", r["launch_ms_p10_p50_p90"], "lat", d.get("latency", {}).get("ms_p10_p50_p90"), "cpu", cb.get("value"))
+PY
+      done ;;
+    prof)
+      STEPS=200 bash tools/prof_configs.sh "$TAG" "$cfgs" ;;
+    pmc)
+      for c in $cfgs; do
+        PMC_GROUPS="FETCH_SIZE;WRITE_SIZE" bash tools/pmc.sh "${TAG}_$c" "$c"
+        cp "$OUT/pmc_traffic.json" "$OUT/pmc_traffic_${TAG}_$c.json"
+      done ;;
+    valu)
+      for c in $cfgs; do
+        PMC_GROUPS="SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVES" bash tools/pmc.sh "${TAG}_valu_$c" "$c"
+      done ;;
+    ab)
+      c="${arg%%:*}"; sets="${arg#*:}"
+      bash tools/gpu_env_ab.sh "$TAG" "$c" "$sets" ;;
+    dist)
+      EVAM_BENCH_BACKEND=gloo timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+        --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 2 --steps 100 --warmup 20 \
+        > "$OUT/bench_dist2_$TAG.json" 2> "$OUT/bench_dist2_$TAG.err" || { tail -20 "$OUT/bench_dist2_$TAG.err"; exit 1; }
+      tail -1 "$OUT/bench_dist2_$TAG.json" ;;
+    *) echo "unknown step $st"; exit 2 ;;
+  esac
+done
+echo "[gpu.sh] done"; date
