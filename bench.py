@@ -496,7 +496,9 @@ def main():
                       + (" [host feed, PCIe-inclusive]" if feed is not None else ""),
             "value": round(value, 1),
             "unit": "frames/s",
-            "n_gpus": tot.devices,  # distinct GPUs (a gloo rehearsal may put several ranks on one)
+            # RCCL: one rank per GPU by construction (it refuses two ranks on one device); a gloo rehearsal may put
+            # several ranks on one GPU, counted once by device_key
+            "n_gpus": world if (world > 1 and backend == "nccl") else tot.devices,
             "ranks": world,
             "steps": args.steps,
             "warmup": args.warmup,

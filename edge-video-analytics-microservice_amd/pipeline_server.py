@@ -333,6 +333,15 @@ class _Request:
         self.error = None
 
 
+
+def _bind_thread_device(device: int) -> None:
+    """Make ``device`` the calling thread's current HIP device, so a model call on a runner / hub thread
+    allocates and launches on the GPU whose pipelines it serves (``devices`` option), not on GPU 0."""
+    import torch
+
+    if torch.cuda.is_available() and int(device) < torch.cuda.device_count():
+        torch.cuda.set_device(int(device))
+
 class BatchHub:
     """Per-device batching hub: one ``evam_pp_run`` (and one model call) per stage key per tick, over the
     frames / ROIs of every pipeline the device owns.
@@ -347,8 +356,10 @@ class BatchHub:
     thread blocks only on its own request, so a slow stream never holds up a tick beyond the budget.
     """
 
-    def __init__(self, device: int, max_batch: int = 64, max_wait_s: float = 0.002, target: int | None = None):
+    def __init__(self, device: int, max_batch: int = 64, max_wait_s: float = 0.002, target: int | None = None,
+                 drain_timeout_s: float = 2.0):
         self.device = int(device)
+        self.drain_timeout_s = float(drain_timeout_s)  # runner shutdown: how long held-back results may wait
         self.max_batch = max(1, int(max_batch))
         self.max_wait_s = float(max_wait_s)
         self.target = int(target) if target else None
@@ -409,6 +420,7 @@ class BatchHub:
         return None, wait
 
     def _loop(self):
+        _bind_thread_device(self.device)
         while True:
             with self._cv:
                 while True:
@@ -478,6 +490,7 @@ class DeviceRunner:
         """The runner thread. Whatever escapes the loop (a bug, not a stream's error: those fail only their
         own pipeline) fails every pipeline the runner still holds, so no ``wait()`` blocks on a dead thread."""
         try:
+            _bind_thread_device(self.hub.device)
             self._loop()
         except BaseException as e:  # noqa: BLE001
             with self._cv:
@@ -487,15 +500,35 @@ class DeviceRunner:
                 p._fail(e)
 
     def _drain(self):
-        """Hand held-back results to destinations that have room again; forget the pipelines that are done."""
+        """Hand held-back results to destinations that have room again. A pipeline whose last result (the
+        end-of-stream marker included) went out is complete: only then does its ``wait()`` return."""
         keep = []
         for p in self._draining:
             try:
                 if not p._flush_out():
                     keep.append(p)
-            except Exception:  # noqa: BLE001 — the destination itself failed: nothing left to deliver to
-                pass
+                    continue
+            except Exception as e:  # noqa: BLE001 — the destination itself failed: nothing left to deliver to
+                p.error, p.state = f"{type(e).__name__}: {e}", p.ERROR
+                p._out_backlog.clear()
+            p._done.set()
         self._draining = keep
+
+    def _drain_at_shutdown(self, timeout_s: float):
+        """Keep flushing held-back results for up to ``timeout_s``; a pipeline whose destination still cannot
+        take them ends in ERROR with the number of undelivered results (never a silent drop)."""
+        deadline = time.perf_counter() + timeout_s
+        while self._draining and time.perf_counter() < deadline:
+            self._drain()
+            if self._draining:
+                time.sleep(0.001)
+        for p in self._draining:
+            n = len(p._out_backlog)
+            p.error = f"destination full at shutdown: {n} result(s) undelivered after {timeout_s:g} s"
+            p.state = p.ERROR
+            p._out_backlog.clear()
+            p._done.set()
+        self._draining = []
 
     def _finish(self, p, e=None):
         """End pipeline ``p`` (``e``: its error), isolated from the other pipelines of the device."""
@@ -517,10 +550,11 @@ class DeviceRunner:
             with self._cv:
                 while not self._pipes and not self._draining and not self._stop:
                     self._cv.wait()
-                if self._stop and not self._pipes:
-                    self._drain()  # shutdown: what a full destination still cannot take is dropped
-                    return
+                stopping = self._stop and not self._pipes
                 pipes = list(self._pipes)
+            if stopping:
+                self._drain_at_shutdown(self.hub.drain_timeout_s)
+                return
             if self._draining:
                 self._drain()
             ready, oldest, total, done = [], None, 0, []
@@ -531,6 +565,10 @@ class DeviceRunner:
                     except Exception as e:  # noqa: BLE001
                         self._finish(p, e)
                         done.append(p)
+                        continue
+                    if len(p._out_backlog) >= p._out_limit and not p._stop.is_set():
+                        # backpressure: a destination that does not keep up stops its own stream (no ingest,
+                        # no tick), like a blocking push in a native pipeline; the other streams go on
                         continue
                 try:
                     p._ingest()
@@ -645,7 +683,7 @@ class _InferenceStage:
         self.slot = slot  # the pipeline's logical device: its BatchHub / DeviceRunner
         self.server = server
         net = el.properties.get("model") or el.properties.get("enc-model")
-        self.model = server.model_for(net)
+        self.model = server.model_for(net, device)
         if self.model is None:
             raise RuntimeError(f"{el.name or el.factory}: no model registered for {net!r} "
                                "(PipelineServer.register_model)")
@@ -841,7 +879,7 @@ class ActionRecognitionStage(_InferenceStage):
         self.ring = None
         self.t = 0
         dec = el.properties.get("dec-model")
-        self.decoder = server.model_for(dec) if dec else None
+        self.decoder = server.model_for(dec, device) if dec else None
         mp = el.properties.get("model-proc")
         self.dec_proc = json.load(open(mp)) if mp and os.path.exists(mp) else None
         if self.dec_proc:  # the decoder's model-proc carries the encoder's input_preproc too
@@ -919,6 +957,7 @@ class Pipeline:
         self._done = threading.Event()
         self._runner = False
         self._out_backlog = collections.deque()  # runner mode: results a full destination queue could not take
+        self._out_limit = 1  # held-back results at which the runner stops ingesting / running this stream
         # logical device: pipeline k of the server runs on devices[(k - 1) mod G] (streams partitioned over GPUs)
         self.slot = server.slot_for(instance_id)
         self.device = server.devices[self.slot]
@@ -962,6 +1001,8 @@ class Pipeline:
         else:
             self._runner = True
             self._batch = max([getattr(s, "batch_size", 1) for s in self.stages] + [1])
+            dst = self.destination.get("metadata", self.destination)
+            self._out_limit = max(1, self._batch, int(getattr(dst.get("output"), "maxsize", 0) or 0))
             self._pend_t0 = time.perf_counter()
             self.server.runner(self.slot).add(self)
         return self.id
@@ -1056,7 +1097,10 @@ class Pipeline:
         dst = self.destination.get("metadata", self.destination)
         if dst.get("output") is not None:
             self._put(dst["output"], None)
-        self._done.set()
+        if not self._out_backlog:
+            # otherwise complete once the device runner has handed the held-back results (and the end-of-stream
+            # marker) to the destination (DeviceRunner._drain), so wait() never returns ahead of them
+            self._done.set()
 
     def _frames(self):
         src = self.source
@@ -1193,7 +1237,8 @@ class _Server:
         self.options: dict = {}
         self.definitions: dict = {}
         self.models: dict = {}
-        self.registry: dict = {}
+        self.registry: dict = {}      # network or alias/version -> model serving every device
+        self.registry_dev: dict = {}  # (network or alias/version, device) -> model bound to that device
         self.instances: list[Pipeline] = []
         self.started = False
         self.device = 0
@@ -1217,7 +1262,8 @@ class _Server:
                 o = self.options
                 h = self._hubs[slot] = BatchHub(self.devices[slot], max_batch=int(o.get("batch_max", 64)),
                                                 max_wait_s=float(o.get("batch_wait_ms", 2.0)) / 1e3,
-                                                target=o.get("batch_target"))
+                                                target=o.get("batch_target"),
+                                                drain_timeout_s=float(o.get("drain_timeout_ms", 2000.0)) / 1e3)
             return h
 
     def runner(self, slot: int = 0) -> DeviceRunner:
@@ -1292,13 +1338,20 @@ class _Server:
             raise ValueError("; ".join(errors))
         self.started = True
 
-    def model_for(self, network):
+    def model_for(self, network, device=None):
+        """The model bound to ``network`` (a path or an ``alias/version`` key) for ``device``: a registration for
+        that device first, then a device-independent one."""
         if network is None:
             return None
-        if network in self.registry:
-            return self.registry[network]
         m = re.search(r"([^/]+)/([^/]+)/[^/]+/[^/]+\.xml$", str(network))
-        return self.registry.get(f"{m.group(1)}/{m.group(2)}") if m else None
+        keys = [network] + ([f"{m.group(1)}/{m.group(2)}"] if m else [])
+        for k in keys:
+            if device is not None and (k, int(device)) in self.registry_dev:
+                return self.registry_dev[(k, int(device))]
+        for k in keys:
+            if k in self.registry:
+                return self.registry[k]
+        return None
 
     def proc_for(self, network):
         for alias, versions in self.models.items():
@@ -1338,9 +1391,16 @@ class PipelineServer:
         return list(_SERVER.instances)
 
     @staticmethod
-    def register_model(network_or_key: str, model: InferenceModel):
-        """Bind a model to a network path or an ``alias/version`` key (replaces OpenVINO loading)."""
-        _SERVER.registry[network_or_key] = model
+    def register_model(network_or_key: str, model: InferenceModel, device: int | None = None):
+        """Bind a model to a network path or an ``alias/version`` key (replaces OpenVINO loading).
+
+        ``device``: the model serves only the pipelines placed on that logical device (option ``devices``: its
+        weights live on that GPU); register one per device. Without it the model serves every device, and its
+        ``fn`` receives each device's input tensors (it must accept any of them)."""
+        if device is None:
+            _SERVER.registry[network_or_key] = model
+        else:
+            _SERVER.registry_dev[(network_or_key, int(device))] = model
 
     @staticmethod
     def models():

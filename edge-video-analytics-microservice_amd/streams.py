@@ -35,12 +35,28 @@ def local_batch(frames_by_stream, world: int, rank: int) -> list:
 
 
 def device_key(local_device: int) -> int:
-    """Identity of a physical device across ranks: host and local device index (ranks that share a GPU in a
-    rehearsal share a key)."""
+    """Identity of a physical device across ranks (ranks that share a GPU in a rehearsal share a key): the
+    machine (``/etc/machine-id``, else the hostname — containers may share one) and the device's PCI location
+    (bus / device / domain from the HIP properties when a GPU is visible, else the local index)."""
     import socket
     import zlib
 
-    return (zlib.crc32(socket.gethostname().encode()) << 8) | (int(local_device) & 0xFF)
+    host = socket.gethostname()
+    try:
+        with open("/etc/machine-id") as f:
+            host = f.read().strip() + "/" + host
+    except OSError:
+        pass
+    loc = f"idx{int(local_device)}"
+    try:
+        import torch
+
+        if torch.cuda.is_available() and int(local_device) < torch.cuda.device_count():
+            pr = torch.cuda.get_device_properties(int(local_device))
+            loc = "pci{}:{}:{}".format(*(getattr(pr, k, -1) for k in ("pci_domain_id", "pci_bus_id", "pci_device_id")))
+    except Exception:  # noqa: BLE001 — identity only; the index is the fallback
+        pass
+    return zlib.crc32(f"{host}|{loc}".encode()) & 0x7FFFFFFFFFFF
 
 
 @dataclass

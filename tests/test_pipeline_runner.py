@@ -234,9 +234,112 @@ def test_runner_full_destination_does_not_stall_others(stubbed):
     fast = _start(ps, pre, 9, fast_q)
     assert fast.wait(30)["state"] == "COMPLETED"
     assert len(_drain(fast_q)) == 9
-    assert slow.wait(30)["state"] == "COMPLETED"
+    assert not slow._done.is_set()  # its results are still held back: not complete yet
     got = _drain(slow_q)  # the runner hands the held-back results over as the queue empties
     assert [json.loads(x)["timestamp"] for x in got] == list(range(9))
+    assert slow.wait(30)["state"] == "COMPLETED"
+
+
+def test_runner_backpressure_bounds_the_backlog(stubbed):
+    """a consumer that never reads stops its own stream (no ingest, no tick) once its held-back
+    results reach the destination's size; the backlog stays bounded while the other streams complete, and every
+    result arrives, in order, once the consumer reads."""
+    import time
+
+    ps, pre, mdir = stubbed
+    ps.PipelineServer.start({"pipeline_dir": PIPES, "model_dir": mdir, "batch_max": 8, "batch_target": 4,
+                             "batch_wait_ms": 1})
+    register(ps)
+    slow_q, fast_q = queue.Queue(maxsize=2), queue.Queue()
+    slow = _start(ps, pre, 400, slow_q)
+    fast = _start(ps, pre, 64, fast_q)
+    assert fast.wait(30)["state"] == "COMPLETED"
+    assert len(_drain(fast_q)) == 64
+    time.sleep(0.2)  # the runner keeps polling the stalled stream
+    assert slow._out_limit == 2
+    assert len(slow._out_backlog) <= slow._out_limit + 8   # at most one tick past the limit
+    assert slow.frames - 2 - len(slow._out_backlog) <= 1024  # ingested ahead: bounded by kIngest, not 400 results
+    got = _drain(slow_q)
+    assert [json.loads(x)["timestamp"] for x in got] == list(range(400))
+    assert slow.wait(30)["state"] == "COMPLETED"
+
+
+def test_runner_wait_then_stop_delivers_everything(stubbed):
+    """wait() returns only once every result and the end-of-stream marker are in the destination, so
+    stop() right after it loses nothing, even while the consumer lags behind a small queue."""
+    import threading
+    import time
+
+    ps, pre, mdir = stubbed
+    ps.PipelineServer.start({"pipeline_dir": PIPES, "model_dir": mdir, "batch_max": 8, "batch_target": 4})
+    register(ps)
+    q = queue.Queue(maxsize=3)
+    got = []
+
+    def consumer():
+        while True:
+            x = q.get(timeout=30)
+            if x is None:
+                got.append(None)
+                return
+            got.append(json.loads(x)["timestamp"])
+            time.sleep(0.002)
+
+    th = threading.Thread(target=consumer)
+    th.start()
+    p = _start(ps, pre, 40, q)
+    assert p.wait(60)["state"] == "COMPLETED"
+    ps.PipelineServer.stop()
+    th.join(30)
+    assert got == list(range(40)) + [None]
+
+
+def test_runner_shutdown_reports_undelivered_results(stubbed):
+    """at shutdown, results a destination still cannot take after drain_timeout_ms are reported (the
+    pipeline ends in ERROR with the count), never dropped silently."""
+    ps, pre, mdir = stubbed
+    ps.PipelineServer.start({"pipeline_dir": PIPES, "model_dir": mdir, "batch_max": 8, "batch_target": 4,
+                             "drain_timeout_ms": 100})
+    register(ps)
+    q = queue.Queue(maxsize=2)
+    p = _start(ps, pre, 12, q)
+    import time
+
+    t0 = time.time()
+    while len(p._out_backlog) < 1 and time.time() - t0 < 30:
+        time.sleep(0.01)
+    ps.PipelineServer.stop()
+    st = p.status()
+    assert st["state"] == "ERROR" and "undelivered" in st["message"], st
+    assert p._done.is_set()
+
+
+def test_models_bind_per_device(stubbed):
+    """with devices=[0, 1] a model registered for a device serves only the pipelines placed there; a
+    device-independent registration remains the fallback."""
+    ps, pre, mdir = stubbed
+    ps.PipelineServer.start({"pipeline_dir": PIPES, "model_dir": mdir, "devices": [0, 1], "batch_max": 8,
+                             "batch_target": 4, "batch_wait_ms": 50})
+    register(ps)  # the device-independent classifier (and a detector every device could use)
+    seen = {0: 0, 1: 0}
+
+    def det_on(dev):
+        def fn(t):
+            seen[dev] += t.shape[0]
+            return torch.full((t.shape[0], 1, 7), -1.0)
+        return ps.InferenceModel(fn, (64, 64), name="det")
+
+    for dev in (0, 1):
+        ps.PipelineServer.register_model("det_alias/det_ver", det_on(dev), device=dev)
+    outs = [queue.Queue() for _ in range(4)]
+    pipes = [_start(ps, pre, 6, q) for q in outs]
+    for p, q in zip(pipes, outs):
+        assert p.wait(30)["state"] == "COMPLETED"
+        assert len(_drain(q)) == 6
+    assert seen == {0: 12, 1: 12}
+    assert pipes[0].stages[0].model is not pipes[1].stages[0].model
+    assert pipes[0].stages[0].model is pipes[2].stages[0].model
+    assert pipes[0].stages[1].model is pipes[1].stages[1].model  # the classifier: one registration for both
 
 
 def test_runner_partitions_streams_over_devices(stubbed):

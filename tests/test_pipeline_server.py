@@ -459,7 +459,7 @@ def test_classify_reclassify_interval(ps, evam, per_call):
     class FakeServer:
         device = 0
 
-        def model_for(self, net):
+        def model_for(self, net, device=None):
             return ps.InferenceModel(None, (24, 24), {"input_preproc": []}, name="cls")
 
         def hub(self, slot=0):
