@@ -87,7 +87,12 @@ class EvamTransform(ctypes.Structure):
 
 class EvamStats(ctypes.Structure):
     _fields_ = [("src_bytes", ctypes.c_int64), ("dst_bytes", ctypes.c_int64), ("n_items", c_i32),
-                ("n_launches", c_i32), ("last_kernel_ms", ctypes.c_float)]
+                ("n_launches", c_i32), ("last_kernel_ms", ctypes.c_float), ("kernels", ctypes.c_uint32)]
+
+
+# evam_pp_stats.kernels bits (include/evam_pp.h evam_kernel_family)
+KERNEL_GENERIC, KERNEL_ROWS, KERNEL_STAGED, KERNEL_WAVE = 1, 2, 4, 8
+KERNEL_STRIP, KERNEL_BAND, KERNEL_ROI, KERNEL_ROI_STRIP, KERNEL_ROI_WAVE, KERNEL_ROI_DENSE = 16, 32, 64, 128, 256, 512
 
 
 STRUCT_SIZES = {EvamImage: 48, EvamRoi: 20, EvamPreproc: 56, EvamTensor: 32, EvamTransform: 40, EvamStats: 32}

@@ -133,7 +133,15 @@ typedef struct evam_pp_stats {
     int32_t n_items;
     int32_t n_launches;
     float last_kernel_ms;/* duration of the last run's kernel(s) from HIP events (EVAM_OPT_TIMING) */
+    uint32_t kernels;    /* kernel families the last run launched: EVAM_KERNEL_* bits (always filled)      */
 } evam_pp_stats;
+
+/* evam_pp_stats.kernels bits (diagnostics: which kernel family served a call). */
+enum evam_kernel_family {
+    EVAM_KERNEL_GENERIC = 1, EVAM_KERNEL_ROWS = 2, EVAM_KERNEL_STAGED = 4, EVAM_KERNEL_WAVE = 8,
+    EVAM_KERNEL_STRIP = 16, EVAM_KERNEL_BAND = 32, EVAM_KERNEL_ROI = 64, EVAM_KERNEL_ROI_STRIP = 128,
+    EVAM_KERNEL_ROI_WAVE = 256, EVAM_KERNEL_ROI_DENSE = 512
+};
 
 enum evam_pp_option {
     EVAM_OPT_STATS  = 1, /* compute evam_pp_stats byte accounting on every run           */

@@ -140,12 +140,15 @@ def test_roi_batch(evam, O, coracle, gpu, fmt):
     ((17, 5), "f32", "aspect-ratio", "top_left"),        # K=1, nfull=0
     ((64, 64), "f32", "aspect-ratio", "center"),         # R*DW = 256 exactly
 ])
-@pytest.mark.parametrize("roi_kernel", ["1", "0"])
+@pytest.mark.parametrize("roi_kernel", ["dense", "wave", "strip", "roi", "generic"])
 def test_roi_kernels(evam, O, coracle, gpu, fmt, dst, dtype, resize, placement, roi_kernel, monkeypatch):
-    """Per-item-geometry batches through the staged ROI kernel and (EVAM_PP_ROI=0) the generic one."""
+    """Per-item-geometry batches through the dense ROI kernel (4:2:0 default), the ROI wave kernel
+    (EVAM_PP_ROI_STRIP=3), the strip kernel's ROI mode (EVAM_PP_ROI_STRIP=2), the staged ROI kernel
+    (EVAM_PP_ROI_STRIP=0; packed formats' default) and the generic one (EVAM_PP_ROI=0)."""
     import torch
 
-    monkeypatch.setenv("EVAM_PP_ROI", roi_kernel)
+    monkeypatch.setenv("EVAM_PP_ROI", "0" if roi_kernel == "generic" else "1")
+    monkeypatch.setenv("EVAM_PP_ROI_STRIP", {"dense": "1", "wave": "3", "strip": "2"}.get(roi_kernel, "0"))
     rng = np.random.default_rng(zlib.crc32(f"{fmt}{dst}{resize}".encode()))
     W, H = 480, 270
     frames = [O.random_frame(rng, fc(O, fmt), W, H, pattern="gradient" if i else "uniform") for i in range(3)]
@@ -457,6 +460,7 @@ def test_roi_kernel_px4(evam, O, coracle, gpu, fmt, dst, dtype, monkeypatch):
     import torch
 
     monkeypatch.setenv("EVAM_PP_ROI_PX", "4")
+    monkeypatch.setenv("EVAM_PP_ROI_STRIP", "0")  # the ROI kernel (4:2:0 batches default to the strip kernel)
     rng = np.random.default_rng(zlib.crc32(f"px4{fmt}{dst}".encode()))
     W, H = 320, 200
     frames = [O.random_frame(rng, fc(O, fmt), W, H, pattern="gradient" if i else "uniform") for i in range(2)]
@@ -479,6 +483,7 @@ def test_roi_kernel_xcd_order(evam, O, coracle, gpu, fmt, monkeypatch):
     import torch
 
     monkeypatch.setenv("EVAM_PP_ROI_XCD", "1")
+    monkeypatch.setenv("EVAM_PP_ROI_STRIP", "0")  # the ROI kernel (4:2:0 batches default to the strip kernel)
     rng = np.random.default_rng(zlib.crc32(f"xcd{fmt}".encode()))
     W, H = 192, 108
     frames = [O.random_frame(rng, fc(O, fmt), W, H, pattern="gradient" if i % 2 else "uniform") for i in range(11)]
@@ -592,6 +597,7 @@ def test_roi_work_units(evam, O, coracle, gpu, unit, monkeypatch):
     import torch
 
     monkeypatch.setenv("EVAM_PP_ROI_UNIT", unit)
+    monkeypatch.setenv("EVAM_PP_ROI_STRIP", "0")  # the ROI kernel (4:2:0 batches default to the strip kernel)
     rng = np.random.default_rng(zlib.crc32(f"unit{unit}".encode()))
     W, H = 640, 360
     frames = [O.random_frame(rng, O.NV12, W, H, pattern="gradient" if i else "uniform") for i in range(2)]
@@ -614,6 +620,7 @@ def test_roi_tail_split(evam, O, coracle, gpu, tail, dst, monkeypatch):
     import torch
 
     monkeypatch.setenv("EVAM_PP_ROI_TAIL", tail)
+    monkeypatch.setenv("EVAM_PP_ROI_STRIP", "0")  # the ROI kernel (4:2:0 batches default to the strip kernel)
     rng = np.random.default_rng(zlib.crc32(f"tail{tail}{dst}".encode()))
     W, H = 640, 360
     frames = [O.random_frame(rng, O.NV12, W, H, pattern="gradient" if i else "uniform") for i in range(2)]
@@ -636,6 +643,7 @@ def test_roi_kernel_three_buffers(evam, O, coracle, gpu, fmt, buf, monkeypatch):
     import torch
 
     monkeypatch.setenv("EVAM_PP_ROI_NBUF", "3")
+    monkeypatch.setenv("EVAM_PP_ROI_STRIP", "0")  # the ROI kernel (4:2:0 batches default to the strip kernel)
     if buf != "0":
         monkeypatch.setenv("EVAM_PP_ROI_BUF", buf)
     rng = np.random.default_rng(zlib.crc32(f"nb3{fmt}{buf}".encode()))
@@ -651,3 +659,78 @@ def test_roi_kernel_three_buffers(evam, O, coracle, gpu, fmt, buf, monkeypatch):
                          rois=[evam.Roi(*r) for r in rois])
         ref, _ = run_oracle(O, coracle, frames, shape, "f32", info, rois=rois)
         assert_same(got, ref, f"roi 3 buffers {fmt} buf={buf} dst={dst}")
+
+
+@pytest.mark.parametrize("fmt", ["NV12", "I420"])
+@pytest.mark.parametrize("kernel", ["dense", "dense_ring", "wave", "wave_ring2", "strip"])
+@pytest.mark.parametrize("dst,waves,resize", [
+    ((72, 72), "4", "no-aspect-ratio"),      # C3 shape: one 128-column strip, 4 row bands of 18
+    ((72, 72), "1", "no-aspect-ratio"),      # one wave walks all 72 rows
+    ((72, 72), "8", "aspect-ratio"),         # 8 bands of 9 rows, letterbox rows / columns
+    ((48, 300), "4", "no-aspect-ratio"),     # 64-column strips (PX 1), 300 rows: two row tiles of 256 / 44
+    ((300, 70), "4", "crop"),                # three 128-column strips x 1 band, aspect + central crop
+    ((520, 33), "8", "aspect-ratio"),        # five strips x 1 band, narrow letterboxed rows
+    ((16, 40), "2", "aspect-ratio"),         # dense: one step spans 5 rows
+    ((12, 20), "4", "no-aspect-ratio"),      # dense: 7 rows per step (the deepest span a ring takes)
+])
+def test_roi_strip_mode(evam, O, coracle, gpu, fmt, kernel, dst, waves, resize, monkeypatch):
+    """The ROI wave kernel (packed rings of any depth; wave_ring2: rings of the fewest bytes, two entries of the
+    widest footprint, so wide crops run 2-deep and narrow ones deeper) and the strip kernel's ROI mode
+    (EVAM_PP_ROI_STRIP=2), both resolving per-item geometry on the device from each RoiRec: every wave layout
+    (strips x row bands, EVAM_PP_ROI_STRIP_WAVES), row tiles for outputs taller than the bands hold, crops whose
+    footprints need 1 KB segments (up to ~900 px wide) next to tiny and partially outside ones, and every resize
+    mode; u8 and fp32 against the oracle."""
+    import torch
+
+    monkeypatch.setenv("EVAM_PP_ROI_STRIP_WAVES", waves)
+    monkeypatch.setenv("EVAM_PP_ROI_STRIP", {"strip": "2", "wave": "3", "wave_ring2": "3"}.get(kernel, "1"))
+    if kernel in ("wave_ring2", "dense_ring"):
+        monkeypatch.setenv("EVAM_PP_ROI_RING", "16")  # the fewest bytes: the widest footprint runs the shallowest ring
+    rng = np.random.default_rng(zlib.crc32(f"rs{fmt}{dst}{waves}{resize}".encode()))
+    W, H = 1280, 720
+    frames = [O.random_frame(rng, fc(O, fmt), W, H, pattern="gradient" if i else "uniform") for i in range(3)]
+    rois = []
+    for k in range(45):
+        si = k % 3
+        w, h = int(rng.integers(2, 900 if k % 5 == 0 else 300)), int(rng.integers(2, 600 if k % 7 == 0 else 200))
+        x, y = int(rng.integers(-40, W - 2)), int(rng.integers(-40, H - 2))
+        rois.append((si, x, y, max(w, 2 - x), max(h, 2 - y)))
+    rois += [(0, 0, 0, W, H), (1, W - 2, H - 2, 9, 9), (2, 101, 51, 1, 1), (0, 10, 20, 0, 0)]  # w=0: the full frame
+    kw = {"resize": "aspect-ratio", "crop": "central"} if resize == "crop" else {"resize": resize}
+    for dtype in ("u8", "f32"):
+        info = evam.PreProcInfo(placement="center", fill=(9, 99, 199), color_space="RGB", **kw,
+                                **({"range": (0.0, 1.0), "mean": (0.1, 0.2, 0.3), "std": (0.3, 0.2, 0.1)}
+                                   if dtype == "f32" else {}))
+        shape = (len(rois), 3, dst[1], dst[0])
+        tdt = torch.float32 if dtype == "f32" else torch.uint8
+        got, _ = run_hip(evam, torch, upload(evam, frames, gpu), shape, tdt, info, rois=[evam.Roi(*r) for r in rois])
+        ref, _ = run_oracle(O, coracle, frames, shape, dtype, info, rois=rois)
+        assert_same(got, ref, f"roi strip {fmt} {dst} waves={waves} {resize} {dtype}")
+
+
+def test_roi_strip_mode_selected(evam, O, gpu, monkeypatch):
+    """4:2:0 ROI batches run on the strip kernel's ROI mode (one launch); packed formats keep the ROI kernel, and
+    EVAM_PP_ROI_STRIP=0 restores it for 4:2:0. Checked through the kernel families the library reports for the call
+    (evam_pp_stats.kernels)."""
+    import torch
+
+    N = evam.native
+    rng = np.random.default_rng(4)
+    rois = [evam.Roi(i % 2, 10 * i, 5 * i, 50 + i, 40 + 2 * i) for i in range(8)]
+    for fmt, want in (("NV12", N.KERNEL_ROI_DENSE), ("I420", N.KERNEL_ROI_DENSE), ("BGRX", N.KERNEL_ROI)):
+        frames = [O.random_frame(rng, fc(O, fmt), 320, 240) for _ in range(2)]
+        out = torch.zeros((8, 3, 72, 72), dtype=torch.float32, device=gpu)
+        pp = evam.HipPreProcessor(device=0)
+        pp.convert(upload(evam, frames, gpu), out, evam.PreProcInfo(range=(0.0, 1.0)), rois=rois)
+        torch.cuda.synchronize()
+        st = pp.stats()
+        assert st.n_launches == 1 and st.kernels == want, (fmt, st.kernels)
+        pp.close()
+    for knob, want in (("3", N.KERNEL_ROI_WAVE), ("2", N.KERNEL_ROI_STRIP), ("0", N.KERNEL_ROI)):
+        monkeypatch.setenv("EVAM_PP_ROI_STRIP", knob)
+        pp = evam.HipPreProcessor(device=0)
+        out = torch.zeros((8, 3, 72, 72), dtype=torch.float32, device=gpu)
+        pp.convert(upload(evam, [O.random_frame(rng, O.NV12, 320, 240)] * 2, gpu), out, None, rois=rois)
+        torch.cuda.synchronize()
+        assert pp.stats().kernels == want, (knob, pp.stats().kernels)
+        pp.close()

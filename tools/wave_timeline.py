@@ -26,7 +26,7 @@ SLOTS = 12  # kTraceSlots of the trace build
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c4", "c5"])
+    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c4", "c5"])
     ap.add_argument("--steps", type=int, default=40)
     a = ap.parse_args()
     if "trace" not in os.environ.get("EVAM_PP_LIB", ""):
@@ -44,7 +44,13 @@ def main():
     DW, DH = wl["dst"]
     sets = [evam.ImageBatch(bench.device_frames(evam, torch, wl, n, dev, seed=1234 + 7919 * k)) for k in range(5)]
     dt = torch.float32 if wl["dtype"] == "f32" else torch.uint8
-    outs = [torch.empty((n * (ring or 1), 3, DH, DW), dtype=dt, device=dev) for _ in range(1 if ring else 5)]
+    rois = None
+    if wl.get("rois"):  # C3: the strip kernel's ROI mode (one workgroup of 4 waves per ROI)
+        import numpy as onp
+        rois = [evam.RoiBatch(onp.array(bench.seed_rois(wl["rois"], n, *wl["src"], seed=k), dtype=onp.int32))
+                for k in range(4)]
+    nout = len(rois[0]) if rois else n * (ring or 1)
+    outs = [torch.empty((nout, 3, DH, DW), dtype=dt, device=dev) for _ in range(1 if ring else 5)]
     pp = evam.HipPreProcessor(device=0)
     lib = evam.native.load_library()
     lib.evam_pp_debug_trace.argtypes = [ctypes.c_void_p, ctypes.c_int]
@@ -55,7 +61,7 @@ def main():
         if ring:
             pp.convert(sets[t % 5], outs[0], info, slot_offset=t % ring, slot_stride=ring)
         else:
-            pp.convert(sets[t % 5], outs[t % 5], info)
+            pp.convert(sets[t % 5], outs[t % 5], info, rois=rois[t % 4] if rois else None)
     torch.cuda.synchronize()
     cap = 16384
     buf = (ctypes.c_ulonglong * (SLOTS * cap))()
