@@ -288,6 +288,8 @@ def main():
     ap.add_argument("--feed", choices=["device", "host"], default="device",
                     help="host: frames start in pinned host memory and cross PCIe every step (SURVEY §8 f3); "
                          "reported as a separate PCIe-inclusive line, never the headline value")
+    ap.add_argument("--feed-rows", choices=["touched", "all"], default="touched",
+                    help="--feed host: copy only the source rows the resize reads (default) or whole frames")
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU-baseline work")
     ap.add_argument("--pool", type=int, default=0,
                     help="frame/output sets cycled step by step (0: auto, >= 3x the 256 MiB Infinity Cache; "
@@ -302,6 +304,9 @@ def main():
     ap.add_argument("--frames-per-stream", type=int, default=16384, help="--via pipeline: frames per stream")
     ap.add_argument("--stream-batch", type=int, default=16, help="--via pipeline: gvadetect batch-size per stream")
     ap.add_argument("--hub-batch", type=int, default=256, help="--via pipeline: max frames per hub launch")
+    ap.add_argument("--inflight", type=int, default=1,
+                    help="launches in flight: step t runs on handle/stream t mod N (independent outputs), so launch "
+                         "t+1's ramp overlaps launch t's tail; reported as its own line, timed by wall clock")
     ap.add_argument("--runner", choices=["device", "threads"], default="device",
                     help="--via pipeline: one runner thread per device (default) or one thread per pipeline")
     args = ap.parse_args()
@@ -373,7 +378,12 @@ def main():
     n_out = 1 if ring else P
     outs = [torch.empty((out_n, 3, DH, DW), dtype=dtype, device=device) for _ in range(n_out)]
     pool_bytes = P * in_bytes + n_out * out_n * 3 * DH * DW * esz
-    pp = evam.HipPreProcessor(device=local)
+    if args.inflight > 1:  # one handle per stream; the streams run side by side
+        inflight_streams = [torch.cuda.Stream(device) for _ in range(args.inflight)]
+        pps = [evam.HipPreProcessor(device=local, stream=st) for st in inflight_streams]
+    else:
+        pps = [evam.HipPreProcessor(device=local)]
+    pp = pps[0]
 
     feed = None
     if args.feed == "host":
@@ -381,14 +391,18 @@ def main():
             raise SystemExit("--feed host is wired for full-frame batches (c1, c2, c4)")
         feed = evam.feed.HostFeed(evam.preproc.FOURCC_BY_NAME[wl["fourcc"]], *wl["src"], batch=n, depth=3,
                                   device=local)
+        if args.feed_rows == "touched":  # only the source rows the resize reads cross PCIe
+            feed.set_geometry(DW, DH, info)
         frng = np.random.default_rng(1234 + rank)
         for hb in feed.host:   # stands in for a decoder writing into the pinned ring
             hb.numpy()[:] = frng.integers(0, 256, hb.numel(), dtype=np.uint8)
 
-    def step(t, k=None):
-        """One launch; k = pool set (default: set t mod P, so consecutive steps touch different sets)."""
+    def step(t, k=None, inflight=False):
+        """One launch; k = pool set (default: set t mod P, so consecutive steps touch different sets).
+        inflight: on handle t mod --inflight (its own stream)."""
         k = t % P if k is None else k
         out = outs[k % n_out]
+        pp = pps[t % len(pps)] if inflight else pps[0]
         if feed is not None:
             j = feed.acquire()
             feed.submit(j)
@@ -411,9 +425,10 @@ def main():
     alg_bytes = int(round(sum(acc) / len(acc)))  # mean over the ROI sets a run cycles through
     pp.set_option(evam.native.OPT_STATS, 0)
 
+    inflight = len(pps) > 1
     for t in range(args.warmup):
-        step(t)
-    stream = torch.cuda.current_stream(device)
+        step(t, inflight=inflight)
+    stream = inflight_streams[0] if inflight else torch.cuda.current_stream(device)  # where pps[0] launches
     e0 = torch.cuda.Event(enable_timing=True)
     e1 = torch.cuda.Event(enable_timing=True)
     if world > 1:
@@ -428,7 +443,7 @@ def main():
     if ev_from == 0:
         e0.record(stream)
     for t in range(args.steps):
-        step(t)
+        step(t, inflight=inflight)
         if t == 0 and ev_from == 1:
             e0.record(stream)
     t_submit = time.perf_counter() - t0  # host time to enqueue the K steps (≈ wall when host-bound)
@@ -438,6 +453,8 @@ def main():
         dist.barrier()
     wall = time.perf_counter() - t0
     kern_ms = e0.elapsed_time(e1) / (args.steps - ev_from)  # one launch per step
+    if inflight:  # launches overlap on several streams: the launch rate is the wall-clock step
+        kern_ms = wall / args.steps * 1e3
     # Per-launch spread (median, p10 / p90), measured after the timed region: one event
     # pair around each of up to 200 extra steps, so the timed loop above carries no per-step events.
     n_dist = min(args.steps, 200)
@@ -493,7 +510,8 @@ def main():
     if rank == 0:
         res = {
             "metric": (METRIC if args.config == "c2" else f"{METRIC} [{args.config}]")
-                      + (" [host feed, PCIe-inclusive]" if feed is not None else ""),
+                      + (" [host feed, PCIe-inclusive]" if feed is not None else "")
+                      + (f" [inflight {len(pps)}]" if inflight else ""),
             "value": round(value, 1),
             "unit": "frames/s",
             # RCCL: one rank per GPU by construction (it refuses two ranks on one device); a gloo rehearsal may put
@@ -519,6 +537,8 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "algorithmic_bytes_per_launch": alg_bytes, "mean_launch_ms": round(kern_ms, 5),
                          "event_launches": args.steps - ev_from,
+                         "timing": ("wall clock over the timed steps (launches in flight on several streams)"
+                                    if inflight else "HIP events on the launch stream"),
                          "launch_ms_p10_p50_p90": [pct[10], pct[50], pct[90]], "resident": resident},
             "latency": latency,
         }
@@ -535,16 +555,19 @@ def main():
                                **{k: r[k] for k in ("algorithmic_bytes_per_launch", "mean_launch_ms", "event_launches",
                                                     "launch_ms_p10_p50_p90", "resident")}}
         if feed is not None:
-            res["h2d"] = {"bytes_per_step": feed.bytes_per_batch,
+            res["h2d"] = {"bytes_per_step": feed.bytes_per_batch, "frame_bytes": feed.frame_bytes,
+                          "rows": args.feed_rows,
                           "GBps": round(feed.bytes_per_batch * args.steps / wall_max / 1e9, 2),
                           "note": "frames copied from pinned host memory every step on a copy stream, overlapped "
-                                  "with the kernel (depth-3 ring); roofline.mean_launch_ms includes copy waits"}
+                                  "with the kernel (depth-3 ring; rows=touched: only the source rows the resize "
+                                  "reads, strided 2-D copies); roofline.mean_launch_ms includes copy waits"}
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(wl, args.cpu_budget)
         else:
             res["cpu_baseline"] = None
         print(json.dumps(res), flush=True)
-    pp.close()
+    for h in pps:
+        h.close()
     if world > 1:
         dist.destroy_process_group()
 

@@ -1008,7 +1008,6 @@ __global__ __launch_bounds__(kThreads) void evam_pp_staged(const SParams P) {
             const uint8_t* sc0 = buf + (2 * R + 2 * r) * SLOT;
             const uint32_t lY0j = lY0[j], lY1j = lY1[j], lC0j = lC0[j], lC1j = lC1[j], wpj = wp[j];
             uint32_t v[3];
-#ifndef EVAM_PP_NO_SAT
             if constexpr (kYUV) {
                 const int ya = y0 + lr.R0(Y - Y0), yb = y0 + lr.R1(Y - Y0);
                 const bool share = (ya >> 1) == (yb >> 1);
@@ -1048,32 +1047,9 @@ __global__ __launch_bounds__(kThreads) void evam_pp_staged(const SParams P) {
                 put(v);
                 continue;
             }
-#endif
             const uint32_t a0 = wa[j] & 0xFFFF, a1 = wa[j] >> 16;  // 15-bit
             int c[4][3];
-            if constexpr (kYUV) {
-                const int ya = y0 + lr.R0(Y - Y0), yb = y0 + lr.R1(Y - Y0);
-                const bool share = (ya >> 1) == (yb >> 1);
-                const uint8_t* sc1 = share ? sc0 : sc0 + SLOT;
-                Chroma<FMT> cA, cB, cC, cD;
-                if constexpr (FMT == kNV12) {
-                    cA.u = *reinterpret_cast<const uint16_t*>(sc0 + lC0j);
-                    cB.u = *reinterpret_cast<const uint16_t*>(sc0 + lC1j);
-                    cC.u = *reinterpret_cast<const uint16_t*>(sc1 + lC0j);
-                    cD.u = *reinterpret_cast<const uint16_t*>(sc1 + lC1j);
-                } else {
-                    const uint8_t* sv0 = sc0 + 2 * R * SLOT;
-                    const uint8_t* sv1 = sc1 + 2 * R * SLOT;
-                    cA.u = sc0[lC0j]; cA.v = sv0[lC0j];
-                    cB.u = sc0[lC1j]; cB.v = sv0[lC1j];
-                    cC.u = sc1[lC0j]; cC.v = sv1[lC0j];
-                    cD.u = sc1[lC1j]; cD.v = sv1[lC1j];
-                }
-                y_plus_uv((int)sy0[lY0j], chroma_terms<FMT>(cA), c[0][0], c[0][1], c[0][2]);
-                y_plus_uv((int)sy0[lY1j], chroma_terms<FMT>(cB), c[1][0], c[1][1], c[1][2]);
-                y_plus_uv((int)sy1[lY0j], chroma_terms<FMT>(cC), c[2][0], c[2][1], c[2][2]);
-                y_plus_uv((int)sy1[lY1j], chroma_terms<FMT>(cD), c[3][0], c[3][1], c[3][2]);
-            } else {
+            {  // packed sources (BGRx / BGR)
                 const uint8_t* rowp[2] = {sy0, sy1};
 #pragma unroll
                 for (int q = 0; q < 4; q++) {
@@ -1381,27 +1357,12 @@ __global__ __launch_bounds__(kThreads) void evam_pp_wave(const WParams P) {
         for (int j = 0; j < PX; j++) {
             const uint32_t tY0 = lY[j] & 0xFFFF, tY1 = lY[j] >> 16;
             int c0[3], c1[3];
-#ifndef EVAM_PP_NO_SAT
             if constexpr (kYUV) {
                 const uint32_t tC0 = lC[j] & 0xFFFF, tC1 = lC[j] >> 16;
                 const uint8_t* svv = FMT == kNV12 ? sc + 1 : sv;
                 hrow_sat(sy[tY0], sy[tY1], uv_terms_sat(sc[tC0], svv[tC0]), uv_terms_sat(sc[tC1], svv[tC1]),
                          (wa[j] >> 4) & 0x0FFF0FFFu, H[j]);
                 continue;
-            }
-#endif
-            if constexpr (kYUV) {
-                const uint32_t tC0 = lC[j] & 0xFFFF, tC1 = lC[j] >> 16;
-                Chroma<FMT> cA, cB;
-                if constexpr (FMT == kNV12) {
-                    cA.u = *reinterpret_cast<const uint16_t*>(sc + tC0);
-                    cB.u = *reinterpret_cast<const uint16_t*>(sc + tC1);
-                } else {
-                    cA.u = sc[tC0]; cA.v = sv[tC0];
-                    cB.u = sc[tC1]; cB.v = sv[tC1];
-                }
-                y_plus_uv((int)sy[tY0], chroma_terms<FMT>(cA), c0[0], c0[1], c0[2]);
-                y_plus_uv((int)sy[tY1], chroma_terms<FMT>(cB), c1[0], c1[1], c1[2]);
             } else if constexpr (FMT == kBGRX) {
                 const uint32_t q0 = *reinterpret_cast<const uint32_t*>(sy + tY0);
                 const uint32_t q1 = *reinterpret_cast<const uint32_t*>(sy + tY1);
@@ -1422,35 +1383,11 @@ __global__ __launch_bounds__(kThreads) void evam_pp_wave(const WParams P) {
         for (int j = 0; j < PX; j++) {
             const uint32_t tY0 = lY[j] & 0xFFFF, tY1 = lY[j] >> 16;
             const uint32_t tC0 = lC[j] & 0xFFFF, tC1 = lC[j] >> 16;
-#ifndef EVAM_PP_NO_SAT
-            {
-                const uint8_t* svv = FMT == kNV12 ? sc + 1 : sv;
-                const UVs sA = uv_terms_sat(sc[tC0], svv[tC0]), sB = uv_terms_sat(sc[tC1], svv[tC1]);
-                const uint32_t wp = (wa[j] >> 4) & 0x0FFF0FFFu;
-                hrow_sat(sya[tY0], sya[tY1], sA, sB, wp, HA[j]);
-                hrow_sat(syb[tY0], syb[tY1], sA, sB, wp, HB[j]);
-                continue;
-            }
-#endif
-            Chroma<FMT> cA, cB;
-            if constexpr (FMT == kNV12) {
-                cA.u = *reinterpret_cast<const uint16_t*>(sc + tC0);
-                cB.u = *reinterpret_cast<const uint16_t*>(sc + tC1);
-            } else {
-                cA.u = sc[tC0]; cA.v = sv[tC0];
-                cB.u = sc[tC1]; cB.v = sv[tC1];
-            }
-            const UV3 tA = chroma_terms<FMT>(cA), tB = chroma_terms<FMT>(cB);
-            const uint32_t a0 = wa[j] & 0xFFFF, a1 = wa[j] >> 16;
-            int c0[3], c1[3];
-            y_plus_uv((int)sya[tY0], tA, c0[0], c0[1], c0[2]);
-            y_plus_uv((int)sya[tY1], tB, c1[0], c1[1], c1[2]);
-#pragma unroll
-            for (int ch = 0; ch < 3; ch++) HA[j][ch] = __umul24(c0[ch], a0) + __umul24(c1[ch], a1);
-            y_plus_uv((int)syb[tY0], tA, c0[0], c0[1], c0[2]);
-            y_plus_uv((int)syb[tY1], tB, c1[0], c1[1], c1[2]);
-#pragma unroll
-            for (int ch = 0; ch < 3; ch++) HB[j][ch] = __umul24(c0[ch], a0) + __umul24(c1[ch], a1);
+            const uint8_t* svv = FMT == kNV12 ? sc + 1 : sv;
+            const UVs sA = uv_terms_sat(sc[tC0], svv[tC0]), sB = uv_terms_sat(sc[tC1], svv[tC1]);
+            const uint32_t wp = (wa[j] >> 4) & 0x0FFF0FFFu;
+            hrow_sat(sya[tY0], sya[tY1], sA, sB, wp, HA[j]);
+            hrow_sat(syb[tY0], syb[tY1], sA, sB, wp, HB[j]);
         }
     };
 
@@ -2087,6 +2024,7 @@ struct WRParams {
     int ring_bytes;          // one wave's LDS ring (a multiple of 16)
     int color_rgb;
     uint32_t fill;
+    int rt_rows;             // dense kernel: rows of one wave's row table (the most rows of a band, <= 64)
 };
 constexpr int kRingMax = 8;  // most ring entries (rows of DMA in flight) of one wave
 
@@ -2463,6 +2401,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_num_sgpr(96))) void evam
     const uint8_t* p2 = reinterpret_cast<const uint8_t*>(((uint64_t)rec[5] << 32) | rec[4]);
     const int pitch0 = (int)rec[6], pitch1 = (int)rec[7], pitch2 = (int)rec[8];
     const int index = (int)rec[14];
+    EVAM_WSTAMP(7);  // the record arrived
     Geom g;
     roi_geometry(FMT, (int)(rec[9] & 0xFFFF), (int)(rec[9] >> 16), true, (int)rec[10], (int)rec[11], (int)rec[12],
                  (int)rec[13], mode, placement, DW, DH, g);  // never empty: the host validated every item
@@ -2472,6 +2411,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_num_sgpr(96))) void evam
     const int ox = __builtin_amdgcn_readfirstlane(g.ox), oy = __builtin_amdgcn_readfirstlane(g.oy);
     const double scx = 1. / ((double)rw / cw), scy = 1. / ((double)rh / ch);
     const int row0 = (int)(rec[15] & 0xFFFF), row1 = (int)(rec[15] >> 16);
+#ifdef EVAM_PP_TRACE
+    asm volatile("" ::"v"(scx), "v"(scy));
+    EVAM_WSTAMP(8);  // geometry and scales
+#endif
     const int th = (row1 - row0 + nbw - 1) / nbw;
     const int Y0 = min(row0 + wave * th, row1), Y1 = min(Y0 + th, row1), rows = Y1 - Y0;  // rows <= 64 (host)
     // footprint of the visible columns (crop-relative taps of the first and last)
@@ -2500,12 +2443,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_num_sgpr(96))) void evam
     const int span = (63 + DW - 1) / DW + 1;  // rows one step reads (the host sizes the ring for them)
     while (Dr > span && (Dr - 1) * (niY + NPC * niC) + 3 * ((Dr * DW + 63) / 64 + 1) > 63) Dr--;
     Dr = max(Dr, 1);
-    // LDS carve: [colTab DW x 8 B][rowTab 64 x 16 B per wave][ring RB per wave]
+    // LDS carve: [colTab DW x 8 B][rowTab rt_rows x 16 B per wave][ring RB per wave]
     uint2* const colTab = reinterpret_cast<uint2*>(smem);
     const int ctb = (DW * 8 + 15) & ~15;
-    const int nw = nbw;
-    uint4* const rowTab = reinterpret_cast<uint4*>(smem + ctb) + wave * 64;
-    uint8_t* const wbuf = smem + ctb + nw * 64 * 16 + wave * RB;
+    const int nw = nbw, rtr = P.rt_rows;
+    uint4* const rowTab = reinterpret_cast<uint4*>(smem + ctb) + wave * rtr;
+    uint8_t* const wbuf = smem + ctb + nw * rtr * 16 + wave * RB;
     // band row table, one row per lane: weights, ring entry, second chroma segment, fill flag; and the source rows
     // (crop-relative) for the DMA
     int lr0 = 0, lr1 = 0;
@@ -2522,6 +2465,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_num_sgpr(96))) void evam
         }
         rowTab[lane] = e;
     }
+#ifdef EVAM_PP_TRACE
+    asm volatile("" ::"v"(lr0), "v"(lr1));
+    EVAM_WSTAMP(9);  // footprint and row table
+#endif
     // per-lane DMA source columns of the luma / chroma chunks: chunk q = lane + 64 b -> (tap, chunk c)
     uint32_t dY[2], dC[2];
     bool tY[2], tC[2], vY[2], vC[2];
@@ -3322,7 +3269,6 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(96))) void
                 const uint32_t a0 = wa[k][j] & 0xFFFF, a1 = wa[k][j] >> 16;
                 const uint32_t tY0 = lY[k][j] & 0xFFFF, tY1 = lY[k][j] >> 16;
                 int c[4][3];
-#ifndef EVAM_PP_NO_SAT
                 if constexpr (kYUV) {
                     const uint32_t tC0 = lC[k][j] & 0xFFFF, tC1 = lC[k][j] >> 16;
                     const uint8_t* sv0 = FMT == kNV12 ? sc0 + 1 : sc0 + 2 * R * segC;
@@ -3335,28 +3281,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(96))) void
                     for (int ch3 = 0; ch3 < 3; ch3++) v[ch3][j] = vfinal<OUT>(H0[ch3], H1[ch3], wb0, wb1);
                     continue;
                 }
-#endif
-                if constexpr (kYUV) {
-                    const uint32_t tC0 = lC[k][j] & 0xFFFF, tC1 = lC[k][j] >> 16;
-                    Chroma<FMT> cA, cB, cC, cD;
-                    if constexpr (FMT == kNV12) {
-                        cA.u = *reinterpret_cast<const uint16_t*>(sc0 + tC0);
-                        cB.u = *reinterpret_cast<const uint16_t*>(sc0 + tC1);
-                        cC.u = *reinterpret_cast<const uint16_t*>(sc1 + tC0);
-                        cD.u = *reinterpret_cast<const uint16_t*>(sc1 + tC1);
-                    } else {
-                        const uint8_t* sv0 = sc0 + 2 * R * segC;
-                        const uint8_t* sv1 = sc1 + 2 * R * segC;
-                        cA.u = sc0[tC0]; cA.v = sv0[tC0];
-                        cB.u = sc0[tC1]; cB.v = sv0[tC1];
-                        cC.u = sc1[tC0]; cC.v = sv1[tC0];
-                        cD.u = sc1[tC1]; cD.v = sv1[tC1];
-                    }
-                    y_plus_uv((int)sy0[tY0], chroma_terms<FMT>(cA), c[0][0], c[0][1], c[0][2]);
-                    y_plus_uv((int)sy0[tY1], chroma_terms<FMT>(cB), c[1][0], c[1][1], c[1][2]);
-                    y_plus_uv((int)sy1[tY0], chroma_terms<FMT>(cC), c[2][0], c[2][1], c[2][2]);
-                    y_plus_uv((int)sy1[tY1], chroma_terms<FMT>(cD), c[3][0], c[3][1], c[3][2]);
-                } else {
+                {  // packed sources (BGRx / BGR)
                     const uint8_t* tap[4] = {sy0 + tY0, sy0 + tY1, sy1 + tY0, sy1 + tY1};
 #pragma unroll
                     for (int q = 0; q < 4; q++) {
@@ -4078,6 +4003,7 @@ hipError_t launch_roiw(int f, int out, int px, const WRParams& p, int grid, int 
 struct RoiStripPlan {
     int px, slot, nstrips, nbw, nw, lds, tiles;  // tiles: row tiles (units) per ROI
     int unit_rows;                               // output rows of one unit (the last may be shorter)
+    int rt_rows;                                 // dense kernel: row-table rows per wave
     int wave_kernel;                             // 2: evam_pp_roid (dense), 1: evam_pp_roiw, 0: the strip kernel's ROI mode
     int ring_bytes;                              // evam_pp_roiw: one wave's ring
 };
@@ -4121,17 +4047,18 @@ bool plan_roi_strip(int f, int DW, int DH, int out_dtype, int max_cw, int max_ch
     // ceil(63 / DW) + 1 rows; plus one in flight) of the widest footprint; the rest of the budget lets narrow crops run
     // deeper rings. Budget: the LDS of a CU shared by the workgroups one round needs (C3: 1,600 ROIs -> 7 per CU).
     if (chunks > 64) return false;  // a tap segment over 1 KB: two DMA instructions per plane at most
-    const int step_rows = r.wave_kernel == 2 ? (63 + DW - 1) / DW + 1 : 1;
+    const int step_rows = r.wave_kernel == 2 ? (63 + DW - 1) / DW + 1 : 2;
     if (step_rows + 1 > kRingMax) return false;  // DW < 10: 64 pixels span more rows than a ring holds
     const int emax = 16 * (2 * chunks + 2 * npc * chunks);
-    const int fixed = r.wave_kernel == 2 ? ((DW * 8 + 15) & ~15) + r.nw * 64 * 16 : 0;  // colTab + rowTabs
+    r.rt_rows = (r.unit_rows + r.nbw - 1) / r.nbw;  // the most rows of one wave's band
+    const int fixed = r.wave_kernel == 2 ? ((DW * 8 + 15) & ~15) + r.nw * r.rt_rows * 16 : 0;  // colTab + rowTabs
     const int64_t units = (int64_t)count * r.tiles;
     const int per_cu = (int)std::max<int64_t>(1, std::min<int64_t>(8, (units + n_cu - 1) / n_cu));
     // LDS is allocated in 1 KB granules per workgroup (static LUT included)
     int rb = ((((160 * 1024) / per_cu) & ~1023) - lut_static - 16 - fixed) / r.nw & ~15;
     if (kn.roi_ring > 0) rb = kn.roi_ring & ~15;
     rb = std::min(rb, 8 * 1024);
-    const int rmin = (step_rows + 1) * emax;
+    const int rmin = step_rows * emax;  // the rows one step reads, of the widest footprint
     r.ring_bytes = std::max(rb, rmin);
     r.lds = fixed + r.nw * r.ring_bytes + 16;  // + 16: a right-edge tap reads past its footprint (weight 0)
     if (r.lds + lut_static > 160 * 1024) return false;
@@ -4965,6 +4892,7 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
             w.nstrips = r.nstrips;
             w.nbw = r.nbw;
             w.ring_bytes = r.ring_bytes;
+            w.rt_rows = r.rt_rows;
             w.color_rgb = color_rgb;
             w.fill = fill;
             hipError_t e = r.wave_kernel == 2 ? launch_roid(f, cfg->out_dtype, w, qrec[f], r.nw, r.lds, h->stream)

@@ -45,3 +45,41 @@ def test_feed_rejects_oversize_batch(evam, O, gpu):
     feed = evam.feed.HostFeed("NV12", 64, 48, batch=1, depth=2)
     with pytest.raises(ValueError):
         feed.fill(feed.acquire(), [O.random_frame(np.random.default_rng(0), O.NV12, 64, 48)] * 2)
+
+
+@pytest.mark.parametrize("fmt,resize,src,dst", [("NV12", "aspect-ratio", (384, 216), (64, 64)),
+                                                ("I420", "no-aspect-ratio", (200, 120), (40, 20)),
+                                                ("NV12", "crop", (320, 180), (48, 48)),
+                                                ("BGRX", "no-aspect-ratio", (120, 96), (30, 24))])
+def test_feed_touched_rows_only(evam, O, coracle, gpu, fmt, resize, src, dst):
+    """set_geometry: only the rows the resize reads cross PCIe (strided 2-D copies); the device slots start
+    poisoned (0xA5), so a kernel reading any row the plan skipped would break parity with the oracle."""
+    import torch
+
+    fc = {"NV12": O.NV12, "I420": O.I420, "BGRX": O.BGRX}[fmt]
+    (W, H), (DW, DH), B = src, dst, 2
+    kw = {"resize": "aspect-ratio", "crop": "central"} if resize == "crop" else {"resize": resize}
+    info = evam.PreProcInfo(range=(0.0, 1.0), **kw)
+    feed = evam.feed.HostFeed(fc, W, H, batch=B, depth=2)
+    feed.set_geometry(DW, DH, info)
+    for d in feed.dev:
+        d.fill_(0xA5)
+    assert feed.bytes_per_batch < B * feed.frame_bytes
+    pp = evam.HipPreProcessor(device=0)
+    lut = O.np_norm_lut(1, (0.0, 1.0))
+    rng = np.random.default_rng(5)
+    mode = info.resize_mode()
+    for step in range(3):
+        frames = [O.random_frame(rng, fc, W, H) for _ in range(B)]
+        k = feed.acquire()
+        feed.fill(k, frames)
+        feed.submit(k)
+        out = torch.empty((B, 3, DH, DW), dtype=torch.float32, device=gpu)
+        pp.convert(feed.batch(k), out, info)
+        feed.release(k)
+        torch.cuda.synchronize()
+        ref = np.zeros((B, 3, DH, DW), np.float32)
+        for i, f in enumerate(frames):
+            coracle.preprocess_item(f, None, ref, i, mode=mode, lut=lut)
+        assert np.array_equal(out.cpu().numpy().view(np.uint32), ref.view(np.uint32)), f"step {step}"
+    pp.close()

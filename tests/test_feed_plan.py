@@ -1,0 +1,46 @@
+"""Host feed copy plan (CPU): the source rows a full-frame pre-process reads (feed.touched_rows, from the
+library's own row table) and the strided copy commands that move them (feed.copy_runs)."""
+import numpy as np
+import pytest
+
+
+def test_touched_rows_c4_is_a_third(evam, O):
+    F = evam.feed
+    rows = F.touched_rows(O.NV12, 3840, 2160, 640, 640, 1)  # C4: 1/6 scale, letterbox
+    assert len(rows[0]) == 720 and len(rows[1]) == 360
+    assert F.copy_runs(rows[0]) == [(2, 2, 6, 360)] and F.copy_runs(rows[1]) == [(1, 1, 3, 360)]
+
+
+@pytest.mark.parametrize("src,dst,mode", [((1920, 1080), (512, 512), 0), ((3840, 2160), (640, 640), 1),
+                                          ((1920, 1080), (224, 224), 2), ((768, 432), (512, 512), 0),
+                                          ((640, 360), (72, 50), 1)])
+def test_touched_rows_match_oracle_table(evam, O, coracle, src, dst, mode):
+    """Luma rows = both clamped taps of every visible output row of the oracle's own y table."""
+    F = evam.feed
+    (W, H), (DW, DH) = src, dst
+    rh, top = F.resized_height(W, H, DW, DH, mode)
+    ofs, _, _ = coracle.linear_table(H, rh, False)
+    want = sorted({min(max(int(s) + d, 0), H - 1) for s in ofs[top:top + DH] for d in (0, 1)})
+    rows = F.touched_rows(O.NV12, W, H, DW, DH, mode)
+    assert rows[0] == want and rows[1] == sorted({r >> 1 for r in want})
+
+
+@pytest.mark.parametrize("seed", range(20))
+def test_copy_runs_cover_rows(evam, seed):
+    """Every row is copied; a strided plan copies nothing else (the bounding-span fallback may)."""
+    F = evam.feed
+    rng = np.random.default_rng(seed)
+    rows = sorted(set(rng.integers(0, 400, int(rng.integers(1, 60))).tolist()))
+    if seed % 3 == 0:  # periodic: runs of 2 every 5 rows
+        rows = sorted({5 * k + d for k in range(40) for d in (1, 2)})
+    cmds = F.copy_runs(rows)
+    got = set()
+    for r0, length, stride, runs in cmds:
+        assert length <= stride
+        for k in range(runs):
+            got.update(range(r0 + k * stride, r0 + k * stride + length))
+    assert set(rows) <= got
+    if len(cmds) > 1 or cmds[0][3] > 1:
+        assert got == set(rows)
+    if seed % 3 == 0:
+        assert cmds == [(1, 2, 5, 40)]

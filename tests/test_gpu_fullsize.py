@@ -174,3 +174,38 @@ def test_c5_ring_step(evam, O, coracle, gpu, shape, monkeypatch):
     untouched = [s * 16 + 5 for s in range(32)]
     assert (ring[untouched] == 7).all().item()
     pp.close()
+
+
+@pytest.mark.parametrize("config", ["c5", "c2"])
+def test_inflight_two_streams_bit_equal(evam, gpu, config):
+    """bench.py --inflight 2: successive launches alternate between two handles bound to two HIP streams (their
+    outputs are independent, so launch t+1's ramp overlaps launch t's tail). The tensors equal one-at-a-time
+    launches on one stream bit for bit (C5: four ring steps into one [32,16,...] clip ring; C2: four batches)."""
+    import torch
+
+    wl = bench.WORKLOADS[config]
+    info = bench.make_info(evam, wl)
+    sets = [evam.ImageBatch(bench.device_frames(evam, torch, wl, 32, gpu, seed=77 + k)) for k in range(2)]
+    DW, DH = wl["dst"]
+    ring = wl.get("ring")
+    shape = (32 * ring, 3, DH, DW) if ring else (32, 3, DH, DW)
+
+    def run(pps, streams):
+        outs = [torch.full(shape, 7.0, device=gpu) for _ in range(1 if ring else 4)]
+        for t in range(4):
+            with torch.cuda.stream(streams[t % len(streams)]):
+                if ring:
+                    pps[t % len(pps)].convert(sets[t % 2], outs[0], info, slot_offset=t, slot_stride=ring)
+                else:
+                    pps[t % len(pps)].convert(sets[t % 2], outs[t], info)
+        torch.cuda.synchronize()
+        return [o.cpu() for o in outs]
+
+    serial = run([evam.HipPreProcessor(device=0)], [torch.cuda.current_stream(gpu)])
+    streams = [torch.cuda.Stream(gpu) for _ in range(2)]
+    pps = [evam.HipPreProcessor(device=0, stream=s) for s in streams]
+    two = run(pps, streams)
+    for a, b in zip(serial, two):
+        assert torch.equal(a.view(torch.int32), b.view(torch.int32))
+    for p in pps:
+        p.close()

@@ -95,6 +95,13 @@ def main():
             "first row landed (absolute)": dist(t[:, 3]),
             "end (absolute)": dist(end)},
         "us_per_row_after_first": dist(loop / np.maximum(rows, 1)),
+        # dense ROI kernel (slots 7-9): record arrived, geometry + scales, footprint + row table
+        **({"prologue_us_entry_to_record_geometry_rowtable_firstdma": [
+            dist((tr[:, 7].astype(np.int64) - tr[:, 0].astype(np.int64)) * 10 / 1000.0),
+            dist((tr[:, 8].astype(np.int64) - tr[:, 7].astype(np.int64)) * 10 / 1000.0),
+            dist((tr[:, 9].astype(np.int64) - tr[:, 8].astype(np.int64)) * 10 / 1000.0),
+            dist((tr[:, 1].astype(np.int64) - tr[:, 9].astype(np.int64)) * 10 / 1000.0)]}
+           if (tr[:, 9] != 0).all() else {}),
         "end_by_xcc": {int(x): round(float(end[xcc == x].max()), 2) for x in sorted(set(xcc.tolist()))},
         # dispatch-order rank of the wave's workgroup on its CU (linear workgroup index // CUs): the older
         # waves of a SIMD win its issue arbitration (MI355X_MICROARCH.md, Two waves per SIMD, item 2)
