@@ -1598,6 +1598,7 @@ struct TParams {
     const RoiRec* recs;
     int mode, placement;         // evam_resize_mode, evam_placement
     int nbw;                     // row bands per workgroup
+    int prio;                    // 1: progress-based wave priority (s_setprio 3 -> 0 over the quarters of a wave's rows)
 };
 static_assert(sizeof(TParams) <= 4000, "strip / band kernel arguments must fit the 4 KB kernarg segment");
 
@@ -1903,6 +1904,11 @@ __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
     const int ra = n ? vr0 : Y1;
     for (int Y = Y0; Y < ra; Y++) put_fill(Y);
 
+    // Progress-based priority (EVAM_PP_PRIO): waves of a SIMD otherwise share issue by age, so the youngest
+    // workgroups' waves lag and end the launch alone; a wave lowers its priority as it passes each quarter of its
+    // rows, so the ones behind get the issue slots when several are ready.
+    const int pq1 = P.prio ? n / 4 : -1, pq2 = P.prio ? n / 2 : -1, pq3 = P.prio ? (3 * n) / 4 : -1;
+    if (P.prio) __builtin_amdgcn_s_setprio(3);
     const int nst = full ? 3 * PX : 3;
     // one output row: row i of the tile's visible rows, ring entry kk (compile-time after unrolling)
     auto row = [&](int i, int kk, auto has_pad) {
@@ -1921,6 +1927,9 @@ __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
 #ifdef EVAM_PP_TRACE
         if (i == 0) EVAM_WSTAMP(3);
 #endif
+        if (i == pq1) __builtin_amdgcn_s_setprio(2);
+        else if (i == pq2) __builtin_amdgcn_s_setprio(1);
+        else if (i == pq3) __builtin_amdgcn_s_setprio(0);
         const int Y = vr0 + i;
         const uint32_t wb0 = (uint32_t)__builtin_amdgcn_readlane(lb0, i), wb1 = (uint32_t)__builtin_amdgcn_readlane(lb1, i);
         const int ya = __builtin_amdgcn_readlane(lr0, i), yb = __builtin_amdgcn_readlane(lr1, i);
@@ -2025,6 +2034,7 @@ struct WRParams {
     int color_rgb;
     uint32_t fill;
     int rt_rows;             // dense kernel: rows of one wave's row table (the most rows of a band, <= 64)
+    int prio;                // dense kernel: progress-based wave priority (as the strip kernel's)
 };
 constexpr int kRingMax = 8;  // most ring entries (rows of DMA in flight) of one wave
 
@@ -2594,7 +2604,13 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_num_sgpr(96))) void evam
     const int T = rows * DW;
     int r = lane / DW, c = lane - (lane / DW) * DW;
     const int so = (int)((uint32_t)(Y0 * DW) * (uint32_t)esz);
+    // progress-based priority (EVAM_PP_PRIO): 3 -> 0 over the quarters of the wave's pixels
+    const int pq1 = P.prio ? (T / 4) & ~63 : -1, pq2 = P.prio ? (T / 2) & ~63 : -1, pq3 = P.prio ? (3 * T / 4) & ~63 : -1;
+    if (P.prio) __builtin_amdgcn_s_setprio(3);
     for (int p0s = 0; p0s < T; p0s += 64) {
+        if (p0s == pq1) __builtin_amdgcn_s_setprio(2);
+        else if (p0s == pq2) __builtin_amdgcn_s_setprio(1);
+        else if (p0s == pq3) __builtin_amdgcn_s_setprio(0);
         // rows this step touches: lane 0's and lane 63's (clamped to the band); wait for the last visible one's DMA
         const int rlo = __builtin_amdgcn_readfirstlane(r);
         const int rhi = min(__builtin_amdgcn_readlane(r, 63), rows - 1);
@@ -2894,7 +2910,13 @@ __global__ __launch_bounds__(256) void evam_pp_band(const TParams P) {
     uint32_t HA[PX][3], HB[PX][3];
     int pa = -1, pb = -1;
     const int nst = 3;  // stores per output row (one PX-wide store per channel)
+    // progress-based priority (EVAM_PP_PRIO), as in the strip kernel
+    const int pq1 = P.prio ? n / 4 : -1, pq2 = P.prio ? n / 2 : -1, pq3 = P.prio ? (3 * n) / 4 : -1;
+    if (P.prio) __builtin_amdgcn_s_setprio(3);
     for (int i = 0; i < n; i++) {
+        if (i == pq1) __builtin_amdgcn_s_setprio(2);
+        else if (i == pq2) __builtin_amdgcn_s_setprio(1);
+        else if (i == pq3) __builtin_amdgcn_s_setprio(0);
         const int ra = __builtin_amdgcn_readlane(lr0, i), rb = __builtin_amdgcn_readlane(lr1, i);
         // rows up to rb landed: issued after them, the DMA of later rows and the stores of rows 0 .. i-1
         const int kd = (rb - rlo + 1) + NPC * (((y0 + rb) >> 1) - clo + 1);
@@ -3441,10 +3463,12 @@ struct Knobs {
     int roi_strip = 1, roi_strip_waves = 4;        // 4:2:0 ROI batches: 1 the dense ROI kernel, 3 the ROI wave kernel,
                                                    // 2 the strip kernel's ROI mode, 0 the ROI kernel; waves per workgroup
     int roi_ring = -1;                             // ROI wave kernel: ring bytes per wave (-1: the LDS budget, <= 8 KB)
+    int prio = 0;                                  // progress-based wave priority in the strip kernel
     void read() {
         roi_strip = env_int("EVAM_PP_ROI_STRIP", roi_strip);
         roi_strip_waves = env_int("EVAM_PP_ROI_STRIP_WAVES", roi_strip_waves);
         roi_ring = env_int("EVAM_PP_ROI_RING", roi_ring);
+        prio = env_int("EVAM_PP_PRIO", prio);
         band = env_int("EVAM_PP_BAND", band); band_px = env_int("EVAM_PP_BAND_PX", band_px);
         strip = env_int("EVAM_PP_STRIP", strip); strip_th = env_int("EVAM_PP_STRIP_TH", strip_th);
         strip_waves = env_int("EVAM_PP_STRIP_WAVES", strip_waves);
@@ -4893,6 +4917,7 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
             w.nbw = r.nbw;
             w.ring_bytes = r.ring_bytes;
             w.rt_rows = r.rt_rows;
+            w.prio = kn.prio;
             w.color_rgb = color_rgb;
             w.fill = fill;
             hipError_t e = r.wave_kernel == 2 ? launch_roid(f, cfg->out_dtype, w, qrec[f], r.nw, r.lds, h->stream)
@@ -4918,6 +4943,7 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
             tp->slot_stride = dst->slot_stride;
             tp->color_rgb = color_rgb;
             tp->fill = fill;
+            tp->prio = kn.prio;
             hipError_t e = launch_roi_strip(f, cfg->out_dtype, r.px, r.slot, *tp, qrec[f], r.nw, r.lds, h->stream);
             if (e != hipSuccess) return fail(EVAM_PP_ERR_HIP, "kernel launch failed: %s", hipGetErrorString(e));
             launches++; kmask |= EVAM_KERNEL_ROI_STRIP;
@@ -4958,6 +4984,7 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
                     tp->slot_stride = dst->slot_stride;
                     tp->color_rgb = color_rgb;
                     tp->fill = fill;
+                    tp->prio = kn.prio;
                     for (int m0 = mfirst[f]; m0 < mfirst[f + 1]; m0 += kArgItems) {
                         const int nm = std::min(kArgItems, mfirst[f + 1] - m0);
                         fill_args(tp->items, m0, nm);
@@ -4986,6 +5013,7 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
                     tp->slot_stride = dst->slot_stride;
                     tp->color_rgb = color_rgb;
                     tp->fill = fill;
+                    tp->prio = kn.prio;
                     for (int m0 = mfirst[f]; m0 < mfirst[f + 1]; m0 += kArgItems) {
                         const int nm = std::min(kArgItems, mfirst[f + 1] - m0);
                         fill_args(tp->items, m0, nm);
