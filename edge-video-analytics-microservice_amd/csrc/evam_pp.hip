@@ -4350,6 +4350,7 @@ struct evam_pp {
     Knobs knobs;                   // EVAM_PP_* tuning knobs, read once at evam_pp_create
     std::vector<int> sc_fmt;       // per-call scratch, kept to avoid reallocation
     std::vector<int> sc_bucket;
+    std::vector<int> sc_sfmt;      // per-call source format ids
     std::vector<int> sc_order;
     std::vector<int> sc_members;   // item indices grouped by source format
     std::vector<Geom> sc_geo;
@@ -4572,17 +4573,23 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
     int max_cw[4] = {0, 0, 0, 0}, max_ch[4] = {0, 0, 0, 0};
     uint32_t x0_mask[4] = {0, 0, 0, 0};  // crop origins x0 mod 32 present (wave-kernel staging bound)
     bool uniform[4] = {true, true, true, true};
-    for (int i = 0; i < n_items; i++) {
-        const evam_roi* r = items ? &items[i] : nullptr;
-        const int si = items ? r->src_index : i;
-        if (si < 0 || si >= n_srcs)
-            return fail(EVAM_PP_ERR_INVALID_ARG, "evam_pp_run: items[%d].src_index %d out of range", i, si);
+    // output slots are linear in the item index: the first and the last bound them all
+    for (int i : {0, n_items - 1}) {
         const int64_t slot = (int64_t)dst->slot_offset + (int64_t)i * dst->slot_stride;
         if (slot < 0 || slot >= dst->n)
             return fail(EVAM_PP_ERR_INVALID_ARG, "evam_pp_run: item %d -> slot %lld outside tensor batch %d", i,
                         (long long)slot, dst->n);
+    }
+    std::vector<int>& sfmt = h->sc_sfmt;  // per source: format id (looked up once, not per ROI)
+    sfmt.resize(n_srcs);
+    for (int i = 0; i < n_srcs; i++) sfmt[i] = fmt_id(srcs[i].fourcc);
+    for (int i = 0; i < n_items; i++) {
+        const evam_roi* r = items ? &items[i] : nullptr;
+        const int si = items ? r->src_index : i;
+        if ((unsigned)si >= (unsigned)n_srcs)
+            return fail(EVAM_PP_ERR_INVALID_ARG, "evam_pp_run: items[%d].src_index %d out of range", i, si);
         const evam_image& s = srcs[si];
-        const int f = fmt_id(s.fourcc);
+        const int f = sfmt[si];
         fmt[i] = f;
         Geom& g = geo[i];
         if (roi_clip(f, s.width, s.height, r != nullptr, r ? r->x : 0, r ? r->y : 0, r ? r->w : 0, r ? r->h : 0, g))
