@@ -1593,11 +1593,6 @@ struct TParams {
     int nstrips, units;          // strips per row; waves of work in the launch
     int segY, segC;              // bytes of one staged luma / chroma row (multiples of 16)
     int nrY;                     // most luma rows of one band (the chroma rows follow at nrY * segY)
-    // strip kernel, ROI mode (per-item geometry): one workgroup per record; its nw waves are the nstrips
-    // strips x nbw row bands of the record's output rows; the geometry is resolved on the device
-    const RoiRec* recs;
-    int mode, placement;         // evam_resize_mode, evam_placement
-    int nbw;                     // row bands per workgroup
     int prio;                    // 1: progress-based wave priority (s_setprio 3 -> 0 over the quarters of a wave's rows)
 };
 static_assert(sizeof(TParams) <= 4000, "strip / band kernel arguments must fit the 4 KB kernarg segment");
@@ -1620,12 +1615,7 @@ static_assert(sizeof(TParams) <= 4000, "strip / band kernel arguments must fit t
 // bytes), the copy floor of those bytes on the same box (profiles/r03c_strip_bw.txt).
 // Letterbox rows are plain fill stores outside the ring; letterbox columns are a per-lane select in the
 // strips that have any. D = ring depth (rows of DMA in flight).
-// ROI mode (ROI = true; per-item geometry: gvaclassify batches, C3): one workgroup per RoiRec, whose 64 bytes (one
-// scalar load) carry the frame and the caller's rect; every wave resolves the crop, resized size and placement with
-// the host's own roi_geometry and computes its strip's footprint, then runs the same ring. The waves of a workgroup
-// are the output's nstrips strips x nbw row bands of the record's rows. SLOT: bytes of one ring segment (the widest
-// strip footprint the host admits; 512 for classifier-sized crops, so 8 workgroups of 4 waves fit a CU).
-template <int FMT, int OUT, int D, int PX, bool ROI = false, int SLOT = strip_slot(PX)>
+template <int FMT, int OUT, int D, int PX>
 __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
     // the LUT at a static LDS address (folds into the reads' immediate offsets); the rings after it
     __shared__ __attribute__((aligned(16))) float lut_s[OUT == 1 ? 768 : 4];
@@ -1633,7 +1623,7 @@ __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
     static_assert(FMT == kNV12 || FMT == kI420, "4:2:0 sources");
     static_assert(D >= 1 && D <= 4, "ring depth");
     static_assert(PX == 1 || PX == 2, "pixels per lane");
-    static_assert(SLOT == 512 || SLOT == 1024, "ring segment");
+    constexpr int SLOT = strip_slot(PX);
     constexpr int NPC = FMT == kI420 ? 2 : 1;  // chroma planes
     constexpr int NMIN = 2 + NPC;              // fewest DMA instructions of one row (chroma row shared)
     const int lane = threadIdx.x & 63;
@@ -1646,75 +1636,33 @@ __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
     double k_scale_x, k_scale_y;
     const float* k_lut;
     int2 sf;
-    if constexpr (!ROI) {
-        // grid (tile column, tile row, item): every kernel-argument load of the prologue has an address known at
-        // entry, so they all go out in one batch (one round trip before the first DMA)
-        const int item = blockIdx.z, ty = blockIdx.y;
-        const ItemArg& it = P.items[item];
-        sf = P.sfoot[min((int)blockIdx.x * 8 + wave, kSfoot - 1)];
-        const int p_TH = P.TH;
-        p_nw = P.nw; p_DH = P.DH; p_DW = P.DW;
-        p0 = it.plane[0];
-        p1 = it.plane[1];
-        p2 = it.plane[2];
-        pitch0 = it.pitch[0]; pitch1 = it.pitch[1]; pitch2 = it.pitch[2];
-        x0 = it.x0; y0 = it.y0;
-        index = it.index;
-        asm volatile("" ::"s"(p_nw), "s"(p_TH), "s"(p_DH), "s"(p_DW), "s"(P.ox), "s"(P.rw), "s"(P.oy), "s"(P.rh),
-                     "s"(P.wave_bytes), "s"(p0), "s"(p1), "s"(p2), "s"(pitch0), "s"(pitch1), "s"(pitch2), "s"(x0), "s"(y0),
-                     "s"(index), "s"(sf.x), "s"(sf.y), "s"(P.dst), "s"(P.slot_offset), "s"(P.slot_stride));
-        // the row table's and the LUT DMA's parameters in the same batch, as opaque values the compiler cannot
-        // reload: loaded where first used, they were one or two more dependent kernel-argument round trips before
-        // the first DMA
-        k_scale_y = P.scale_y;
-        k_ch = P.ch; k_rgb = P.color_rgb;
-        k_lut = P.lut;
-        asm volatile("" : "+s"(k_scale_y), "+s"(k_ch), "+s"(k_lut), "+s"(k_rgb));
-        strip = (int)blockIdx.x * p_nw + wave;
-        Y0 = ty * p_TH; Y1 = min(Y0 + p_TH, p_DH);
-        g_ox = P.ox; g_rw = P.rw; g_oy = P.oy; g_rh = P.rh; g_cw = P.cw;
-        k_scale_x = P.scale_x;
-    } else {
-        // the record first (a PCIe read from the pinned slot), with the launch parameters in the same batch
-        typedef unsigned int u32x16 __attribute__((ext_vector_type(16)));
-        const u32x16 rec = *((const __attribute__((address_space(4))) u32x16*)(P.recs) + blockIdx.x);
-        const int ns = P.nstrips, nbw = P.nbw, mode = P.mode, placement = P.placement;
-        p_nw = P.nw; p_DH = P.DH; p_DW = P.DW;
-        k_rgb = P.color_rgb;
-        k_lut = P.lut;
-        asm volatile("" ::"s"(ns), "s"(nbw), "s"(mode), "s"(placement), "s"(p_nw), "s"(p_DH), "s"(p_DW), "s"(P.wave_bytes), "s"(P.dst),
-                     "s"(P.slot_offset), "s"(P.slot_stride));
-        asm volatile("" : "+s"(k_lut), "+s"(k_rgb));
-        static_assert(offsetof(RoiRec, pitch) == 24 && offsetof(RoiRec, width) == 36 && offsetof(RoiRec, x) == 40 &&
-                      offsetof(RoiRec, item) == 56 && offsetof(RoiRec, row0) == 60, "RoiRec dword map");
-        p0 = reinterpret_cast<const uint8_t*>(((uint64_t)rec[1] << 32) | rec[0]);
-        p1 = reinterpret_cast<const uint8_t*>(((uint64_t)rec[3] << 32) | rec[2]);
-        p2 = reinterpret_cast<const uint8_t*>(((uint64_t)rec[5] << 32) | rec[4]);
-        pitch0 = (int)rec[6]; pitch1 = (int)rec[7]; pitch2 = (int)rec[8];
-        index = (int)rec[14];
-        Geom g;
-        roi_geometry(FMT, (int)(rec[9] & 0xFFFF), (int)(rec[9] >> 16), true, (int)rec[10], (int)rec[11], (int)rec[12],
-                     (int)rec[13], mode, placement, p_DW, p_DH, g);  // never empty: the host validated every item
-        x0 = __builtin_amdgcn_readfirstlane(g.x0); y0 = __builtin_amdgcn_readfirstlane(g.y0);
-        g_cw = __builtin_amdgcn_readfirstlane(g.cw); k_ch = __builtin_amdgcn_readfirstlane(g.ch);
-        g_rw = __builtin_amdgcn_readfirstlane(g.rw); g_rh = __builtin_amdgcn_readfirstlane(g.rh);
-        g_ox = __builtin_amdgcn_readfirstlane(g.ox); g_oy = __builtin_amdgcn_readfirstlane(g.oy);
-        k_scale_x = 1. / ((double)g_rw / g_cw);
-        k_scale_y = 1. / ((double)g_rh / k_ch);
-        const int row0 = (int)(rec[15] & 0xFFFF), row1 = (int)(rec[15] >> 16);
-        strip = wave % ns;
-        const int band = wave / ns, th = (row1 - row0 + nbw - 1) / nbw;
-        Y0 = min(row0 + band * th, row1); Y1 = min(Y0 + th, row1);
-        // this strip's footprint: the taps of its first and last visible output columns (crop-relative)
-        const int Xv0 = max(strip * 64 * PX, g_ox), Xv1 = min(min(strip * 64 * PX + 64 * PX, p_DW), g_ox + g_rw) - 1;
-        sf = int2{-1, -1};
-        if (Xv0 <= Xv1) {
-            int sa, sb, c0, c1;
-            linear_coef(Xv0 - g_ox, k_scale_x, g_cw, true, sa, c0, c1);
-            linear_coef(Xv1 - g_ox, k_scale_x, g_cw, true, sb, c0, c1);
-            sf = int2{__builtin_amdgcn_readfirstlane(sa), __builtin_amdgcn_readfirstlane(min(sb + 1, g_cw - 1))};
-        }
-    }
+    // grid (tile column, tile row, item): every kernel-argument load of the prologue has an address known at
+    // entry, so they all go out in one batch (one round trip before the first DMA)
+    const int item = blockIdx.z, ty = blockIdx.y;
+    const ItemArg& it = P.items[item];
+    sf = P.sfoot[min((int)blockIdx.x * 8 + wave, kSfoot - 1)];
+    const int p_TH = P.TH;
+    p_nw = P.nw; p_DH = P.DH; p_DW = P.DW;
+    p0 = it.plane[0];
+    p1 = it.plane[1];
+    p2 = it.plane[2];
+    pitch0 = it.pitch[0]; pitch1 = it.pitch[1]; pitch2 = it.pitch[2];
+    x0 = it.x0; y0 = it.y0;
+    index = it.index;
+    asm volatile("" ::"s"(p_nw), "s"(p_TH), "s"(p_DH), "s"(p_DW), "s"(P.ox), "s"(P.rw), "s"(P.oy), "s"(P.rh),
+                 "s"(P.wave_bytes), "s"(p0), "s"(p1), "s"(p2), "s"(pitch0), "s"(pitch1), "s"(pitch2), "s"(x0), "s"(y0),
+                 "s"(index), "s"(sf.x), "s"(sf.y), "s"(P.dst), "s"(P.slot_offset), "s"(P.slot_stride));
+    // the row table's and the LUT DMA's parameters in the same batch, as opaque values the compiler cannot
+    // reload: loaded where first used, they were one or two more dependent kernel-argument round trips before
+    // the first DMA
+    k_scale_y = P.scale_y;
+    k_ch = P.ch; k_rgb = P.color_rgb;
+    k_lut = P.lut;
+    asm volatile("" : "+s"(k_scale_y), "+s"(k_ch), "+s"(k_lut), "+s"(k_rgb));
+    strip = (int)blockIdx.x * p_nw + wave;
+    Y0 = ty * p_TH; Y1 = min(Y0 + p_TH, p_DH);
+    g_ox = P.ox; g_rw = P.rw; g_oy = P.oy; g_rh = P.rh; g_cw = P.cw;
+    k_scale_x = P.scale_x;
     const int X0 = strip * 64 * PX;
     const bool live = X0 < p_DW;  // a wave past the last strip only joins the LUT barrier
     const bool cols = live && sf.x >= 0;
@@ -1784,8 +1732,8 @@ __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
     const int npro = min(n, D);
     for (int i = 0; i < npro; i++) issue(i, i);
     EVAM_WSTAMP(1);
-    EVAM_WTRACE_VAL(5, (unsigned long long)(ROI ? index : (int)blockIdx.z) | ((unsigned long long)strip << 16) |
-                           ((unsigned long long)(ROI ? blockIdx.x : blockIdx.y) << 32) | ((unsigned long long)n << 48));
+    EVAM_WTRACE_VAL(5, (unsigned long long)blockIdx.z | ((unsigned long long)strip << 16) |
+                           ((unsigned long long)blockIdx.y << 32) | ((unsigned long long)n << 48));
 
     // per-lane column state of the lane's PX pixels: tap offsets inside the staged segments, packed
     // 11-bit weights, store offsets
@@ -2020,7 +1968,7 @@ __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// ROI wave kernel (per-item geometry, 4:2:0 sources: gvaclassify batches, C3)
+// dense ROI kernel (per-item geometry, 4:2:0 sources: gvaclassify batches, C3)
 // ------------------------------------------------------------------------------------------------
 struct WRParams {
     const RoiRec* recs;      // one record per workgroup: an ROI (or a row tile of a tall output)
@@ -2029,12 +1977,12 @@ struct WRParams {
     int slot_offset, slot_stride;
     int DW, DH;
     int mode, placement;     // evam_resize_mode, evam_placement
-    int nstrips, nbw;        // the workgroup's waves: nstrips strips x nbw row bands of the record's rows
+    int nbw;                 // the workgroup's waves: row bands of the record's rows
     int ring_bytes;          // one wave's LDS ring (a multiple of 16)
     int color_rgb;
     uint32_t fill;
-    int rt_rows;             // dense kernel: rows of one wave's row table (the most rows of a band, <= 64)
-    int prio;                // dense kernel: progress-based wave priority (as the strip kernel's)
+    int rt_rows;             // rows of one wave's row table (the most rows of a band, <= 64)
+    int prio;                // progress-based wave priority (as the strip kernel's)
 };
 constexpr int kRingMax = 8;  // most ring entries (rows of DMA in flight) of one wave
 
@@ -2054,325 +2002,6 @@ __device__ __forceinline__ void vmcnt_le(int n) {
 #undef EVAM_VMC
 }
 
-// ROI batches (per-item geometry) over 4:2:0 sources. One workgroup per RoiRec; its waves are the output's
-// nstrips strips (64·PX columns, lane l: columns l, l + 64) x nbw row bands of the record's rows, and each wave
-// streams its rows alone through a ring in LDS, with no workgroup barrier after the prologue:
-//  * the record (frame planes, pitches and size, the caller's rect, item, rows) is one 64-byte scalar load; the
-//    crop, resized size and placement come from the host's own roi_geometry, the strip's OpenCV coefficients from
-//    linear_coef, per lane;
-//  * a ring entry is exactly one output row's source bytes, packed: [Y tap0][Y tap1] (nY 16-byte chunks each) then
-//    [C tap0][C tap1] per chroma plane (nC chunks each); the luma chunks of a row are ONE LDS-DMA instruction (one
-//    chunk per lane, per-lane source offsets; two for footprints over 512 B) and so are the chroma chunks of a
-//    plane — a 72-wide classifier row of a 200-pixel crop costs 2 DMA instructions instead of 4 mostly idle ones;
-//  * the ring holds as many entries as the wave's ring_bytes allow (up to kRingMax): narrow crops run deep rings,
-//    wide ones shallow, so every wave keeps about the same BYTES in flight (Little's law: the per-CU bytes in flight
-//    set the rate, not the row count) whatever the crop width;
-//  * the waits are exact: the wave counts every vector-memory operation it issues (pos) and remembers pos after each
-//    entry's DMA (one lane of dpos per entry), so row i waits with vmcnt(pos - dpos[i mod D]) — the stores and the
-//    later rows' DMA stay in flight.
-// Per pixel the arithmetic is the strip kernel's (BT.601 saturating two-tap registers, v_dot2 horizontal pass,
-// VResizeLinear as mulhi_u24, the LUT, planar stores).
-template <int FMT, int OUT, int PX>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_num_sgpr(96))) void evam_pp_roiw(const WRParams P) {
-    __shared__ __attribute__((aligned(16))) float lut_s[OUT == 1 ? 768 : 4];
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    static_assert(FMT == kNV12 || FMT == kI420, "4:2:0 sources");
-    static_assert(PX == 1 || PX == 2, "pixels per lane");
-    constexpr int NPC = FMT == kI420 ? 2 : 1;  // chroma planes
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    EVAM_WSTAMP(0);
-    // the record first (a PCIe read from the pinned slot), the launch parameters in the same batch
-    typedef unsigned int u32x16 __attribute__((ext_vector_type(16)));
-    const u32x16 rec = *((const __attribute__((address_space(4))) u32x16*)(P.recs) + blockIdx.x);
-    const int ns = P.nstrips, nbw = P.nbw, mode = P.mode, placement = P.placement, DW = P.DW, DH = P.DH;
-    const int RB = P.ring_bytes;
-    int k_rgb = P.color_rgb;
-    const float* k_lut = P.lut;
-    asm volatile("" ::"s"(ns), "s"(nbw), "s"(mode), "s"(placement), "s"(DW), "s"(DH), "s"(RB), "s"(P.dst),
-                 "s"(P.slot_offset), "s"(P.slot_stride), "s"(P.fill));
-    asm volatile("" : "+s"(k_lut), "+s"(k_rgb));
-    static_assert(offsetof(RoiRec, pitch) == 24 && offsetof(RoiRec, width) == 36 && offsetof(RoiRec, x) == 40 &&
-                  offsetof(RoiRec, item) == 56 && offsetof(RoiRec, row0) == 60, "RoiRec dword map");
-    const uint8_t* p0 = reinterpret_cast<const uint8_t*>(((uint64_t)rec[1] << 32) | rec[0]);
-    const uint8_t* p1 = reinterpret_cast<const uint8_t*>(((uint64_t)rec[3] << 32) | rec[2]);
-    const uint8_t* p2 = reinterpret_cast<const uint8_t*>(((uint64_t)rec[5] << 32) | rec[4]);
-    const int pitch0 = (int)rec[6], pitch1 = (int)rec[7], pitch2 = (int)rec[8];
-    const int index = (int)rec[14];
-    Geom g;
-    roi_geometry(FMT, (int)(rec[9] & 0xFFFF), (int)(rec[9] >> 16), true, (int)rec[10], (int)rec[11], (int)rec[12],
-                 (int)rec[13], mode, placement, DW, DH, g);  // never empty: the host validated every item
-    const int x0 = __builtin_amdgcn_readfirstlane(g.x0), y0 = __builtin_amdgcn_readfirstlane(g.y0);
-    const int cw = __builtin_amdgcn_readfirstlane(g.cw), ch = __builtin_amdgcn_readfirstlane(g.ch);
-    const int rw = __builtin_amdgcn_readfirstlane(g.rw), rh = __builtin_amdgcn_readfirstlane(g.rh);
-    const int ox = __builtin_amdgcn_readfirstlane(g.ox), oy = __builtin_amdgcn_readfirstlane(g.oy);
-    const double scx = 1. / ((double)rw / cw), scy = 1. / ((double)rh / ch);
-    const int row0 = (int)(rec[15] & 0xFFFF), row1 = (int)(rec[15] >> 16);
-    const int strip = wave % ns, band = wave / ns, th = (row1 - row0 + nbw - 1) / nbw;
-    const int Y0 = min(row0 + band * th, row1), Y1 = min(Y0 + th, row1);
-    const int X0 = strip * 64 * PX;
-    // the strip's footprint: the taps of its first and last visible output columns (crop-relative)
-    const int Xv0 = max(X0, ox), Xv1 = min(min(X0 + 64 * PX, DW), ox + rw) - 1;
-    const bool cols = Xv0 <= Xv1;
-    int fsY = 0, nY = 0, fsC = 0, nC = 0;
-    if (cols) {
-        int sa, sb, c0, c1;
-        linear_coef(Xv0 - ox, scx, cw, true, sa, c0, c1);
-        linear_coef(Xv1 - ox, scx, cw, true, sb, c0, c1);
-        footprint_chunks(FMT, 1, x0 + sa, x0 + min(sb + 1, cw - 1), fsY, nY, fsC, nC);
-        fsY = __builtin_amdgcn_readfirstlane(fsY); nY = __builtin_amdgcn_readfirstlane(nY);
-        fsC = __builtin_amdgcn_readfirstlane(fsC); nC = __builtin_amdgcn_readfirstlane(nC);
-    }
-    // visible output rows of the band (the rest are letterbox fill)
-    const int vr0 = max(Y0, oy), vr1 = min(Y1, oy + rh);
-    const int n = cols && vr1 > vr0 ? vr1 - vr0 : 0;
-    // row table, one visible row per lane: source rows relative to the crop, weights << 8
-    int lr0 = 0, lr1 = 0, lb0 = 0, lb1 = 0;
-    if (lane < n) {
-        int sy, b0, b1;
-        linear_coef(vr0 + lane - oy, scy, ch, false, sy, b0, b1);
-        lr0 = min(max(sy, 0), ch - 1);
-        lr1 = min(max(sy + 1, 0), ch - 1);
-        lb0 = b0 << 8;
-        lb1 = b1 << 8;
-    }
-    // per-lane column state of the lane's PX pixels (offsets relative to the tap's segment), stores per row
-    bool xin[PX], padc[PX];
-    uint32_t lY[PX], lC0[PX], lC1[PX], wp[PX], vo[PX];
-    bool anyp = false;
-    int nst = 0;  // store instructions of one output row (3 per pixel column group with a lane inside the output)
-    const size_t esz = OUT == 1 ? 4 : 1;
-#pragma unroll
-    for (int j = 0; j < PX; j++) {
-        const int X = X0 + lane + 64 * j;
-        xin[j] = X < DW;
-        vo[j] = (uint32_t)(xin[j] ? X : 0) * (uint32_t)esz;
-        lY[j] = lC0[j] = lC1[j] = wp[j] = 0;
-        padc[j] = true;
-        const int dx = X - ox;
-        if (cols && xin[j] && dx >= 0 && dx < rw) {
-            int s0, a0, a1;
-            linear_coef(dx, scx, cw, true, s0, a0, a1);
-            const int ca = x0 + s0;  // tap 1 reads ca + 1: at the right edge (s0 = cw - 1) its weight a1 is 0
-            lY[j] = (uint32_t)(ca - fsY);
-            if constexpr (FMT == kNV12) {
-                lC0[j] = (uint32_t)(2 * (ca >> 1) - fsC);
-                lC1[j] = (uint32_t)(2 * ((ca + 1) >> 1) - fsC);
-            } else {
-                lC0[j] = (uint32_t)((ca >> 1) - fsC);
-                lC1[j] = (uint32_t)(((ca + 1) >> 1) - fsC);
-            }
-            wp[j] = (uint32_t)a0 | ((uint32_t)a1 << 16);
-            padc[j] = false;
-        }
-        anyp |= xin[j] && padc[j];
-        nst += __builtin_amdgcn_ballot_w64(xin[j]) != 0 ? 3 : 0;
-    }
-    const bool anypad = cols && __builtin_amdgcn_ballot_w64(anyp) != 0;
-    // ring: entry = [Y0][Y1] nY chunks each, then [C0][C1] nC chunks each per chroma plane
-    const int nchY = 2 * nY, nchC = 2 * nC;
-    const int segY = 16 * nY, segC = 16 * nC, offC = 16 * nchY;
-    const int E = 16 * (nchY + NPC * nchC);
-    const int niY = (nchY + 63) >> 6, niC = (nchC + 63) >> 6;  // DMA instructions per plane (<= 2: host bound)
-    int Dr = E > 0 ? min(kRingMax, RB / E) : 1;
-    while (Dr > 1 && (Dr - 1) * (niY + NPC * niC + nst) > 63) Dr--;  // every wait fits the 6-bit vmcnt
-    Dr = max(Dr, 1);
-    // per-lane DMA source columns of the luma / chroma chunks: chunk q = lane + 64 b -> (tap, chunk c)
-    uint32_t dY[2], dC[2];
-    bool tY[2], tC[2], vY[2], vC[2];
-#pragma unroll
-    for (int b = 0; b < 2; b++) {
-        const int q = lane + 64 * b;
-        tY[b] = q >= nY;
-        vY[b] = q < nchY;
-        dY[b] = (uint32_t)(fsY + 16 * (tY[b] ? q - nY : q));
-        tC[b] = q >= nC;
-        vC[b] = q < nchC;
-        dC[b] = (uint32_t)(fsC + 16 * (tC[b] ? q - nC : q));
-    }
-    const __amdgpu_buffer_rsrc_t rsY = __builtin_amdgcn_make_buffer_rsrc((void*)p0, (short)0, 0x7FFFFFFF, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rsU = __builtin_amdgcn_make_buffer_rsrc((void*)p1, (short)0, 0x7FFFFFFF, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rsV = __builtin_amdgcn_make_buffer_rsrc((void*)(NPC == 2 ? p2 : p1), (short)0, 0x7FFFFFFF, 0x00020000);
-    uint8_t* const wbuf = smem + wave * RB;
-    int pos = 0;  // vector-memory operations this wave issued (wave-uniform)
-    auto issue = [&](int i, int e) {
-        const int ya = y0 + __builtin_amdgcn_readlane(lr0, i), yb = y0 + __builtin_amdgcn_readlane(lr1, i);
-        const int ca = ya >> 1, cb = yb >> 1;
-        uint8_t* const eb = wbuf + e * E;
-#pragma unroll
-        for (int b = 0; b < 2; b++) {
-            if (b < niY) {
-                if (vY[b])
-                    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsY, (__attribute__((address_space(3))) void*)(eb + 1024 * b), 16,
-                                                             (uint32_t)((tY[b] ? yb : ya) * pitch0) + dY[b], 0, 0, EVAM_PP_LOAD_AUX);
-                pos++;  // lane 0 (b = 0) / lane 0 of the second instruction (b < niY) always loads
-            }
-        }
-#pragma unroll
-        for (int b = 0; b < 2; b++) {
-            if (b < niC) {
-                const bool on = vC[b] && !(tC[b] && ca == cb);  // a chroma row both taps share is staged once
-                if (on)
-                    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsU, (__attribute__((address_space(3))) void*)(eb + offC + 1024 * b),
-                                                             16, (uint32_t)((tC[b] ? cb : ca) * pitch1) + dC[b], 0, 0, EVAM_PP_LOAD_AUX);
-                const int issued = __builtin_amdgcn_ballot_w64(on) != 0 ? 1 : 0;
-                pos += issued;
-                if constexpr (NPC == 2) {
-                    if (on)
-                        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsV, (__attribute__((address_space(3))) void*)(eb + offC + 16 * nchC + 1024 * b),
-                                                                 16, (uint32_t)((tC[b] ? cb : ca) * pitch2) + dC[b], 0, 0, EVAM_PP_LOAD_AUX);
-                    pos += issued;
-                }
-            }
-        }
-    };
-    // LUT first (oldest VMEM operation of waves 0-2), then the ring's first rows
-    const int nw = ns * nbw;
-    const bool lut_early = nw >= 3;
-    if constexpr (OUT == 1) {
-        if (lut_early && wave < 3) {
-            const __amdgpu_buffer_rsrc_t rsL = __builtin_amdgcn_make_buffer_rsrc((void*)k_lut, (short)0, 3072, 0x00020000);
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsL, (__attribute__((address_space(3))) void*)(lut_s + wave * 256), 16,
-                                                     (uint32_t)lane * 16u, (k_rgb ? 2 - wave : wave) * 1024, 0, 0);
-            pos++;
-        }
-    }
-    const int lut_pos = pos;
-    int dpos = 0;  // lane e: pos right after ring entry e's DMA
-    const int npro = min(n, Dr);
-    for (int i = 0; i < npro; i++) {
-        issue(i, i);
-        dpos = lane == i ? pos : dpos;
-    }
-    EVAM_WSTAMP(1);
-    const size_t plane = (size_t)DW * DH;
-    uint8_t* const d0 = reinterpret_cast<uint8_t*>(P.dst) + (size_t)(P.slot_offset + index * P.slot_stride) * 3 * plane * esz;
-    uint8_t* const d1 = d0 + plane * esz;
-    uint8_t* const d2 = d1 + plane * esz;
-    // output planes in source channel order (B, G, R): planes 0 and 2 exchanged for RGB
-    const __amdgpu_buffer_rsrc_t rsO0 = __builtin_amdgcn_make_buffer_rsrc((void*)(k_rgb ? d2 : d0), (short)0, 0x7FFFFFFF, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rsO1 = __builtin_amdgcn_make_buffer_rsrc((void*)d1, (short)0, 0x7FFFFFFF, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rsO2 = __builtin_amdgcn_make_buffer_rsrc((void*)(k_rgb ? d0 : d2), (short)0, 0x7FFFFFFF, 0x00020000);
-    const uint32_t fq0 = P.fill & 0xFF, fq1 = (P.fill >> 8) & 0xFF, fq2 = (P.fill >> 16) & 0xFF;
-    const uint32_t fsh = OUT == 1 ? 2 : 0;
-    const uint32_t fill0 = (k_rgb ? fq2 : fq0) << fsh, fill1 = fq1 << fsh, fill2 = (k_rgb ? fq0 : fq2) << fsh;
-    if constexpr (OUT == 1) {
-        if (lut_early) {
-            // this wave's LUT section landed (everything issued after it may stay in flight); LDS-only barrier
-            vmcnt_le(pos - lut_pos);
-            lds_barrier();
-        } else {  // workgroups of 1-2 waves
-            for (int idx = threadIdx.x; idx < 768; idx += nw * 64)
-                lut_s[idx] = k_lut[k_rgb ? 512 - (idx & ~255) + (idx & 255) : idx];
-            __syncthreads();
-        }
-    }
-    EVAM_WSTAMP(2);
-    const uint8_t* lutb = reinterpret_cast<const uint8_t*>(lut_s);
-    // BT.601 chroma-term constants: the additive ones in VGPRs so every term is one v_mad
-    uint32_t kb = kKBs, kg = kKGs, kr = kKRs;
-    int cvg = kCVG, cug = kCUG;
-    asm volatile("" : "+v"(kb), "+v"(kg), "+v"(kr), "+s"(cvg), "+s"(cug));
-    auto uvt = [&](uint32_t U, uint32_t V) {
-        int gu = __mul24((int)U, cug) + (int)kg;
-        asm("" : "+v"(gu));
-        return UVs{__umul24(U, (uint32_t)kCUB) + kb, (uint32_t)(__mul24((int)V, cvg) + gu), __umul24(V, (uint32_t)kCVR) + kr};
-    };
-    auto put = [&](int Y, int j, uint32_t v0, uint32_t v1, uint32_t v2) {
-        if (!xin[j]) return;
-        const int so = (int)((uint32_t)(Y * DW) * (uint32_t)esz);
-        if constexpr (OUT == 1) {
-            __builtin_amdgcn_raw_buffer_store_b32(*reinterpret_cast<const uint32_t*>(lutb + v0), rsO0, vo[j], so, EVAM_PP_STORE_AUX);
-            __builtin_amdgcn_raw_buffer_store_b32(*reinterpret_cast<const uint32_t*>(lutb + 1024 + v1), rsO1, vo[j], so, EVAM_PP_STORE_AUX);
-            __builtin_amdgcn_raw_buffer_store_b32(*reinterpret_cast<const uint32_t*>(lutb + 2048 + v2), rsO2, vo[j], so, EVAM_PP_STORE_AUX);
-        } else {
-            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v0, rsO0, vo[j], so, EVAM_PP_STORE_AUX);
-            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v1, rsO1, vo[j], so, EVAM_PP_STORE_AUX);
-            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v2, rsO2, vo[j], so, EVAM_PP_STORE_AUX);
-        }
-    };
-    auto put_fill = [&](int Y) {
-#pragma unroll
-        for (int j = 0; j < PX; j++) put(Y, j, fill0, fill1, fill2);
-        pos += nst;
-    };
-    const int ra = n ? vr0 : Y1;
-    for (int Y = Y0; Y < ra; Y++) put_fill(Y);  // letterbox rows above
-    auto row = [&](int i, int e, auto has_pad) {
-        constexpr bool PADC = decltype(has_pad)::value;
-        vmcnt_le(pos - __builtin_amdgcn_readlane(dpos, e));  // row i's DMA landed
-#ifdef EVAM_PP_TRACE
-        if (i == 0) EVAM_WSTAMP(3);
-#endif
-        const int Y = vr0 + i;
-        const uint32_t wb0 = (uint32_t)__builtin_amdgcn_readlane(lb0, i), wb1 = (uint32_t)__builtin_amdgcn_readlane(lb1, i);
-        const int ya = __builtin_amdgcn_readlane(lr0, i), yb = __builtin_amdgcn_readlane(lr1, i);
-        const bool share = ((y0 + ya) >> 1) == ((y0 + yb) >> 1);
-        const uint8_t* const eb = wbuf + e * E;
-        const int soC = share ? 0 : segC;  // second source row's chroma segment
-#pragma unroll
-        for (int j = 0; j < PX; j++) {
-            const uint8_t* ay = eb + lY[j];
-            const uint8_t* ac0 = eb + offC + lC0[j];
-            const uint8_t* ac1 = eb + offC + lC1[j];
-            const uint32_t yA = luma_term(ay[0]), yB = luma_term(ay[1]);
-            const uint32_t yC = luma_term(ay[segY]), yD = luma_term(ay[segY + 1]);
-            UVs tA, tB, tC, tE;
-            if constexpr (FMT == kNV12) {
-                tA = uvt(ac0[0], ac0[1]);
-                tB = uvt(ac1[0], ac1[1]);
-                tC = uvt(ac0[soC], ac0[soC + 1]);
-                tE = uvt(ac1[soC], ac1[soC + 1]);
-            } else {
-                const int oV = 16 * nchC;  // the V plane's chunks follow the U plane's
-                tA = uvt(ac0[0], ac0[oV]);
-                tB = uvt(ac1[0], ac1[oV]);
-                tC = uvt(ac0[soC], ac0[oV + soC]);
-                tE = uvt(ac1[soC], ac1[oV + soC]);
-            }
-            uint32_t h0[3], h1[3];
-            h0[0] = hpass_sat(yA, tA.b, yB, tB.b, wp[j]);
-            h0[1] = hpass_sat(yA, tA.g, yB, tB.g, wp[j]);
-            h0[2] = hpass_sat(yA, tA.r, yB, tB.r, wp[j]);
-            h1[0] = hpass_sat(yC, tC.b, yD, tE.b, wp[j]);
-            h1[1] = hpass_sat(yC, tC.g, yD, tE.g, wp[j]);
-            h1[2] = hpass_sat(yC, tC.r, yD, tE.r, wp[j]);
-            uint32_t v[3];
-#pragma unroll
-            for (int c = 0; c < 3; c++) v[c] = vfinal<OUT>(h0[c], h1[c], wb0, wb1);
-            if constexpr (PADC) {
-                v[0] = padc[j] ? fill0 : v[0];
-                v[1] = padc[j] ? fill1 : v[1];
-                v[2] = padc[j] ? fill2 : v[2];
-            }
-            put(Y, j, v[0], v[1], v[2]);
-        }
-        pos += nst;
-        asm volatile("" ::: "memory");  // issue order is what the counted waits assume
-        if (i + Dr < n) {  // this entry's reads are done: the stores consumed them
-            issue(i + Dr, e);
-            dpos = lane == e ? pos : dpos;
-        }
-        asm volatile("" ::: "memory");
-    };
-    auto ring = [&](auto has_pad) {
-        int e = 0;
-        for (int i = 0; i < n; i++) {
-            row(i, e, has_pad);
-            e = e + 1 == Dr ? 0 : e + 1;
-        }
-    };
-    if (anypad) ring(std::true_type{});
-    else ring(std::false_type{});
-    for (int Y = max(ra, vr1); Y < Y1; Y++) put_fill(Y);  // letterbox rows below
-#ifdef EVAM_PP_TRACE
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    EVAM_WSTAMP(4);
-    EVAM_WTRACE_VAL(5, (unsigned long long)index | ((unsigned long long)Dr << 16) | ((unsigned long long)E << 32) |
-                           ((unsigned long long)n << 48));
-#endif
-}
-
 // Dense ROI kernel (per-item geometry, 4:2:0 sources: gvaclassify batches, C3). One workgroup per RoiRec, whose
 // nbw waves each own a band of the record's output rows — every column of them: the band's rows x DW pixels are
 // one flat run, walked 64 pixels per step (pixel p = 64 s + lane), so a 72-wide classifier row keeps every lane
@@ -2381,10 +2010,15 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_num_sgpr(96))) void evam
 //  * Tables: the item's OpenCV column coefficients once per workgroup (colTab, 8 B per output column: tap offsets
 //    inside the staged segments and the packed 11-bit weights), its row coefficients once per wave (rowTab, 16 B per
 //    band row: weights, ring entry, second chroma segment, fill flag); a pixel reads its column and row entry.
-//  * Ring: as evam_pp_roiw — a visible row's luma chunks are one LDS-DMA instruction and its chroma chunks one per
-//    plane, entries are packed to the crop's footprint, and the ring is as deep as the wave's bytes allow (up to
-//    kRingMax), so every wave keeps about the same bytes in flight whatever the crop width. Step s waits (exactly:
-//    pos / dpos counting) for the last row it touches; a row's entry is refilled once no later step reads it.
+//  * Ring: a ring entry is exactly one visible row's source bytes, packed: [Y tap0][Y tap1] (nY 16-byte chunks each)
+//    then [C tap0][C tap1] per chroma plane (nC chunks each); a row's luma chunks are ONE LDS-DMA instruction (one
+//    chunk per lane, per-lane source offsets; two for footprints over 512 B) and so are its chroma chunks per plane
+//    (a 200-pixel crop's row: 2 DMA instructions, not 4 mostly idle ones). The ring holds as many entries as the wave's
+//    ring_bytes allow (up to kRingMax): narrow crops run deep rings, wide ones shallow, so every wave keeps about the
+//    same bytes in flight whatever the crop width. The waits are exact: the wave counts every vector-memory operation
+//    it issues (pos) and remembers pos after each row's DMA (lane vi of dpos), so step s waits with vmcnt(pos -
+//    dpos[last row it reads]) and the stores and later rows' DMA stay in flight; a row's entry is refilled once no
+//    later step reads it.
 //  * Letterbox rows and columns are pixels of the run like any other (fill flag / pad bit -> the fill value).
 template <int FMT, int OUT>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_num_sgpr(96))) void evam_pp_roid(const WRParams P) {
@@ -3460,13 +3094,13 @@ struct Knobs {
                                                                               // rows per tile, ring depth, waves, px
     int strip_waves = 16;                          // strip / band kernels: resident waves per CU the tiles are sized for
     int band = 1, band_px = 0;                     // band kernel: allowed (2: forced), pixels per lane
-    int roi_strip = 1, roi_strip_waves = 4;        // 4:2:0 ROI batches: 1 the dense ROI kernel, 3 the ROI wave kernel,
-                                                   // 2 the strip kernel's ROI mode, 0 the ROI kernel; waves per workgroup
-    int roi_ring = -1;                             // ROI wave kernel: ring bytes per wave (-1: the LDS budget, <= 8 KB)
+    int roi_dense = 1, roi_dense_waves = 4;        // 4:2:0 ROI batches on the dense ROI kernel (0: the ROI kernel); its
+                                                   // waves (row bands) per workgroup
+    int roi_ring = -1;                             // dense ROI kernel: ring bytes per wave (-1: the LDS budget, <= 8 KB)
     int prio = 0;                                  // progress-based wave priority in the strip kernel
     void read() {
-        roi_strip = env_int("EVAM_PP_ROI_STRIP", roi_strip);
-        roi_strip_waves = env_int("EVAM_PP_ROI_STRIP_WAVES", roi_strip_waves);
+        roi_dense = env_int("EVAM_PP_ROI_DENSE", roi_dense);
+        roi_dense_waves = env_int("EVAM_PP_ROI_DENSE_WAVES", roi_dense_waves);
         roi_ring = env_int("EVAM_PP_ROI_RING", roi_ring);
         prio = env_int("EVAM_PP_PRIO", prio);
         band = env_int("EVAM_PP_BAND", band); band_px = env_int("EVAM_PP_BAND_PX", band_px);
@@ -3924,55 +3558,6 @@ hipError_t launch_strip(int f, int out, int d, int px, const TParams& p, dim3 gr
     }
 }
 
-// ROI mode of the strip kernel (per-item geometry): ring depth 2; 64-column strips with 512-byte segments, 128-column
-// strips with 512- or 1024-byte segments.
-template <int FMT, int OUT, int PX, int SLOT>
-hipError_t launch_roi_strip_t(const TParams& p, int grid, int nw, int lds, hipStream_t s) {
-    if (lds > 64 * 1024) {
-        hipError_t e = hipFuncSetAttribute((const void*)evam_pp_strip<FMT, OUT, 2, PX, true, SLOT>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-        if (e != hipSuccess) return e;
-    }
-    hipLaunchKernelGGL((evam_pp_strip<FMT, OUT, 2, PX, true, SLOT>), dim3(grid), dim3(64 * nw), lds, s, p);
-    return hipGetLastError();
-}
-template <int FMT, int OUT>
-const void* roi_strip_fn_t(int px, int slot) {
-    return px == 1 ? (const void*)evam_pp_strip<FMT, OUT, 2, 1, true, 512>
-         : slot == 512 ? (const void*)evam_pp_strip<FMT, OUT, 2, 2, true, 512> : (const void*)evam_pp_strip<FMT, OUT, 2, 2, true, 1024>;
-}
-const void* roi_strip_fn(int f, int out, int px, int slot) {
-    switch (f * 2 + out) {
-    case kNV12 * 2 + 0: return roi_strip_fn_t<kNV12, 0>(px, slot);
-    case kNV12 * 2 + 1: return roi_strip_fn_t<kNV12, 1>(px, slot);
-    case kI420 * 2 + 0: return roi_strip_fn_t<kI420, 0>(px, slot);
-    default: return roi_strip_fn_t<kI420, 1>(px, slot);
-    }
-}
-template <int FMT, int OUT>
-hipError_t launch_roi_strip_f(int px, int slot, const TParams& p, int grid, int nw, int lds, hipStream_t s) {
-    if (px == 1) return launch_roi_strip_t<FMT, OUT, 1, 512>(p, grid, nw, lds, s);
-    if (slot == 512) return launch_roi_strip_t<FMT, OUT, 2, 512>(p, grid, nw, lds, s);
-    return launch_roi_strip_t<FMT, OUT, 2, 1024>(p, grid, nw, lds, s);
-}
-hipError_t launch_roi_strip(int f, int out, int px, int slot, const TParams& p, int grid, int nw, int lds, hipStream_t s) {
-    switch (f * 2 + out) {
-    case kNV12 * 2 + 0: return launch_roi_strip_f<kNV12, 0>(px, slot, p, grid, nw, lds, s);
-    case kNV12 * 2 + 1: return launch_roi_strip_f<kNV12, 1>(px, slot, p, grid, nw, lds, s);
-    case kI420 * 2 + 0: return launch_roi_strip_f<kI420, 0>(px, slot, p, grid, nw, lds, s);
-    default: return launch_roi_strip_f<kI420, 1>(px, slot, p, grid, nw, lds, s);
-    }
-}
-
-template <int FMT, int OUT, int PX>
-hipError_t launch_roiw_t(const WRParams& p, int grid, int nw, int lds, hipStream_t s) {
-    if (lds > 64 * 1024) {
-        hipError_t e = hipFuncSetAttribute((const void*)evam_pp_roiw<FMT, OUT, PX>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-        if (e != hipSuccess) return e;
-    }
-    hipLaunchKernelGGL((evam_pp_roiw<FMT, OUT, PX>), dim3(grid), dim3(64 * nw), lds, s, p);
-    return hipGetLastError();
-}
 template <int FMT, int OUT>
 hipError_t launch_roid_t(const WRParams& p, int grid, int nw, int lds, hipStream_t s) {
     if (lds > 64 * 1024) {
@@ -3998,98 +3583,50 @@ hipError_t launch_roid(int f, int out, const WRParams& p, int grid, int nw, int 
     default: return launch_roid_t<kI420, 1>(p, grid, nw, lds, s);
     }
 }
-const void* roiw_fn(int f, int out, int px) {
-    switch ((f * 2 + out) * 2 + (px == 2)) {
-    case (kNV12 * 2 + 0) * 2: return (const void*)evam_pp_roiw<kNV12, 0, 1>;
-    case (kNV12 * 2 + 0) * 2 + 1: return (const void*)evam_pp_roiw<kNV12, 0, 2>;
-    case (kNV12 * 2 + 1) * 2: return (const void*)evam_pp_roiw<kNV12, 1, 1>;
-    case (kNV12 * 2 + 1) * 2 + 1: return (const void*)evam_pp_roiw<kNV12, 1, 2>;
-    case (kI420 * 2 + 0) * 2: return (const void*)evam_pp_roiw<kI420, 0, 1>;
-    case (kI420 * 2 + 0) * 2 + 1: return (const void*)evam_pp_roiw<kI420, 0, 2>;
-    case (kI420 * 2 + 1) * 2: return (const void*)evam_pp_roiw<kI420, 1, 1>;
-    default: return (const void*)evam_pp_roiw<kI420, 1, 2>;
-    }
-}
-hipError_t launch_roiw(int f, int out, int px, const WRParams& p, int grid, int nw, int lds, hipStream_t s) {
-    switch ((f * 2 + out) * 2 + (px == 2)) {
-    case (kNV12 * 2 + 0) * 2: return launch_roiw_t<kNV12, 0, 1>(p, grid, nw, lds, s);
-    case (kNV12 * 2 + 0) * 2 + 1: return launch_roiw_t<kNV12, 0, 2>(p, grid, nw, lds, s);
-    case (kNV12 * 2 + 1) * 2: return launch_roiw_t<kNV12, 1, 1>(p, grid, nw, lds, s);
-    case (kNV12 * 2 + 1) * 2 + 1: return launch_roiw_t<kNV12, 1, 2>(p, grid, nw, lds, s);
-    case (kI420 * 2 + 0) * 2: return launch_roiw_t<kI420, 0, 1>(p, grid, nw, lds, s);
-    case (kI420 * 2 + 0) * 2 + 1: return launch_roiw_t<kI420, 0, 2>(p, grid, nw, lds, s);
-    case (kI420 * 2 + 1) * 2: return launch_roiw_t<kI420, 1, 1>(p, grid, nw, lds, s);
-    default: return launch_roiw_t<kI420, 1, 2>(p, grid, nw, lds, s);
-    }
-}
-
-// ROI-strip plan for a 4:2:0 group with per-item geometry (gvaclassify batches: C3).
-struct RoiStripPlan {
-    int px, slot, nstrips, nbw, nw, lds, tiles;  // tiles: row tiles (units) per ROI
-    int unit_rows;                               // output rows of one unit (the last may be shorter)
-    int rt_rows;                                 // dense kernel: row-table rows per wave
-    int wave_kernel;                             // 2: evam_pp_roid (dense), 1: evam_pp_roiw, 0: the strip kernel's ROI mode
-    int ring_bytes;                              // evam_pp_roiw: one wave's ring
+// Dense ROI kernel plan for a 4:2:0 group with per-item geometry (gvaclassify batches: C3).
+struct RoiDensePlan {
+    int nbw, lds, tiles;  // waves (row bands) per workgroup, dynamic LDS, row tiles (units) per ROI
+    int unit_rows;        // output rows of one unit (the last may be shorter)
+    int rt_rows;          // row-table rows per wave (the most rows of one band, <= 64)
+    int ring_bytes;       // one wave's ring
 };
-//  * PX 2 (128-column strips) for outputs wider than 64 columns: a 72-wide classifier row is one wave-row of DMA and
-//    stores (the second pixel column of a lane is live in 8 lanes); PX 1 otherwise.
-//  * Segment (SLOT) bytes: every strip's footprint must fit one DMA instruction of SLOT / 16 chunks for every crop the
-//    group can hold. A strip of 64 PX columns spans at most (64 PX - 1) x ratio + 3 source pixels, with ratio =
-//    cw / rw <= max(max_cw / DW, max_ch / DH) in every resize mode (no-aspect: rw = DW; aspect: rw = DW or cw DH / ch;
-//    aspect + crop: rw >= DW), and at most max_cw + 1 when one strip covers the whole output row.
-//  * Waves: nstrips x nbw row bands (about four waves per workgroup, at most 64 rows per wave: the lane-held row
-//    table); ROIs taller than nbw x 64 output rows become several row tiles (units).
-// Returns false where the ROI kernel must serve the group (packed formats, > 8 strips, wider footprints).
-bool plan_roi_strip(int f, int DW, int DH, int out_dtype, int max_cw, int max_ch, int count, int n_cu, const Knobs& kn,
-                    RoiStripPlan& r) {
+//  * Waves: nbw row bands of all DW columns (EVAM_PP_ROI_DENSE_WAVES, default 4: 18 rows each at 72 x 72); ROIs taller
+//    than nbw x 64 output rows become several row tiles (units).
+//  * Footprint bound: a row's taps span at most max_cw + 1 source pixels of any crop of the group; it must fit two DMA
+//    instructions per plane (64 16-byte chunks per tap segment).
+//  * Ring: at least the rows one 64-pixel step reads (ceil(63 / DW) + 1) of the widest footprint; the rest of the budget
+//    — the CU's LDS shared by the workgroups one round needs (C3: 1,600 ROIs -> 7 per CU), at most 8 KB per wave —
+//    lets narrow crops run deeper rings.
+// Returns false where the ROI kernel must serve the group (packed formats, wider footprints, DW < 10).
+bool plan_roi_dense(int f, int DW, int DH, int out_dtype, int max_cw, int count, int n_cu, const Knobs& kn,
+                    RoiDensePlan& r) {
     if ((f != kNV12 && f != kI420) || DH > 65535) return false;
-    // kernel: 1 the dense ROI kernel (default), 3 the ROI wave kernel, 2 the strip kernel's ROI mode
-    r.wave_kernel = kn.roi_strip == 2 ? 0 : (kn.roi_strip == 3 ? 1 : 2);
-    r.px = kn.strip_px > 0 ? kn.strip_px : (DW > 64 ? 2 : 1);
-    if (r.px != 1 && r.px != 2) return false;
-    const int sw = r.wave_kernel == 2 ? DW : 64 * r.px;  // columns of one wave's rows (dense: all of them)
-    r.nstrips = (DW + sw - 1) / sw;
-    if (r.nstrips > 8) return false;
-    const double ratio = std::max((double)max_cw / DW, (double)max_ch / DH);
-    int span = (int)std::ceil((sw - 1) * ratio) + 3;
-    if (r.nstrips == 1) span = std::min(span, max_cw + 1);
-    const int chunks = (span + 32) / 16 + 1;  // 16-byte windows of the luma (and NV12 chroma) footprint
-    r.slot = chunks * 16 <= 512 ? 512 : 1024;
-    if (r.wave_kernel == 0 && (chunks * 16 > r.slot || (r.px == 1 && r.slot > 512))) return false;
-    r.nbw = std::max(1, std::min(8 / r.nstrips, kn.roi_strip_waves / r.nstrips));
-    r.nw = r.nstrips * r.nbw;
+    const int chunks = (max_cw + 1 + 32) / 16 + 1;  // 16-byte windows of the luma (and NV12 chroma) footprint
+    if (chunks > 64) return false;
+    const int step_rows = (63 + DW - 1) / DW + 1;
+    if (step_rows + 1 > kRingMax) return false;  // DW < 10: 64 pixels span more rows than a ring holds
+    r.nbw = std::max(1, std::min(8, kn.roi_dense_waves));
     r.unit_rows = std::min(DH, r.nbw * 64);
     r.tiles = (DH + r.unit_rows - 1) / r.unit_rows;
+    r.rt_rows = (r.unit_rows + r.nbw - 1) / r.nbw;
     const int npc = f == kI420 ? 2 : 1;
     const int lut_static = out_dtype == EVAM_DTYPE_F32 ? kLutBytes : 16;
-    if (r.wave_kernel == 0) {
-        const int wave_bytes = 2 * (2 + 2 * npc) * r.slot;  // D = 2 ring entries
-        r.lds = r.nw * wave_bytes + 16;  // + 16: a right-edge tap reads past its footprint (weight 0)
-        return r.lds + lut_static <= 64 * 1024;
-    }
-    // Packed rings (evam_pp_roid / evam_pp_roiw): at least the rows one step reads (dense: 64 pixels span up to
-    // ceil(63 / DW) + 1 rows; plus one in flight) of the widest footprint; the rest of the budget lets narrow crops run
-    // deeper rings. Budget: the LDS of a CU shared by the workgroups one round needs (C3: 1,600 ROIs -> 7 per CU).
-    if (chunks > 64) return false;  // a tap segment over 1 KB: two DMA instructions per plane at most
-    const int step_rows = r.wave_kernel == 2 ? (63 + DW - 1) / DW + 1 : 2;
-    if (step_rows + 1 > kRingMax) return false;  // DW < 10: 64 pixels span more rows than a ring holds
     const int emax = 16 * (2 * chunks + 2 * npc * chunks);
-    r.rt_rows = (r.unit_rows + r.nbw - 1) / r.nbw;  // the most rows of one wave's band
-    const int fixed = r.wave_kernel == 2 ? ((DW * 8 + 15) & ~15) + r.nw * r.rt_rows * 16 : 0;  // colTab + rowTabs
+    const int fixed = ((DW * 8 + 15) & ~15) + r.nbw * r.rt_rows * 16;  // colTab + rowTabs
     const int64_t units = (int64_t)count * r.tiles;
     const int per_cu = (int)std::max<int64_t>(1, std::min<int64_t>(8, (units + n_cu - 1) / n_cu));
     // LDS is allocated in 1 KB granules per workgroup (static LUT included)
-    int rb = ((((160 * 1024) / per_cu) & ~1023) - lut_static - 16 - fixed) / r.nw & ~15;
+    int rb = ((((160 * 1024) / per_cu) & ~1023) - lut_static - 16 - fixed) / r.nbw & ~15;
     if (kn.roi_ring > 0) rb = kn.roi_ring & ~15;
     rb = std::min(rb, 8 * 1024);
     const int rmin = step_rows * emax;  // the rows one step reads, of the widest footprint
     r.ring_bytes = std::max(rb, rmin);
-    r.lds = fixed + r.nw * r.ring_bytes + 16;  // + 16: a right-edge tap reads past its footprint (weight 0)
+    r.lds = fixed + r.nbw * r.ring_bytes + 16;  // + 16: a right-edge tap reads past its footprint (weight 0)
     if (r.lds + lut_static > 160 * 1024) return false;
-    const void* fn = r.wave_kernel == 2 ? roid_fn(f, out_dtype) : roiw_fn(f, out_dtype, r.px);
-    while (kn.roi_ring <= 0 && resident_per_cu(fn, r.lds, 64 * r.nw) < per_cu && r.ring_bytes - 256 >= rmin) {
+    const void* fn = roid_fn(f, out_dtype);
+    while (kn.roi_ring <= 0 && resident_per_cu(fn, r.lds, 64 * r.nbw) < per_cu && r.ring_bytes - 256 >= rmin) {
         r.ring_bytes -= 256;
-        r.lds = fixed + r.nw * r.ring_bytes + 16;
+        r.lds = fixed + r.nbw * r.ring_bytes + 16;
     }
     return true;
 }
@@ -4617,11 +4154,11 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
     //   uniform geometry        -> staged / wave / row kernels: host-built tables, items in kernel arguments
     //   per-item geometry       -> ROI kernel: raw ROI rect + source (RoiRec), geometry resolved on the device
     //   ROI plan impossible     -> generic kernel, per-item ItemDesc in the descriptor block
-    //   per-item geometry, 4:2:0 -> strip kernel in ROI mode (RoiRec per row tile, geometry resolved on the device)
-    enum { kPathNone, kPathUniform, kPathRoi, kPathGeneric, kPathRoiStrip };
+    //   per-item geometry, 4:2:0 -> dense ROI kernel (RoiRec per row tile, geometry resolved on the device)
+    enum { kPathNone, kPathUniform, kPathRoi, kPathGeneric, kPathRoiDense };
     int path[4];
     QParams qp[4];
-    RoiStripPlan rsp[4];
+    RoiDensePlan rsp[4];
     int qlds[4] = {0, 0, 0, 0}, qbase[4] = {1, 1, 1, 1}, qrec[4] = {0, 0, 0, 0};
     int64_t qslots[4] = {0, 0, 0, 0};
     bool any_generic = false, any_roi = false;
@@ -4629,20 +4166,20 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
         path[f] = kPathNone;
         if (!count[f]) continue;
         if (uniform[f] && kn.rows) path[f] = kPathUniform;
-        else if (kn.roi && kn.roi_strip &&
-                 plan_roi_strip(f, DW, DH, cfg->out_dtype, max_cw[f], max_ch[f], count[f], h->n_cu, kn, rsp[f])) path[f] = kPathRoiStrip;
+        else if (kn.roi && kn.roi_dense &&
+                 plan_roi_dense(f, DW, DH, cfg->out_dtype, max_cw[f], count[f], h->n_cu, kn, rsp[f])) path[f] = kPathRoiDense;
         else if (kn.roi && plan_roi(f, DW, DH, cfg->out_dtype, kn.roi_px, row_bytes_bound(f, max_cw[f]), count[f], h->n_cu,
                                     kn, qp[f], qbase[f], qlds[f], qslots[f])) path[f] = kPathRoi;
         else path[f] = kPathGeneric;
         any_generic |= path[f] == kPathGeneric;
-        any_roi |= path[f] == kPathRoi || path[f] == kPathRoiStrip;
+        any_roi |= path[f] == kPathRoi || path[f] == kPathRoiDense;
     }
     // Full geometry on the host only where something consumes it.
     const bool all_geo = out_xform != nullptr || h->opt_stats;
     int64_t src_bytes = 0;
     for (int i = 0; i < n_items; i++) {
         const int f = fmt[i];
-        if (!all_geo && (path[f] == kPathRoi || path[f] == kPathRoiStrip)) continue;
+        if (!all_geo && (path[f] == kPathRoi || path[f] == kPathRoiDense)) continue;
         if (!all_geo && path[f] == kPathUniform && i != rep[f]) continue;  // same crop size: rep's geometry
         Geom& g = geo[i];
         const evam_roi* r = items ? &items[i] : nullptr;
@@ -4682,7 +4219,7 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
     size_t rec_off[4] = {0, 0, 0, 0}, dyn_bytes = 0;
     if (any_roi) {
         for (int f = 0; f < 4; f++) {
-            if (path[f] == kPathRoiStrip) {
+            if (path[f] == kPathRoiDense) {
                 rec_off[f] = dyn_bytes;
                 dyn_bytes += sizeof(RoiRec) * (size_t)count[f] * (size_t)rsp[f].tiles;
                 continue;
@@ -4763,11 +4300,11 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
         std::vector<int>& bucket = h->sc_bucket;
         bucket.resize(n_items);
         for (int f = 0; f < 4; f++) {
-            if (path[f] == kPathRoiStrip) {
+            if (path[f] == kPathRoiDense) {
                 // records in call order, one per row tile: the frame's planes next to the caller's rect (the
                 // kernel resolves the geometry); every ROI does the same output work, so no ordering pass
                 RoiRec* rr = reinterpret_cast<RoiRec*>(dyn + rec_off[f]);
-                const RoiStripPlan& r = rsp[f];
+                const RoiDensePlan& r = rsp[f];
                 for (int m = mfirst[f]; m < mfirst[f + 1]; m++) {
                     const int i = members[m];
                     const evam_image& sim = srcs[items ? items[i].src_index : i];
@@ -4909,8 +4446,8 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
     };
     for (int f = 0; f < 4; f++) {
         if (path[f] == kPathNone) continue;
-        if (path[f] == kPathRoiStrip && rsp[f].wave_kernel) {
-            const RoiStripPlan& r = rsp[f];
+        if (path[f] == kPathRoiDense) {
+            const RoiDensePlan& r = rsp[f];
             WRParams w{};
             w.recs = reinterpret_cast<const RoiRec*>(d_dyn + rec_off[f]);
             w.lut = lut_d;
@@ -4920,40 +4457,15 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
             w.DW = DW; w.DH = DH;
             w.mode = cfg->resize_mode;
             w.placement = cfg->placement;
-            w.nstrips = r.nstrips;
             w.nbw = r.nbw;
             w.ring_bytes = r.ring_bytes;
             w.rt_rows = r.rt_rows;
             w.prio = kn.prio;
             w.color_rgb = color_rgb;
             w.fill = fill;
-            hipError_t e = r.wave_kernel == 2 ? launch_roid(f, cfg->out_dtype, w, qrec[f], r.nw, r.lds, h->stream)
-                                              : launch_roiw(f, cfg->out_dtype, r.px, w, qrec[f], r.nw, r.lds, h->stream);
+            hipError_t e = launch_roid(f, cfg->out_dtype, w, qrec[f], r.nbw, r.lds, h->stream);
             if (e != hipSuccess) return fail(EVAM_PP_ERR_HIP, "kernel launch failed: %s", hipGetErrorString(e));
-            launches++; kmask |= r.wave_kernel == 2 ? EVAM_KERNEL_ROI_DENSE : EVAM_KERNEL_ROI_WAVE;
-            continue;
-        }
-        if (path[f] == kPathRoiStrip) {
-            const RoiStripPlan& r = rsp[f];
-            TParams* tp = &h->sc_tparams;
-            tp->recs = reinterpret_cast<const RoiRec*>(d_dyn + rec_off[f]);
-            tp->mode = cfg->resize_mode;
-            tp->placement = cfg->placement;
-            tp->nstrips = r.nstrips;
-            tp->nbw = r.nbw;
-            tp->nw = r.nw;
-            tp->DW = DW; tp->DH = DH;
-            tp->wave_bytes = 2 * (2 + 2 * (f == kI420 ? 2 : 1)) * r.slot;
-            tp->lut = lut_d;
-            tp->dst = dst->data;
-            tp->slot_offset = dst->slot_offset;
-            tp->slot_stride = dst->slot_stride;
-            tp->color_rgb = color_rgb;
-            tp->fill = fill;
-            tp->prio = kn.prio;
-            hipError_t e = launch_roi_strip(f, cfg->out_dtype, r.px, r.slot, *tp, qrec[f], r.nw, r.lds, h->stream);
-            if (e != hipSuccess) return fail(EVAM_PP_ERR_HIP, "kernel launch failed: %s", hipGetErrorString(e));
-            launches++; kmask |= EVAM_KERNEL_ROI_STRIP;
+            launches++; kmask |= EVAM_KERNEL_ROI_DENSE;
             continue;
         }
         if (path[f] == kPathRoi) {

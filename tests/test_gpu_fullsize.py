@@ -93,19 +93,20 @@ def test_c2_bench_batch(evam, O, coracle, gpu, shape, monkeypatch):
     pp.close()
 
 
-@pytest.mark.parametrize("kernel", ["dense", "wave", "strip", "roi_tail1", "roi"])
+@pytest.mark.parametrize("kernel", ["dense", "dense_prio", "roi_tail1", "roi"])
 @pytest.mark.parametrize("seed", [0, 3])
 def test_c3_bench_roi_set(evam, O, coracle, gpu, seed, kernel, monkeypatch):
     """C3: bench.py's seeded ROI set (50 per frame, w 24..400, h 24..300) on 32 bench 1080p NV12 frames ->
-    1600x3x72x72 fp32 through the dense ROI kernel (the default), the ROI wave kernel (EVAM_PP_ROI_STRIP=3), the
-    strip kernel's ROI mode (EVAM_PP_ROI_STRIP=2) and the ROI kernel (EVAM_PP_ROI_STRIP=0),
+    1600x3x72x72 fp32 through the dense ROI kernel (the default; with progress-based priority) and the ROI kernel
+    (EVAM_PP_ROI_DENSE=0),
     with and without its tail split (EVAM_PP_ROI_TAIL: the 64 ROIs beyond 6 per CU as row tiles)."""
     import torch
 
-    if kernel in ("strip", "wave"):
-        monkeypatch.setenv("EVAM_PP_ROI_STRIP", "2" if kernel == "strip" else "3")
+    if kernel == "dense_prio":
+        monkeypatch.setenv("EVAM_PP_PRIO", "1")
+        kernel = "dense"
     elif kernel != "dense":
-        monkeypatch.setenv("EVAM_PP_ROI_STRIP", "0")
+        monkeypatch.setenv("EVAM_PP_ROI_DENSE", "0")
         monkeypatch.setenv("EVAM_PP_ROI_TAIL", "1" if kernel == "roi_tail1" else "4")
         kernel = "roi"
 
@@ -119,8 +120,7 @@ def test_c3_bench_roi_set(evam, O, coracle, gpu, seed, kernel, monkeypatch):
     pp.convert(imgs, out, info, rois=evam.RoiBatch(np.array(rois, dtype=np.int32)))
     torch.cuda.synchronize()
     N = evam.native
-    assert pp.stats().kernels == {"roi": N.KERNEL_ROI, "strip": N.KERNEL_ROI_STRIP, "wave": N.KERNEL_ROI_WAVE,
-                                  "dense": N.KERNEL_ROI_DENSE}[kernel]
+    assert pp.stats().kernels == {"roi": N.KERNEL_ROI, "dense": N.KERNEL_ROI_DENSE}[kernel]
     ref = oracle_items(O, coracle, host_frames(O, imgs), rois, out.shape, "f32", info)
     assert_same(out.cpu().numpy(), ref, f"C3 bench ROI set seed {seed} {kernel}")
     pp.close()

@@ -140,15 +140,14 @@ def test_roi_batch(evam, O, coracle, gpu, fmt):
     ((17, 5), "f32", "aspect-ratio", "top_left"),        # K=1, nfull=0
     ((64, 64), "f32", "aspect-ratio", "center"),         # R*DW = 256 exactly
 ])
-@pytest.mark.parametrize("roi_kernel", ["dense", "wave", "strip", "roi", "generic"])
+@pytest.mark.parametrize("roi_kernel", ["dense", "roi", "generic"])
 def test_roi_kernels(evam, O, coracle, gpu, fmt, dst, dtype, resize, placement, roi_kernel, monkeypatch):
-    """Per-item-geometry batches through the dense ROI kernel (4:2:0 default), the ROI wave kernel
-    (EVAM_PP_ROI_STRIP=3), the strip kernel's ROI mode (EVAM_PP_ROI_STRIP=2), the staged ROI kernel
-    (EVAM_PP_ROI_STRIP=0; packed formats' default) and the generic one (EVAM_PP_ROI=0)."""
+    """Per-item-geometry batches through the dense ROI kernel (4:2:0 default), the staged ROI kernel
+    (EVAM_PP_ROI_DENSE=0; packed formats' default) and the generic one (EVAM_PP_ROI=0)."""
     import torch
 
     monkeypatch.setenv("EVAM_PP_ROI", "0" if roi_kernel == "generic" else "1")
-    monkeypatch.setenv("EVAM_PP_ROI_STRIP", {"dense": "1", "wave": "3", "strip": "2"}.get(roi_kernel, "0"))
+    monkeypatch.setenv("EVAM_PP_ROI_DENSE", "1" if roi_kernel == "dense" else "0")
     rng = np.random.default_rng(zlib.crc32(f"{fmt}{dst}{resize}".encode()))
     W, H = 480, 270
     frames = [O.random_frame(rng, fc(O, fmt), W, H, pattern="gradient" if i else "uniform") for i in range(3)]
@@ -460,7 +459,7 @@ def test_roi_kernel_px4(evam, O, coracle, gpu, fmt, dst, dtype, monkeypatch):
     import torch
 
     monkeypatch.setenv("EVAM_PP_ROI_PX", "4")
-    monkeypatch.setenv("EVAM_PP_ROI_STRIP", "0")  # the ROI kernel (4:2:0 batches default to the strip kernel)
+    monkeypatch.setenv("EVAM_PP_ROI_DENSE", "0")  # the ROI kernel (4:2:0 batches default to the dense kernel)
     rng = np.random.default_rng(zlib.crc32(f"px4{fmt}{dst}".encode()))
     W, H = 320, 200
     frames = [O.random_frame(rng, fc(O, fmt), W, H, pattern="gradient" if i else "uniform") for i in range(2)]
@@ -483,7 +482,7 @@ def test_roi_kernel_xcd_order(evam, O, coracle, gpu, fmt, monkeypatch):
     import torch
 
     monkeypatch.setenv("EVAM_PP_ROI_XCD", "1")
-    monkeypatch.setenv("EVAM_PP_ROI_STRIP", "0")  # the ROI kernel (4:2:0 batches default to the strip kernel)
+    monkeypatch.setenv("EVAM_PP_ROI_DENSE", "0")  # the ROI kernel (4:2:0 batches default to the dense kernel)
     rng = np.random.default_rng(zlib.crc32(f"xcd{fmt}".encode()))
     W, H = 192, 108
     frames = [O.random_frame(rng, fc(O, fmt), W, H, pattern="gradient" if i % 2 else "uniform") for i in range(11)]
@@ -597,7 +596,7 @@ def test_roi_work_units(evam, O, coracle, gpu, unit, monkeypatch):
     import torch
 
     monkeypatch.setenv("EVAM_PP_ROI_UNIT", unit)
-    monkeypatch.setenv("EVAM_PP_ROI_STRIP", "0")  # the ROI kernel (4:2:0 batches default to the strip kernel)
+    monkeypatch.setenv("EVAM_PP_ROI_DENSE", "0")  # the ROI kernel (4:2:0 batches default to the dense kernel)
     rng = np.random.default_rng(zlib.crc32(f"unit{unit}".encode()))
     W, H = 640, 360
     frames = [O.random_frame(rng, O.NV12, W, H, pattern="gradient" if i else "uniform") for i in range(2)]
@@ -620,7 +619,7 @@ def test_roi_tail_split(evam, O, coracle, gpu, tail, dst, monkeypatch):
     import torch
 
     monkeypatch.setenv("EVAM_PP_ROI_TAIL", tail)
-    monkeypatch.setenv("EVAM_PP_ROI_STRIP", "0")  # the ROI kernel (4:2:0 batches default to the strip kernel)
+    monkeypatch.setenv("EVAM_PP_ROI_DENSE", "0")  # the ROI kernel (4:2:0 batches default to the dense kernel)
     rng = np.random.default_rng(zlib.crc32(f"tail{tail}{dst}".encode()))
     W, H = 640, 360
     frames = [O.random_frame(rng, O.NV12, W, H, pattern="gradient" if i else "uniform") for i in range(2)]
@@ -643,7 +642,7 @@ def test_roi_kernel_three_buffers(evam, O, coracle, gpu, fmt, buf, monkeypatch):
     import torch
 
     monkeypatch.setenv("EVAM_PP_ROI_NBUF", "3")
-    monkeypatch.setenv("EVAM_PP_ROI_STRIP", "0")  # the ROI kernel (4:2:0 batches default to the strip kernel)
+    monkeypatch.setenv("EVAM_PP_ROI_DENSE", "0")  # the ROI kernel (4:2:0 batches default to the dense kernel)
     if buf != "0":
         monkeypatch.setenv("EVAM_PP_ROI_BUF", buf)
     rng = np.random.default_rng(zlib.crc32(f"nb3{fmt}{buf}".encode()))
@@ -662,30 +661,31 @@ def test_roi_kernel_three_buffers(evam, O, coracle, gpu, fmt, buf, monkeypatch):
 
 
 @pytest.mark.parametrize("fmt", ["NV12", "I420"])
-@pytest.mark.parametrize("kernel", ["dense", "dense_ring", "wave", "wave_ring2", "strip"])
+@pytest.mark.parametrize("kernel", ["dense", "dense_ring", "dense_prio"])
 @pytest.mark.parametrize("dst,waves,resize", [
-    ((72, 72), "4", "no-aspect-ratio"),      # C3 shape: one 128-column strip, 4 row bands of 18
+    ((72, 72), "4", "no-aspect-ratio"),      # C3 shape: 4 row bands of 18, a 64-pixel step spans 2 rows
     ((72, 72), "1", "no-aspect-ratio"),      # one wave walks all 72 rows
     ((72, 72), "8", "aspect-ratio"),         # 8 bands of 9 rows, letterbox rows / columns
-    ((48, 300), "4", "no-aspect-ratio"),     # 64-column strips (PX 1), 300 rows: two row tiles of 256 / 44
-    ((300, 70), "4", "crop"),                # three 128-column strips x 1 band, aspect + central crop
-    ((520, 33), "8", "aspect-ratio"),        # five strips x 1 band, narrow letterboxed rows
-    ((16, 40), "2", "aspect-ratio"),         # dense: one step spans 5 rows
-    ((12, 20), "4", "no-aspect-ratio"),      # dense: 7 rows per step (the deepest span a ring takes)
+    ((48, 300), "4", "no-aspect-ratio"),     # 300 rows: two row tiles of 256 / 44
+    ((300, 70), "4", "crop"),                # aspect + central crop
+    ((520, 33), "8", "aspect-ratio"),        # narrow letterboxed rows, 8 bands of 4-5 rows
+    ((16, 40), "2", "aspect-ratio"),         # one step spans 5 rows
+    ((12, 20), "4", "no-aspect-ratio"),      # 7 rows per step (the deepest span a ring takes)
 ])
-def test_roi_strip_mode(evam, O, coracle, gpu, fmt, kernel, dst, waves, resize, monkeypatch):
-    """The ROI wave kernel (packed rings of any depth; wave_ring2: rings of the fewest bytes, two entries of the
-    widest footprint, so wide crops run 2-deep and narrow ones deeper) and the strip kernel's ROI mode
-    (EVAM_PP_ROI_STRIP=2), both resolving per-item geometry on the device from each RoiRec: every wave layout
-    (strips x row bands, EVAM_PP_ROI_STRIP_WAVES), row tiles for outputs taller than the bands hold, crops whose
-    footprints need 1 KB segments (up to ~900 px wide) next to tiny and partially outside ones, and every resize
-    mode; u8 and fp32 against the oracle."""
+def test_roi_dense_kernel(evam, O, coracle, gpu, fmt, kernel, dst, waves, resize, monkeypatch):
+    """The dense ROI kernel (per-item geometry resolved on the device from each RoiRec; each wave's band rows x DW
+    pixels walked 64 per step): every band layout (EVAM_PP_ROI_DENSE_WAVES), steps spanning up to 7 rows, row tiles
+    for outputs taller than the bands hold, crops whose footprints need two DMA instructions per plane (up to ~900 px
+    wide) next to tiny and partially outside ones, every resize mode, the fewest ring bytes (dense_ring: the widest
+    footprint runs the shallowest ring, narrow crops deeper) and progress-based priority (dense_prio); u8 and fp32
+    against the oracle."""
     import torch
 
-    monkeypatch.setenv("EVAM_PP_ROI_STRIP_WAVES", waves)
-    monkeypatch.setenv("EVAM_PP_ROI_STRIP", {"strip": "2", "wave": "3", "wave_ring2": "3"}.get(kernel, "1"))
-    if kernel in ("wave_ring2", "dense_ring"):
+    monkeypatch.setenv("EVAM_PP_ROI_DENSE_WAVES", waves)
+    if kernel == "dense_ring":
         monkeypatch.setenv("EVAM_PP_ROI_RING", "16")  # the fewest bytes: the widest footprint runs the shallowest ring
+    if kernel == "dense_prio":
+        monkeypatch.setenv("EVAM_PP_PRIO", "1")
     rng = np.random.default_rng(zlib.crc32(f"rs{fmt}{dst}{waves}{resize}".encode()))
     W, H = 1280, 720
     frames = [O.random_frame(rng, fc(O, fmt), W, H, pattern="gradient" if i else "uniform") for i in range(3)]
@@ -705,12 +705,12 @@ def test_roi_strip_mode(evam, O, coracle, gpu, fmt, kernel, dst, waves, resize, 
         tdt = torch.float32 if dtype == "f32" else torch.uint8
         got, _ = run_hip(evam, torch, upload(evam, frames, gpu), shape, tdt, info, rois=[evam.Roi(*r) for r in rois])
         ref, _ = run_oracle(O, coracle, frames, shape, dtype, info, rois=rois)
-        assert_same(got, ref, f"roi strip {fmt} {dst} waves={waves} {resize} {dtype}")
+        assert_same(got, ref, f"roi dense {kernel} {fmt} {dst} waves={waves} {resize} {dtype}")
 
 
-def test_roi_strip_mode_selected(evam, O, gpu, monkeypatch):
-    """4:2:0 ROI batches run on the strip kernel's ROI mode (one launch); packed formats keep the ROI kernel, and
-    EVAM_PP_ROI_STRIP=0 restores it for 4:2:0. Checked through the kernel families the library reports for the call
+def test_roi_dense_selected(evam, O, gpu, monkeypatch):
+    """4:2:0 ROI batches run on the dense ROI kernel (one launch); packed formats keep the ROI kernel, and
+    EVAM_PP_ROI_DENSE=0 restores it for 4:2:0. Checked through the kernel families the library reports for the call
     (evam_pp_stats.kernels)."""
     import torch
 
@@ -726,11 +726,10 @@ def test_roi_strip_mode_selected(evam, O, gpu, monkeypatch):
         st = pp.stats()
         assert st.n_launches == 1 and st.kernels == want, (fmt, st.kernels)
         pp.close()
-    for knob, want in (("3", N.KERNEL_ROI_WAVE), ("2", N.KERNEL_ROI_STRIP), ("0", N.KERNEL_ROI)):
-        monkeypatch.setenv("EVAM_PP_ROI_STRIP", knob)
-        pp = evam.HipPreProcessor(device=0)
-        out = torch.zeros((8, 3, 72, 72), dtype=torch.float32, device=gpu)
-        pp.convert(upload(evam, [O.random_frame(rng, O.NV12, 320, 240)] * 2, gpu), out, None, rois=rois)
-        torch.cuda.synchronize()
-        assert pp.stats().kernels == want, (knob, pp.stats().kernels)
-        pp.close()
+    monkeypatch.setenv("EVAM_PP_ROI_DENSE", "0")
+    pp = evam.HipPreProcessor(device=0)
+    out = torch.zeros((8, 3, 72, 72), dtype=torch.float32, device=gpu)
+    pp.convert(upload(evam, [O.random_frame(rng, O.NV12, 320, 240)] * 2, gpu), out, None, rois=rois)
+    torch.cuda.synchronize()
+    assert pp.stats().kernels == N.KERNEL_ROI
+    pp.close()
