@@ -1594,6 +1594,7 @@ struct TParams {
     int segY, segC;              // bytes of one staged luma / chroma row (multiples of 16)
     int nrY;                     // most luma rows of one band (the chroma rows follow at nrY * segY)
     int prio;                    // 1: progress-based wave priority (s_setprio 3 -> 0 over the quarters of a wave's rows)
+    int ahead;                   // band kernel: source rows issued ahead of the rows the current output row reads
 };
 static_assert(sizeof(TParams) <= 4000, "strip / band kernel arguments must fit the 4 KB kernarg segment");
 
@@ -2046,14 +2047,47 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_num_sgpr(96))) void evam
     const int pitch0 = (int)rec[6], pitch1 = (int)rec[7], pitch2 = (int)rec[8];
     const int index = (int)rec[14];
     EVAM_WSTAMP(7);  // the record arrived
-    Geom g;
-    roi_geometry(FMT, (int)(rec[9] & 0xFFFF), (int)(rec[9] >> 16), true, (int)rec[10], (int)rec[11], (int)rec[12],
-                 (int)rec[13], mode, placement, DW, DH, g);  // never empty: the host validated every item
-    const int x0 = __builtin_amdgcn_readfirstlane(g.x0), y0 = __builtin_amdgcn_readfirstlane(g.y0);
-    const int cw = __builtin_amdgcn_readfirstlane(g.cw), ch = __builtin_amdgcn_readfirstlane(g.ch);
-    const int rw = __builtin_amdgcn_readfirstlane(g.rw), rh = __builtin_amdgcn_readfirstlane(g.rh);
-    const int ox = __builtin_amdgcn_readfirstlane(g.ox), oy = __builtin_amdgcn_readfirstlane(g.oy);
-    const double scx = 1. / ((double)rw / cw), scy = 1. / ((double)rh / ch);
+    // One wave per workgroup resolves the item's geometry, scales and footprint (wave blockIdx mod nbw: the waves of a
+    // workgroup sit on different SIMDs, so a SIMD computes about 1/nbw of its workgroups' geometry — double divisions
+    // and the OpenCV coefficient sequence — instead of every one) and broadcasts it through LDS.
+    __shared__ __attribute__((aligned(16))) int geo_s[16];
+    if (wave == (int)(blockIdx.x % (unsigned)nbw)) {
+        Geom g;
+        roi_geometry(FMT, (int)(rec[9] & 0xFFFF), (int)(rec[9] >> 16), true, (int)rec[10], (int)rec[11], (int)rec[12],
+                     (int)rec[13], mode, placement, DW, DH, g);  // never empty: the host validated every item
+        const double sx = 1. / ((double)g.rw / g.cw), sy = 1. / ((double)g.rh / g.ch);
+        // footprint of the visible columns (crop-relative taps of the first and last)
+        const int Xv0 = max(0, g.ox), Xv1 = min(DW, g.ox + g.rw) - 1;
+        int fY = 0, cY = 0, fC = 0, cC = 0;
+        if (Xv0 <= Xv1) {
+            int sa, sb, c0, c1;
+            linear_coef(Xv0 - g.ox, sx, g.cw, true, sa, c0, c1);
+            linear_coef(Xv1 - g.ox, sx, g.cw, true, sb, c0, c1);
+            footprint_chunks(FMT, 1, g.x0 + sa, g.x0 + min(sb + 1, g.cw - 1), fY, cY, fC, cC);
+        }
+        if (lane == 0) {
+            const long long bx = __double_as_longlong(sx), by = __double_as_longlong(sy);
+            *reinterpret_cast<int4*>(geo_s) = int4{g.x0, g.y0, g.cw, g.ch};
+            *reinterpret_cast<int4*>(geo_s + 4) = int4{g.rw, g.rh, g.ox, g.oy};
+            *reinterpret_cast<int4*>(geo_s + 8) = int4{(int)bx, (int)(bx >> 32), (int)by, (int)(by >> 32)};
+            *reinterpret_cast<int4*>(geo_s + 12) = int4{fY, cY, fC, cC};
+        }
+    }
+    lds_barrier();
+    const int4 ga = *reinterpret_cast<const int4*>(geo_s), gb = *reinterpret_cast<const int4*>(geo_s + 4);
+    const int4 gc = *reinterpret_cast<const int4*>(geo_s + 8), gd = *reinterpret_cast<const int4*>(geo_s + 12);
+    const int x0 = __builtin_amdgcn_readfirstlane(ga.x), y0 = __builtin_amdgcn_readfirstlane(ga.y);
+    const int cw = __builtin_amdgcn_readfirstlane(ga.z), ch = __builtin_amdgcn_readfirstlane(ga.w);
+    const int rw = __builtin_amdgcn_readfirstlane(gb.x), rh = __builtin_amdgcn_readfirstlane(gb.y);
+    const int ox = __builtin_amdgcn_readfirstlane(gb.z), oy = __builtin_amdgcn_readfirstlane(gb.w);
+    const double scx = __longlong_as_double(((long long)(unsigned)__builtin_amdgcn_readfirstlane(gc.y) << 32) |
+                                            (unsigned)__builtin_amdgcn_readfirstlane(gc.x));
+    const double scy = __longlong_as_double(((long long)(unsigned)__builtin_amdgcn_readfirstlane(gc.w) << 32) |
+                                            (unsigned)__builtin_amdgcn_readfirstlane(gc.z));
+    const int fsY = __builtin_amdgcn_readfirstlane(gd.x), nY = __builtin_amdgcn_readfirstlane(gd.y);
+    const int fsC = __builtin_amdgcn_readfirstlane(gd.z), nC = __builtin_amdgcn_readfirstlane(gd.w);
+    const bool cols = nY > 0;
+    (void)rw;
     const int row0 = (int)(rec[15] & 0xFFFF), row1 = (int)(rec[15] >> 16);
 #ifdef EVAM_PP_TRACE
     asm volatile("" ::"v"(scx), "v"(scy));
@@ -2061,18 +2095,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_num_sgpr(96))) void evam
 #endif
     const int th = (row1 - row0 + nbw - 1) / nbw;
     const int Y0 = min(row0 + wave * th, row1), Y1 = min(Y0 + th, row1), rows = Y1 - Y0;  // rows <= 64 (host)
-    // footprint of the visible columns (crop-relative taps of the first and last)
-    const int Xv0 = max(0, ox), Xv1 = min(DW, ox + rw) - 1;
-    const bool cols = Xv0 <= Xv1;
-    int fsY = 0, nY = 0, fsC = 0, nC = 0;
-    if (cols) {
-        int sa, sb, c0, c1;
-        linear_coef(Xv0 - ox, scx, cw, true, sa, c0, c1);
-        linear_coef(Xv1 - ox, scx, cw, true, sb, c0, c1);
-        footprint_chunks(FMT, 1, x0 + sa, x0 + min(sb + 1, cw - 1), fsY, nY, fsC, nC);
-        fsY = __builtin_amdgcn_readfirstlane(fsY); nY = __builtin_amdgcn_readfirstlane(nY);
-        fsC = __builtin_amdgcn_readfirstlane(fsC); nC = __builtin_amdgcn_readfirstlane(nC);
-    }
     const int vr0 = max(Y0, oy), vr1 = min(Y1, oy + rh);
     const int n = cols && vr1 > vr0 ? vr1 - vr0 : 0;  // visible rows (the ring's rows)
     const int voff = vr0 - Y0;                          // band rows above the first visible row
@@ -2400,10 +2422,13 @@ __global__ __launch_bounds__(256) void evam_pp_band(const TParams P) {
     const int rlo = n ? __builtin_amdgcn_readlane(lr0, 0) : 0;
     const int rhi = n ? __builtin_amdgcn_readlane(lr1, n - 1) : -1;
     const int clo = (y0 + rlo) >> 1;
+    // The wave counts every vector-memory operation it issues (pos) and remembers pos right after each luma row's
+    // DMA (lane r - rlo of dpos), so every wait below is exact.
+    int pos = 0, dpos = 0;
     // fp32: the LUT (3 KB, sections in source channel order) by LDS-DMA ahead of the rows, so no VGPR waits
     // on it and the rows' counted waits are unaffected (it is older)
     if constexpr (OUT == 1) {
-        for (int c0 = wave * 64; c0 < 192; c0 += (int)(blockDim.x >> 6) * 64) {
+        for (int c0 = wave * 64; c0 < 192; c0 += (int)(blockDim.x >> 6) * 64, pos++) {
             const int c = c0 + lane, sec = c >> 6;
             const int src = ((k_rgb ? 2 - sec : sec) * 64 + (c & 63)) * 16;
             const __amdgpu_buffer_rsrc_t rsL = __builtin_amdgcn_make_buffer_rsrc((void*)k_lut, (short)0, 3072, 0x00020000);
@@ -2411,16 +2436,20 @@ __global__ __launch_bounds__(256) void evam_pp_band(const TParams P) {
                                                      16, (uint32_t)src, 0, 0, 0);
         }
     }
-    // DMA in need order: luma row r, then its chroma row when r is the first row reading it. Instructions
-    // issued up to row r: kd(r) = (r - rlo + 1) + NPC (c(r) - clo + 1).
-    if (n) {
+    const int lut_pos = pos;
+    // DMA in need order: luma row r, then its chroma row when r is the first row reading it. Rows go out up to
+    // `ahead` source rows past the last row the current output row reads (EVAM_PP_BAND_AHEAD; 64: the whole band
+    // at once), so a wave's first rows do not queue behind the rest of the band in the launch's opening burst.
+    int rnext = rlo, cprev = -1;
+    const int ahead = P.ahead;
+    auto issue_to = [&](int rmax) {
         const uint32_t vo = (uint32_t)lane * 16u;
-        int cprev = -1;
-        for (int r = rlo; r <= rhi; r++) {
-            const int ya = y0 + r, c = ya >> 1;
+        for (; rnext <= rmax; rnext++) {
+            const int r = rnext, ya = y0 + r, c = ya >> 1;
             if (lane < nY)
                 __builtin_amdgcn_raw_ptr_buffer_load_lds(rsY, (__attribute__((address_space(3))) void*)(wbuf + (r - rlo) * segY),
                                                          16, vo, ya * pitch0 + fsY, EVAM_PP_LOAD_AUX, 0);
+            pos++;
             if (c != cprev) {
                 uint8_t* cb = cbuf + (c - clo) * segC;
                 if (lane < nC) {
@@ -2430,17 +2459,19 @@ __global__ __launch_bounds__(256) void evam_pp_band(const TParams P) {
                         __builtin_amdgcn_raw_ptr_buffer_load_lds(rsV, (__attribute__((address_space(3))) void*)(cb + segC / 2),
                                                                  16, vo, c * pitch2 + fsC, EVAM_PP_LOAD_AUX, 0);
                 }
+                pos += NPC;
                 cprev = c;
             }
+            dpos = lane == r - rlo ? pos : dpos;
         }
-    }
-    const int kd_total = n ? (rhi - rlo + 1) + NPC * (((y0 + rhi) >> 1) - clo + 1) : 0;
+    };
+    if (n) issue_to(min(rhi, __builtin_amdgcn_readlane(lr1, 0) + ahead));
     EVAM_WSTAMP(1);
     EVAM_WTRACE_VAL(5, (unsigned long long)n << 48);
 
     if constexpr (OUT == 1) {
-        vmcnt_exact(kd_total);  // this wave's LUT pieces landed (issued before every row)
-        __syncthreads();        // ... and every other wave's
+        vmcnt_le(pos - lut_pos);  // this wave's LUT pieces landed (issued before every row)
+        lds_barrier();            // ... and every other wave's (LDS only: the rows' DMA stays in flight)
     }
     if (!live) return;
 
@@ -2499,7 +2530,10 @@ __global__ __launch_bounds__(256) void evam_pp_band(const TParams P) {
         for (int j = 0; j < PX; j++) { v[0][j] = fill0; v[1][j] = fill1; v[2][j] = fill2; }
         put(Y, v);
     };
-    for (int Y = Y0; Y < (n ? vr0 : Y1); Y++) put_fill(Y);  // letterbox rows above
+    for (int Y = Y0; Y < (n ? vr0 : Y1); Y++) {  // letterbox rows above
+        put_fill(Y);
+        pos += 3;
+    }
 
     uint32_t kb = kKBs, kg = kKGs, kr = kKRs;
     int cvg = kCVG, cug = kCUG;
@@ -2552,9 +2586,8 @@ __global__ __launch_bounds__(256) void evam_pp_band(const TParams P) {
         else if (i == pq2) __builtin_amdgcn_s_setprio(1);
         else if (i == pq3) __builtin_amdgcn_s_setprio(0);
         const int ra = __builtin_amdgcn_readlane(lr0, i), rb = __builtin_amdgcn_readlane(lr1, i);
-        // rows up to rb landed: issued after them, the DMA of later rows and the stores of rows 0 .. i-1
-        const int kd = (rb - rlo + 1) + NPC * (((y0 + rb) >> 1) - clo + 1);
-        vmcnt_exact(kd_total - kd + nst * i);
+        issue_to(rb);  // (issued already unless `ahead` is 0)
+        vmcnt_le(pos - __builtin_amdgcn_readlane(dpos, rb - rlo));  // rows up to rb landed
 #ifdef EVAM_PP_TRACE
         if (i == 0) {
             EVAM_WSTAMP(2);
@@ -2597,7 +2630,10 @@ __global__ __launch_bounds__(256) void evam_pp_band(const TParams P) {
             }
         }
         put(vr0 + i, v);
+        pos += nst;
         asm volatile("" ::: "memory");  // issue order is what the counted waits assume
+        if (i + 1 < n) issue_to(min(rhi, __builtin_amdgcn_readlane(lr1, i + 1) + ahead));
+        asm volatile("" ::: "memory");
     }
     for (int Y = max(n ? vr1 : Y1, Y0); Y < Y1; Y++) put_fill(Y);  // letterbox rows below
 #ifdef EVAM_PP_TRACE
@@ -3098,11 +3134,13 @@ struct Knobs {
                                                    // waves (row bands) per workgroup
     int roi_ring = -1;                             // dense ROI kernel: ring bytes per wave (-1: the LDS budget, <= 8 KB)
     int prio = 0;                                  // progress-based wave priority in the strip kernel
+    int band_ahead = 64;                           // band kernel: source rows issued ahead (64: the whole band at once)
     void read() {
         roi_dense = env_int("EVAM_PP_ROI_DENSE", roi_dense);
         roi_dense_waves = env_int("EVAM_PP_ROI_DENSE_WAVES", roi_dense_waves);
         roi_ring = env_int("EVAM_PP_ROI_RING", roi_ring);
         prio = env_int("EVAM_PP_PRIO", prio);
+        band_ahead = env_int("EVAM_PP_BAND_AHEAD", band_ahead);
         band = env_int("EVAM_PP_BAND", band); band_px = env_int("EVAM_PP_BAND_PX", band_px);
         strip = env_int("EVAM_PP_STRIP", strip); strip_th = env_int("EVAM_PP_STRIP_TH", strip_th);
         strip_waves = env_int("EVAM_PP_STRIP_WAVES", strip_waves);
@@ -3703,7 +3741,7 @@ bool plan_band(int f, const Geom& g, int DW, int DH, int count, int out_dtype, i
         p.wave_bytes = nrY * p.segY + (nrY / 2 + 1) * p.segC;
         nw = std::min(4, nstrips);  // a workgroup: up to four strips of one band
         lds = nw * p.wave_bytes + 16;  // + 16: a right-edge tap reads past its footprint (weight 0)
-        if (lds + lut_static <= 64 * 1024) break;
+        if (lds + lut_static <= 64 * 1024 && nrY <= 64) break;  // <= 64 rows: one lane of the wait table per row
         if (th == 1) return false;
     }
     p.TH = th;
@@ -4533,6 +4571,7 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
                     tp->color_rgb = color_rgb;
                     tp->fill = fill;
                     tp->prio = kn.prio;
+                    tp->ahead = std::max(0, kn.band_ahead);
                     for (int m0 = mfirst[f]; m0 < mfirst[f + 1]; m0 += kArgItems) {
                         const int nm = std::min(kArgItems, mfirst[f + 1] - m0);
                         fill_args(tp->items, m0, nm);
