@@ -1568,9 +1568,10 @@ static_assert(sizeof(RoiRec) == 64, "RoiRec layout");
 constexpr int kMaxStrips = 32;  // per-strip footprints in the kernel arguments: DW <= 2048
 constexpr int kSfoot = 64;      // footprint entries: strip kernel tile column x 8 + wave (<= 8 columns)
 // One staged row segment of the strip kernel: a strip's footprint is at most one DMA instruction's 64
-// 16-byte chunks, so every LDS offset of the ring is a compile-time immediate. 64-column strips (PX = 1)
-// use half-size slots (footprints <= 512 B, downscales <= ~7.7x): half the LDS per wave.
-constexpr int strip_slot(int px) { return px == 1 ? 512 : 1024; }
+// 16-byte chunks, so every LDS offset of the ring is a compile-time immediate. 64-column 4:2:0 strips (PX = 1)
+// use half-size slots (footprints <= 512 B, downscales <= ~7.7x): half the LDS per wave; BGRx rows are four
+// bytes a pixel and always take whole 1 KB slots.
+constexpr int strip_slot(int fmt, int px) { return px == 1 && fmt != kBGRX ? 512 : 1024; }
 
 struct TParams {
     ItemArg items[kArgItems];
@@ -1621,11 +1622,12 @@ __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
     // the LUT at a static LDS address (folds into the reads' immediate offsets); the rings after it
     __shared__ __attribute__((aligned(16))) float lut_s[OUT == 1 ? 768 : 4];
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    static_assert(FMT == kNV12 || FMT == kI420, "4:2:0 sources");
+    static_assert(FMT == kNV12 || FMT == kI420 || FMT == kBGRX, "4:2:0 or BGRx sources");
     static_assert(D >= 1 && D <= 4, "ring depth");
     static_assert(PX == 1 || PX == 2, "pixels per lane");
-    constexpr int SLOT = strip_slot(PX);
-    constexpr int NPC = FMT == kI420 ? 2 : 1;  // chroma planes
+    constexpr int SLOT = strip_slot(FMT, PX);
+    constexpr bool PK = FMT == kBGRX;                 // packed BGRx: one plane, 4 bytes a pixel, no conversion
+    constexpr int NPC = FMT == kI420 ? 2 : (PK ? 0 : 1);  // chroma planes
     constexpr int NMIN = 2 + NPC;              // fewest DMA instructions of one row (chroma row shared)
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1668,7 +1670,7 @@ __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
     const bool live = X0 < p_DW;  // a wave past the last strip only joins the LUT barrier
     const bool cols = live && sf.x >= 0;
     int fsY = 0, nY = 0, fsC = 0, nC = 0;
-    if (cols) footprint_chunks(FMT, 1, x0 + sf.x, x0 + sf.y, fsY, nY, fsC, nC);
+    if (cols) footprint_chunks(FMT, PK ? 4 : 1, x0 + sf.x, x0 + sf.y, fsY, nY, fsC, nC);
     // visible output rows of the tile (the rest are letterbox fill)
     const int vr0 = max(Y0, g_oy), vr1 = min(Y1, g_oy + g_rh);
     const int n = cols && vr1 > vr0 ? vr1 - vr0 : 0;
@@ -1687,7 +1689,8 @@ __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
     const __amdgpu_buffer_rsrc_t rsU = __builtin_amdgcn_make_buffer_rsrc((void*)p1, (short)0, 0x7FFFFFFF, 0x00020000);
     const __amdgpu_buffer_rsrc_t rsV = __builtin_amdgcn_make_buffer_rsrc((void*)(NPC == 2 ? p2 : p1), (short)0, 0x7FFFFFFF, 0x00020000);
     uint8_t* const wbuf = smem + wave * P.wave_bytes;
-    // ring entry: [Y tap0][Y tap1][C tap0][C tap1] (+ [V tap0][V tap1] for I420), SLOT bytes each
+    // ring entry: [Y tap0][Y tap1][C tap0][C tap1] (+ [V tap0][V tap1] for I420), SLOT bytes each; BGRx:
+    // [row tap0][row tap1]
     constexpr int SY = SLOT, SC = SLOT, GRP = 2 * SY + 2 * NPC * SC;
     constexpr int segY = SY, segC = SC;
     auto issue = [&](int i, int k) {
@@ -1701,6 +1704,7 @@ __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
             __builtin_amdgcn_raw_ptr_buffer_load_lds(rsY, (__attribute__((address_space(3))) void*)(e + segY), 16, vo,
                                                      yb * pitch0 + fsY, EVAM_PP_LOAD_AUX, 0);
         }
+        if constexpr (NPC == 0) return;
         const int ca = ya >> 1, cb = yb >> 1;
         if (lane < nC) {
             __builtin_amdgcn_raw_ptr_buffer_load_lds(rsU, (__attribute__((address_space(3))) void*)(e + 2 * segY), 16, vo,
@@ -1754,15 +1758,16 @@ __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
             int s0, a0, a1;
             linear_coef(dx, k_scale_x, g_cw, true, s0, a0, a1);
             const int ca = x0 + s0;  // tap 1 reads ca + 1: at the right edge (s0 = cw - 1) its weight a1 is 0
-            lY[j] = (uint32_t)(ca - fsY);
+            lY[j] = (uint32_t)(ca * (PK ? 4 : 1) - fsY);
             if constexpr (FMT == kNV12) {
                 lC0[j] = (uint32_t)(2 * (ca >> 1) - fsC);
                 lC1[j] = (uint32_t)(2 * ((ca + 1) >> 1) - fsC);
-            } else {
+            } else if constexpr (FMT == kI420) {
                 lC0[j] = (uint32_t)((ca >> 1) - fsC);
                 lC1[j] = (uint32_t)(((ca + 1) >> 1) - fsC);
             }
-            wp[j] = (uint32_t)a0 | ((uint32_t)a1 << 16);
+            // BGRx: the weights carry the 16x that the 4:2:0 path's saturating clamp leaves on its taps
+            wp[j] = PK ? ((uint32_t)a0 << 4) | ((uint32_t)a1 << 20) : (uint32_t)a0 | ((uint32_t)a1 << 16);
             padc[j] = false;
         }
         anyp |= xin[j] && padc[j];
@@ -1885,6 +1890,33 @@ __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
         const bool share = ((y0 + ya) >> 1) == ((y0 + yb) >> 1);
         if (kAblate & 2) {  // diagnostics: no pixel math (no tap reads)
             put_fill(Y);
+        } else if constexpr (PK) {
+            // BGRx: both taps of a source row are two adjacent dwords; channel c of the pair is one v_perm into
+            // two u16 halves, and the horizontal pass one v_dot2 with the 16x weights
+            const int eo = kk * GRP;
+#pragma unroll
+            for (int j = 0; j < PX; j++) {
+                const uint32_t* ay = reinterpret_cast<const uint32_t*>(aY[j] + eo);
+                const uint32_t qa0 = ay[0], qa1 = ay[1], qb0 = ay[SY / 4], qb1 = ay[SY / 4 + 1];
+                uint32_t v[3];
+#pragma unroll
+                for (int c = 0; c < 3; c++) {
+                    const uint32_t sel = 0x0C000C00u | ((uint32_t)(4 + c) << 16) | (uint32_t)c;
+                    const uint32_t ha = __builtin_amdgcn_udot2(
+                        __builtin_bit_cast(evam_u16x2, __builtin_amdgcn_perm(qa1, qa0, sel)),
+                        __builtin_bit_cast(evam_u16x2, wp[j]), 0u, false);
+                    const uint32_t hb = __builtin_amdgcn_udot2(
+                        __builtin_bit_cast(evam_u16x2, __builtin_amdgcn_perm(qb1, qb0, sel)),
+                        __builtin_bit_cast(evam_u16x2, wp[j]), 0u, false);
+                    v[c] = vfinal<OUT>(ha, hb, wb0, wb1);
+                }
+                if constexpr (PADC) {
+                    v[0] = padc[j] ? fill0 : v[0];
+                    v[1] = padc[j] ? fill1 : v[1];
+                    v[2] = padc[j] ? fill2 : v[2];
+                }
+                put(Y, j, v[0], v[1], v[2]);
+            }
         } else {
             const int eo = kk * GRP;  // this entry's offset from entry 0
             // raw taps of the entry into registers: luma bytes of both source rows, chroma of the first
@@ -3485,7 +3517,11 @@ const void* strip_fn(int f, int out, int d, int px) {
     case (kI420 * 2 + 0) * 2: return strip_fn_p<kI420, 0, 1>(d);
     case (kI420 * 2 + 0) * 2 + 1: return strip_fn_p<kI420, 0, 2>(d);
     case (kI420 * 2 + 1) * 2: return strip_fn_p<kI420, 1, 1>(d);
-    default: return strip_fn_p<kI420, 1, 2>(d);
+    case (kI420 * 2 + 1) * 2 + 1: return strip_fn_p<kI420, 1, 2>(d);
+    case (kBGRX * 2 + 0) * 2: return strip_fn_p<kBGRX, 0, 1>(d);
+    case (kBGRX * 2 + 0) * 2 + 1: return strip_fn_p<kBGRX, 0, 2>(d);
+    case (kBGRX * 2 + 1) * 2: return strip_fn_p<kBGRX, 1, 1>(d);
+    default: return strip_fn_p<kBGRX, 1, 2>(d);
     }
 }
 
@@ -3505,7 +3541,7 @@ const void* strip_fn(int f, int out, int d, int px) {
 // REUSE path).
 bool plan_strip(int f, const Geom& g, int DW, int DH, int count, int out_dtype, int n_cu, const XTab* xt,
                 const YTab* yt, uint32_t x0_mask, const Knobs& kn, TParams& p, int& D, int& px, int& lds, int& grid) {
-    if (f != kNV12 && f != kI420) return false;
+    if (f != kNV12 && f != kI420 && f != kBGRX) return false;
     int shared = 0, vis = 0;
     for (int Y = 0; Y + 1 < DH; Y++) {
         const bool pad0 = (yt[Y].b0 | yt[Y].b1) == 0, pad1 = (yt[Y + 1].b0 | yt[Y + 1].b1) == 0;
@@ -3515,7 +3551,7 @@ bool plan_strip(int f, const Geom& g, int DW, int DH, int count, int out_dtype, 
     }
     if (kn.strip != 2 && shared * 8 > vis) return false;  // more than 1 in 8 rows re-stages a row
     if (!x0_mask) x0_mask = 1u << (g.x0 & 31);
-    const int npc = f == kI420 ? 2 : 1;
+    const int npc = f == kI420 ? 2 : (f == kBGRX ? 0 : 1);
     int mY = 0, mC = 0;
     px = 0;
     for (int cand : {2, 1}) {
@@ -3525,13 +3561,13 @@ bool plan_strip(int f, const Geom& g, int DW, int DH, int count, int out_dtype, 
         // two 128-column ones (profiles/r03g_c5_px.txt)
         if (cand == 2 && (DW + 127) / 128 < 4 && kn.strip_px != 2) continue;
         wave_segments(f, g.ox, g.rw, DW, xt, x0_mask, 64 * cand, mY, mC);
-        const int cap = strip_slot(cand) / 16;  // chunks of one slot
+        const int cap = strip_slot(f, cand) / 16;  // chunks of one slot
         if (mY <= cap && mC <= cap) { px = cand; break; }
     }
     if (!px) return false;
     const int nstrips = (DW + 64 * px - 1) / (64 * px);
     if (nstrips > kMaxStrips) return false;
-    const int grp_bytes = (2 + 2 * npc) * strip_slot(px);  // one ring entry: 2 luma + 2 x npc chroma segments
+    const int grp_bytes = (2 + 2 * npc) * strip_slot(f, px);  // one ring entry: 2 luma + 2 x npc chroma segments
     int nw = 4, best = 1 << 30;
     for (int c = 4; c <= 8; c++) {
         const int idle = (nstrips + c - 1) / c * c - nstrips;
@@ -3592,7 +3628,11 @@ hipError_t launch_strip(int f, int out, int d, int px, const TParams& p, dim3 gr
     case (kI420 * 2 + 0) * 2: return launch_strip_t<kI420, 0, 1>(d, p, grid, lds, s);
     case (kI420 * 2 + 0) * 2 + 1: return launch_strip_t<kI420, 0, 2>(d, p, grid, lds, s);
     case (kI420 * 2 + 1) * 2: return launch_strip_t<kI420, 1, 1>(d, p, grid, lds, s);
-    default: return launch_strip_t<kI420, 1, 2>(d, p, grid, lds, s);
+    case (kI420 * 2 + 1) * 2 + 1: return launch_strip_t<kI420, 1, 2>(d, p, grid, lds, s);
+    case (kBGRX * 2 + 0) * 2: return launch_strip_t<kBGRX, 0, 1>(d, p, grid, lds, s);
+    case (kBGRX * 2 + 0) * 2 + 1: return launch_strip_t<kBGRX, 0, 2>(d, p, grid, lds, s);
+    case (kBGRX * 2 + 1) * 2: return launch_strip_t<kBGRX, 1, 1>(d, p, grid, lds, s);
+    default: return launch_strip_t<kBGRX, 1, 2>(d, p, grid, lds, s);
     }
 }
 

@@ -176,6 +176,33 @@ def test_c5_ring_step(evam, O, coracle, gpu, shape, monkeypatch):
     pp.close()
 
 
+@pytest.mark.parametrize("variant", ["strip", "strip_d1", "wave"])
+def test_c5_bgrx_ring_step(evam, O, coracle, gpu, variant, monkeypatch):
+    """C5 with BGRx sources (bench.py c5_bgrx: 32 x 768x432 BGRx -> aspect(max) -> central crop 224x224 fp32 into
+    ring slot t % 16): the strip kernel's packed-format path (the default), and the wave kernel it replaced."""
+    import torch
+
+    monkeypatch.setenv("EVAM_PP_STRIP", "0" if variant == "wave" else "1")
+    if variant == "strip_d1":
+        monkeypatch.setenv("EVAM_PP_STRIP_D", "1")
+    N = evam.native
+    wl = bench.WORKLOADS["c5_bgrx"]
+    info = bench.make_info(evam, wl)
+    ring = torch.full((32 * 16, 3, 224, 224), 7, dtype=torch.float32, device=gpu)
+    pp = evam.HipPreProcessor(device=0)
+    t = 3
+    imgs = bench.device_frames(evam, torch, wl, 32, gpu, seed=4321)
+    pp.convert(imgs, ring, info, slot_offset=t, slot_stride=16)
+    torch.cuda.synchronize()
+    want = N.KERNEL_WAVE if variant == "wave" else N.KERNEL_STRIP
+    assert pp.stats().kernels == want, (variant, pp.stats().kernels)
+    got = ring[[s * 16 + t for s in range(32)]].cpu().numpy()
+    ref = oracle_items(O, coracle, host_frames(O, imgs), [(s, 0, 0, 0, 0) for s in range(32)],
+                       (32, 3, 224, 224), "f32", info)
+    assert_same(got, ref, f"C5 BGRx ring step {variant}")
+    pp.close()
+
+
 @pytest.mark.parametrize("config", ["c5", "c2"])
 def test_inflight_two_streams_bit_equal(evam, gpu, config):
     """bench.py --inflight 2: successive launches alternate between two handles bound to two HIP streams (their
