@@ -557,10 +557,12 @@ def main():
         if feed is not None:
             res["h2d"] = {"bytes_per_step": feed.bytes_per_batch, "frame_bytes": feed.frame_bytes,
                           "rows": args.feed_rows,
+                          "copy": "strided" if feed.strided else "contiguous",
                           "GBps": round(feed.bytes_per_batch * args.steps / wall_max / 1e9, 2),
                           "note": "frames copied from pinned host memory every step on a copy stream, overlapped "
                                   "with the kernel (depth-3 ring; rows=touched: only the source rows the resize "
-                                  "reads, strided 2-D copies); roofline.mean_launch_ms includes copy waits"}
+                                  "reads, as strided 2-D copies unless they cover >= 85% of the frame); "
+                                  "roofline.mean_launch_ms includes copy waits"}
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(wl, args.cpu_budget)
         else:

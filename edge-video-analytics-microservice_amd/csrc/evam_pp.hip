@@ -2697,6 +2697,7 @@ struct QParams {
     int buf_bytes;            // one staging buffer
     int color_rgb;
     uint32_t fill;
+    int prio;                 // progress-based priority (as the strip kernel's), over the quarters of the row groups
 };
 
 
@@ -3039,8 +3040,17 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(96))) void
     };
 
 
+    // progress-based priority (EVAM_PP_PRIO): 3 -> 0 over the quarters of the workgroup's row groups
+    const int pg1 = P.prio ? ngroups / 4 : -1, pg2 = P.prio ? ngroups / 2 : -1, pg3 = P.prio ? (3 * ngroups) / 4 : -1;
+    if (P.prio) __builtin_amdgcn_s_setprio(3);
+    auto step_prio = [&](int grp) {
+        if (grp == pg1) __builtin_amdgcn_s_setprio(2);
+        else if (grp == pg2) __builtin_amdgcn_s_setprio(1);
+        else if (grp == pg3) __builtin_amdgcn_s_setprio(0);
+    };
     if constexpr (NB == 2) {
     for (int grp = 0; grp < ngroups; grp++) {
+        step_prio(grp);
         // Wait for this wave's share of group grp's DMA. Group grp-1 was full (only the last group can
         // be partial), so this wave issued at least 3 stores for each of its nk_w store steps after
         // that DMA: those may stay in flight.
@@ -3063,6 +3073,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(96))) void
     uint8_t* bc = buf0;  // buffer of group grp
     uint8_t* bn = buf2;  // buffer of group grp + 2
     for (int grp = 0; grp < ngroups; grp++) {
+        step_prio(grp);
         vmcnt_at_most(nd_ahead + (grp >= 1 ? 3 * nk_w : 0) + (grp >= 2 ? 3 * nk_w : 0));
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();  // every wave's DMA for grp landed; every wave done reading grp-1
@@ -3162,17 +3173,21 @@ struct Knobs {
                                                                               // rows per tile, ring depth, waves, px
     int strip_waves = 16;                          // strip / band kernels: resident waves per CU the tiles are sized for
     int band = 1, band_px = 0;                     // band kernel: allowed (2: forced), pixels per lane
-    int roi_dense = 1, roi_dense_waves = 4;        // 4:2:0 ROI batches on the dense ROI kernel (0: the ROI kernel); its
-                                                   // waves (row bands) per workgroup
+    int roi_dense = 0, roi_dense_waves = 4;        // 4:2:0 ROI batches on the dense ROI kernel (1) or the ROI kernel (0,
+                                                   // C3: 52.8 vs 61.0 us, profiles/r04k_ab_lines.txt); its waves per workgroup
     int roi_ring = -1;                             // dense ROI kernel: ring bytes per wave (-1: the LDS budget, <= 8 KB)
-    int prio = 0;                                  // progress-based wave priority in the strip kernel
-    int band_ahead = 64;                           // band kernel: source rows issued ahead (64: the whole band at once)
+    int prio = 1;                                  // progress-based wave priority (strip, band, ROI kernels): C2 +3 %,
+                                                   // C4 +3 %, C5 +3-5 %, C1 +9 % (profiles/r04k_ab_lines.txt)
+    int roi_copy = 0;                              // ROI records copied to device memory before the launch (1)
+    int band_ahead = 2;                            // band kernel: source rows issued ahead of the current output row's
+                                                   // (64: the whole band at once; 2 measured +2 % on C1)
     void read() {
         roi_dense = env_int("EVAM_PP_ROI_DENSE", roi_dense);
         roi_dense_waves = env_int("EVAM_PP_ROI_DENSE_WAVES", roi_dense_waves);
         roi_ring = env_int("EVAM_PP_ROI_RING", roi_ring);
         prio = env_int("EVAM_PP_PRIO", prio);
         band_ahead = env_int("EVAM_PP_BAND_AHEAD", band_ahead);
+        roi_copy = env_int("EVAM_PP_ROI_COPY", roi_copy);
         band = env_int("EVAM_PP_BAND", band); band_px = env_int("EVAM_PP_BAND_PX", band_px);
         strip = env_int("EVAM_PP_STRIP", strip); strip_th = env_int("EVAM_PP_STRIP_TH", strip_th);
         strip_waves = env_int("EVAM_PP_STRIP_WAVES", strip_waves);
@@ -4060,6 +4075,7 @@ void evam_pp_destroy(evam_pp* h) {
     if (h->ring.have_copy || h->pin.cur >= 0) {
         (void)hipStreamSynchronize(h->stream);
         if (h->ring.have_copy) (void)hipStreamSynchronize(h->ring.copy);
+        if (h->pin.have_copy) (void)hipStreamSynchronize(h->pin.copy);
     }
     HipRings b;
     h->ring.release(b);
@@ -4501,6 +4517,10 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
     {
         HipRings b;
         if (int rc = h->ring.upload(b, h->stream, h->h_block.data(), h->h_block.size(), &d_block)) return rc;
+        // EVAM_PP_ROI_COPY: the records travel to a device mirror of their slot (one small copy on the copy
+        // stream, overlapping the previous call's kernel) instead of being read over PCIe by every workgroup
+        if (any_roi && kn.roi_copy && dyn_bytes > 0)
+            if (int rc = h->pin.mirror(b, h->stream, dyn_bytes, &d_dyn)) return rc;
     }
     HP(9);
 
@@ -4557,6 +4577,7 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
             q.slot_stride = dst->slot_stride;
             q.color_rgb = color_rgb;
             q.fill = fill;
+            q.prio = kn.prio;
             const int64_t grid = qrec[f];
             if (grid > 0x7FFFFFFF) return fail(EVAM_PP_ERR_INVALID_ARG, "evam_pp_run: too many tiles");
             hipError_t e = launch_roi(f, cfg->out_dtype, kn.roi_px, kn.roi_nbuf, q, (int)grid, qlds[f], h->stream);

@@ -10,7 +10,8 @@ them. ``HostFeed`` is a ring of ``depth`` batch slots. Each slot has:
 One slot moves on a dedicated copy stream: by default as ONE ``hipMemcpyAsync`` of the whole batch; after
 ``set_geometry`` (the pre-processing the batch will get) only the source rows the resize reads cross PCIe —
 the row table's touched luma rows and their chroma rows, as strided ``hipMemcpy2DAsync`` runs per frame and
-plane (C4: 720 of 2,160 luma rows, a third of every frame). The kernels read exactly those rows, so the
+plane (C4: 720 of 2,160 luma rows, a third of every frame), unless they cover >= 85% of the frame (C2), where
+the one contiguous copy is faster. The kernels read exactly those rows, so the
 rows left stale on the device are never used. The copies overlap the pre-process kernel of the previous
 slot on the compute stream, with events in both directions:
 - ``copied[k]``: the compute stream waits on it before the kernel reads slot k;
@@ -114,6 +115,8 @@ def copy_runs(rows: list[int], max_cmds: int = 8) -> list[tuple[int, int, int, i
 
 
 class HostFeed:
+    whole_copy_fraction = 0.85  # touched bytes / frame bytes at or above which one contiguous copy is used
+
     def __init__(self, fourcc, width: int, height: int, batch: int, depth: int = 3, device: int = 0,
                  pitch_align: int = 64):
         import torch
@@ -149,8 +152,17 @@ class HostFeed:
         for (r, p), pr in zip(self.layout, rows):
             plan.append((off, p, copy_runs(pr)))
             off += r * p
-        self._plan = plan
         self.rows_per_plane = [len(r) for r in rows]
+        planned = sum(p * l * k for _, p, cmds in plan for _, l, _, k in cmds)
+        # Strided copies pay per command: when they would move most of the frame anyway (C2: 1080 -> 512 reads
+        # 1,024 of 1,080 rows, one span per plane), one contiguous copy of the batch is faster (55 vs 42 GB/s,
+        # profiles/r04k_ab_lines.txt)
+        self._plan = None if planned >= self.whole_copy_fraction * self.frame_bytes else plan
+
+    @property
+    def strided(self) -> bool:
+        """True when submit() copies only the planned rows (strided 2-D copies), False for one contiguous copy."""
+        return self._plan is not None
 
     @property
     def bytes_per_batch(self) -> int:

@@ -49,7 +49,7 @@ def test_feed_rejects_oversize_batch(evam, O, gpu):
 
 @pytest.mark.parametrize("fmt,resize,src,dst", [("NV12", "aspect-ratio", (384, 216), (64, 64)),
                                                 ("I420", "no-aspect-ratio", (200, 120), (40, 20)),
-                                                ("NV12", "crop", (320, 180), (48, 48)),
+                                                ("NV12", "crop", (320, 192), (48, 48)),
                                                 ("BGRX", "no-aspect-ratio", (120, 96), (30, 24))])
 def test_feed_touched_rows_only(evam, O, coracle, gpu, fmt, resize, src, dst):
     """set_geometry: only the rows the resize reads cross PCIe (strided 2-D copies); the device slots start
@@ -64,7 +64,7 @@ def test_feed_touched_rows_only(evam, O, coracle, gpu, fmt, resize, src, dst):
     feed.set_geometry(DW, DH, info)
     for d in feed.dev:
         d.fill_(0xA5)
-    assert feed.bytes_per_batch < B * feed.frame_bytes
+    assert feed.strided and feed.bytes_per_batch < B * feed.frame_bytes
     pp = evam.HipPreProcessor(device=0)
     lut = O.np_norm_lut(1, (0.0, 1.0))
     rng = np.random.default_rng(5)

@@ -33,13 +33,14 @@ def oracle_items(O, coracle, frames, items, out_shape, dtype, info, slot=lambda 
     return ref
 
 
-@pytest.mark.parametrize("shape", ["default", "band_px2", "band_th16", "wave"])
+@pytest.mark.parametrize("shape", ["default", "band_px2", "band_th16", "ahead64", "noprio", "wave"])
 def test_c1_bench_batch(evam, O, coracle, gpu, shape, monkeypatch):
     """C1: 32 x 768x432 NV12 -> 32x3x512x512 u8, bench frames: the band kernel (default; 2 pixels per lane;
     16-row bands) and the wave kernel's REUSE path (EVAM_PP_WAVE=2)."""
     import torch
 
     for k, v in {"default": {}, "band_px2": {"EVAM_PP_BAND_PX": "2"}, "band_th16": {"EVAM_PP_STRIP_TH": "16"},
+                 "ahead64": {"EVAM_PP_BAND_AHEAD": "64"}, "noprio": {"EVAM_PP_PRIO": "0"},
                  "wave": {"EVAM_PP_WAVE": "2"}}[shape].items():
         monkeypatch.setenv(k, v)
 
@@ -93,20 +94,22 @@ def test_c2_bench_batch(evam, O, coracle, gpu, shape, monkeypatch):
     pp.close()
 
 
-@pytest.mark.parametrize("kernel", ["dense", "dense_prio", "roi_tail1", "roi"])
+@pytest.mark.parametrize("kernel", ["dense", "dense_noprio", "roi_tail1", "roi", "roi_noprio", "roi_copy"])
 @pytest.mark.parametrize("seed", [0, 3])
 def test_c3_bench_roi_set(evam, O, coracle, gpu, seed, kernel, monkeypatch):
     """C3: bench.py's seeded ROI set (50 per frame, w 24..400, h 24..300) on 32 bench 1080p NV12 frames ->
-    1600x3x72x72 fp32 through the dense ROI kernel (the default; with progress-based priority) and the ROI kernel
-    (EVAM_PP_ROI_DENSE=0),
-    with and without its tail split (EVAM_PP_ROI_TAIL: the 64 ROIs beyond 6 per CU as row tiles)."""
+    1600x3x72x72 fp32 through the ROI kernel (the default), with and without its tail split (EVAM_PP_ROI_TAIL: the 64
+    ROIs beyond 6 per CU as row tiles), and the dense ROI kernel (EVAM_PP_ROI_DENSE=1); both with and without
+    progress-based priority (EVAM_PP_PRIO)."""
     import torch
 
-    if kernel == "dense_prio":
-        monkeypatch.setenv("EVAM_PP_PRIO", "1")
-        kernel = "dense"
-    elif kernel != "dense":
-        monkeypatch.setenv("EVAM_PP_ROI_DENSE", "0")
+    if kernel.endswith("_noprio"):
+        monkeypatch.setenv("EVAM_PP_PRIO", "0")
+        kernel = kernel[:-7]
+    if kernel == "roi_copy":  # the records from their device mirror
+        monkeypatch.setenv("EVAM_PP_ROI_COPY", "1")
+    monkeypatch.setenv("EVAM_PP_ROI_DENSE", "1" if kernel == "dense" else "0")
+    if kernel != "dense":
         monkeypatch.setenv("EVAM_PP_ROI_TAIL", "1" if kernel == "roi_tail1" else "4")
         kernel = "roi"
 

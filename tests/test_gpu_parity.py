@@ -366,7 +366,8 @@ def test_stats_and_timing(evam, O, gpu):
 @pytest.mark.parametrize("variant", ["auto", "wave", "px1", "px2", "noreuse", "staged", "staged_xcd", "staged_r1",
                                      "staged_wide", "staged_b3", "staged_slot2k", "strip", "strip_d1", "strip_d2", "strip_d3",
                                      "strip_th5", "strip_nw8", "strip_xcd", "strip_px1", "strip_px2",
-                                     "strip_px2_d4_th7", "band", "band_px1", "band_px2", "band_th5", "band_th64"])
+                                     "strip_px2_d4_th7", "strip_noprio", "band", "band_px1", "band_px2", "band_th5",
+                                     "band_th64", "band_ahead64", "band_noprio"])
 def test_wave_kernel_variants(evam, O, coracle, gpu, fmt, src, dst, resize, variant, monkeypatch):
     """Uniform-geometry batches through the default kernel choice, the wave-row kernel forced
     (EVAM_PP_WAVE=2; every PX / REUSE choice), the staged kernel (EVAM_PP_WAVE=0 EVAM_PP_STRIP=0; with the
@@ -396,7 +397,10 @@ def test_wave_kernel_variants(evam, O, coracle, gpu, fmt, src, dst, resize, vari
            "band": {"EVAM_PP_BAND": "2"}, "band_px1": {"EVAM_PP_BAND": "2", "EVAM_PP_BAND_PX": "1"},
            "band_px2": {"EVAM_PP_BAND": "2", "EVAM_PP_BAND_PX": "2"},
            "band_th5": {"EVAM_PP_BAND": "2", "EVAM_PP_STRIP_TH": "5"},
-           "band_th64": {"EVAM_PP_BAND": "2", "EVAM_PP_STRIP_TH": "64"}}.get(variant, {})
+           "band_th64": {"EVAM_PP_BAND": "2", "EVAM_PP_STRIP_TH": "64"},
+           "strip_noprio": {"EVAM_PP_STRIP": "2", "EVAM_PP_PRIO": "0"},
+           "band_ahead64": {"EVAM_PP_BAND": "2", "EVAM_PP_BAND_AHEAD": "64", "EVAM_PP_STRIP_TH": "20"},
+           "band_noprio": {"EVAM_PP_BAND": "2", "EVAM_PP_PRIO": "0"}}.get(variant, {})
     if variant.startswith(("staged", "band")):
         env["EVAM_PP_STRIP"] = "0"
     for k, v in env.items():
@@ -417,11 +421,14 @@ def test_wave_kernel_variants(evam, O, coracle, gpu, fmt, src, dst, resize, vari
         assert_same(got, ref, f"wave {fmt} {src}->{dst} {resize} {variant} {dtype}")
 
 
-def test_stream_switch_and_descriptor_churn(evam, O, coracle, gpu):
+@pytest.mark.parametrize("roi_copy", ["0", "1"])
+def test_stream_switch_and_descriptor_churn(evam, O, coracle, gpu, roi_copy, monkeypatch):
     """Descriptor slots stay valid across torch stream switches and many changing ROI sets / geometries
-    (the upload ring and the pinned ROI ring wrap; slot fences, one per run of ROI slots, follow the stream)."""
+    (the upload ring and the pinned ROI ring wrap; slot fences, one per run of ROI slots, follow the stream), with
+    the ROI records read from pinned memory or from their device mirror (EVAM_PP_ROI_COPY=1)."""
     import torch
 
+    monkeypatch.setenv("EVAM_PP_ROI_COPY", roi_copy)
     rng = np.random.default_rng(11)
     frames = [O.random_frame(rng, O.NV12, 320, 180) for _ in range(2)]
     imgs = upload(evam, frames, gpu)
@@ -459,7 +466,7 @@ def test_roi_kernel_px4(evam, O, coracle, gpu, fmt, dst, dtype, monkeypatch):
     import torch
 
     monkeypatch.setenv("EVAM_PP_ROI_PX", "4")
-    monkeypatch.setenv("EVAM_PP_ROI_DENSE", "0")  # the ROI kernel (4:2:0 batches default to the dense kernel)
+    monkeypatch.setenv("EVAM_PP_ROI_DENSE", "0")  # the ROI kernel (the default; pinned against a default change)
     rng = np.random.default_rng(zlib.crc32(f"px4{fmt}{dst}".encode()))
     W, H = 320, 200
     frames = [O.random_frame(rng, fc(O, fmt), W, H, pattern="gradient" if i else "uniform") for i in range(2)]
@@ -482,7 +489,7 @@ def test_roi_kernel_xcd_order(evam, O, coracle, gpu, fmt, monkeypatch):
     import torch
 
     monkeypatch.setenv("EVAM_PP_ROI_XCD", "1")
-    monkeypatch.setenv("EVAM_PP_ROI_DENSE", "0")  # the ROI kernel (4:2:0 batches default to the dense kernel)
+    monkeypatch.setenv("EVAM_PP_ROI_DENSE", "0")  # the ROI kernel (the default; pinned against a default change)
     rng = np.random.default_rng(zlib.crc32(f"xcd{fmt}".encode()))
     W, H = 192, 108
     frames = [O.random_frame(rng, fc(O, fmt), W, H, pattern="gradient" if i % 2 else "uniform") for i in range(11)]
@@ -596,7 +603,7 @@ def test_roi_work_units(evam, O, coracle, gpu, unit, monkeypatch):
     import torch
 
     monkeypatch.setenv("EVAM_PP_ROI_UNIT", unit)
-    monkeypatch.setenv("EVAM_PP_ROI_DENSE", "0")  # the ROI kernel (4:2:0 batches default to the dense kernel)
+    monkeypatch.setenv("EVAM_PP_ROI_DENSE", "0")  # the ROI kernel (the default; pinned against a default change)
     rng = np.random.default_rng(zlib.crc32(f"unit{unit}".encode()))
     W, H = 640, 360
     frames = [O.random_frame(rng, O.NV12, W, H, pattern="gradient" if i else "uniform") for i in range(2)]
@@ -619,7 +626,7 @@ def test_roi_tail_split(evam, O, coracle, gpu, tail, dst, monkeypatch):
     import torch
 
     monkeypatch.setenv("EVAM_PP_ROI_TAIL", tail)
-    monkeypatch.setenv("EVAM_PP_ROI_DENSE", "0")  # the ROI kernel (4:2:0 batches default to the dense kernel)
+    monkeypatch.setenv("EVAM_PP_ROI_DENSE", "0")  # the ROI kernel (the default; pinned against a default change)
     rng = np.random.default_rng(zlib.crc32(f"tail{tail}{dst}".encode()))
     W, H = 640, 360
     frames = [O.random_frame(rng, O.NV12, W, H, pattern="gradient" if i else "uniform") for i in range(2)]
@@ -642,7 +649,7 @@ def test_roi_kernel_three_buffers(evam, O, coracle, gpu, fmt, buf, monkeypatch):
     import torch
 
     monkeypatch.setenv("EVAM_PP_ROI_NBUF", "3")
-    monkeypatch.setenv("EVAM_PP_ROI_DENSE", "0")  # the ROI kernel (4:2:0 batches default to the dense kernel)
+    monkeypatch.setenv("EVAM_PP_ROI_DENSE", "0")  # the ROI kernel (the default; pinned against a default change)
     if buf != "0":
         monkeypatch.setenv("EVAM_PP_ROI_BUF", buf)
     rng = np.random.default_rng(zlib.crc32(f"nb3{fmt}{buf}".encode()))
@@ -661,7 +668,7 @@ def test_roi_kernel_three_buffers(evam, O, coracle, gpu, fmt, buf, monkeypatch):
 
 
 @pytest.mark.parametrize("fmt", ["NV12", "I420"])
-@pytest.mark.parametrize("kernel", ["dense", "dense_ring", "dense_prio"])
+@pytest.mark.parametrize("kernel", ["dense", "dense_ring", "dense_noprio"])
 @pytest.mark.parametrize("dst,waves,resize", [
     ((72, 72), "4", "no-aspect-ratio"),      # C3 shape: 4 row bands of 18, a 64-pixel step spans 2 rows
     ((72, 72), "1", "no-aspect-ratio"),      # one wave walks all 72 rows
@@ -677,15 +684,16 @@ def test_roi_dense_kernel(evam, O, coracle, gpu, fmt, kernel, dst, waves, resize
     pixels walked 64 per step): every band layout (EVAM_PP_ROI_DENSE_WAVES), steps spanning up to 7 rows, row tiles
     for outputs taller than the bands hold, crops whose footprints need two DMA instructions per plane (up to ~900 px
     wide) next to tiny and partially outside ones, every resize mode, the fewest ring bytes (dense_ring: the widest
-    footprint runs the shallowest ring, narrow crops deeper) and progress-based priority (dense_prio); u8 and fp32
+    footprint runs the shallowest ring, narrow crops deeper) and without progress-based priority (dense_noprio); u8 and fp32
     against the oracle."""
     import torch
 
+    monkeypatch.setenv("EVAM_PP_ROI_DENSE", "1")
     monkeypatch.setenv("EVAM_PP_ROI_DENSE_WAVES", waves)
     if kernel == "dense_ring":
         monkeypatch.setenv("EVAM_PP_ROI_RING", "16")  # the fewest bytes: the widest footprint runs the shallowest ring
-    if kernel == "dense_prio":
-        monkeypatch.setenv("EVAM_PP_PRIO", "1")
+    if kernel == "dense_noprio":
+        monkeypatch.setenv("EVAM_PP_PRIO", "0")
     rng = np.random.default_rng(zlib.crc32(f"rs{fmt}{dst}{waves}{resize}".encode()))
     W, H = 1280, 720
     frames = [O.random_frame(rng, fc(O, fmt), W, H, pattern="gradient" if i else "uniform") for i in range(3)]
@@ -709,14 +717,15 @@ def test_roi_dense_kernel(evam, O, coracle, gpu, fmt, kernel, dst, waves, resize
 
 
 def test_roi_dense_selected(evam, O, gpu, monkeypatch):
-    """4:2:0 ROI batches run on the dense ROI kernel (one launch); packed formats keep the ROI kernel, and
-    EVAM_PP_ROI_DENSE=0 restores it for 4:2:0. Checked through the kernel families the library reports for the call
-    (evam_pp_stats.kernels)."""
+    """With EVAM_PP_ROI_DENSE=1, 4:2:0 ROI batches run on the dense ROI kernel (one launch) and packed formats keep
+    the ROI kernel; by default (measured faster on C3) every format runs the ROI kernel. Checked through the kernel
+    families the library reports for the call (evam_pp_stats.kernels)."""
     import torch
 
     N = evam.native
     rng = np.random.default_rng(4)
     rois = [evam.Roi(i % 2, 10 * i, 5 * i, 50 + i, 40 + 2 * i) for i in range(8)]
+    monkeypatch.setenv("EVAM_PP_ROI_DENSE", "1")
     for fmt, want in (("NV12", N.KERNEL_ROI_DENSE), ("I420", N.KERNEL_ROI_DENSE), ("BGRX", N.KERNEL_ROI)):
         frames = [O.random_frame(rng, fc(O, fmt), 320, 240) for _ in range(2)]
         out = torch.zeros((8, 3, 72, 72), dtype=torch.float32, device=gpu)
@@ -726,7 +735,7 @@ def test_roi_dense_selected(evam, O, gpu, monkeypatch):
         st = pp.stats()
         assert st.n_launches == 1 and st.kernels == want, (fmt, st.kernels)
         pp.close()
-    monkeypatch.setenv("EVAM_PP_ROI_DENSE", "0")
+    monkeypatch.delenv("EVAM_PP_ROI_DENSE")
     pp = evam.HipPreProcessor(device=0)
     out = torch.zeros((8, 3, 72, 72), dtype=torch.float32, device=gpu)
     pp.convert(upload(evam, [O.random_frame(rng, O.NV12, 320, 240)] * 2, gpu), out, None, rois=rois)
