@@ -3178,7 +3178,6 @@ struct Knobs {
     int roi_ring = -1;                             // dense ROI kernel: ring bytes per wave (-1: the LDS budget, <= 8 KB)
     int prio = 1;                                  // progress-based wave priority (strip, band, ROI kernels): C2 +3 %,
                                                    // C4 +3 %, C5 +3-5 %, C1 +9 % (profiles/r04k_ab_lines.txt)
-    int roi_copy = 0;                              // ROI records copied to device memory before the launch (1)
     int band_ahead = 2;                            // band kernel: source rows issued ahead of the current output row's
                                                    // (64: the whole band at once; 2 measured +2 % on C1)
     void read() {
@@ -3187,7 +3186,6 @@ struct Knobs {
         roi_ring = env_int("EVAM_PP_ROI_RING", roi_ring);
         prio = env_int("EVAM_PP_PRIO", prio);
         band_ahead = env_int("EVAM_PP_BAND_AHEAD", band_ahead);
-        roi_copy = env_int("EVAM_PP_ROI_COPY", roi_copy);
         band = env_int("EVAM_PP_BAND", band); band_px = env_int("EVAM_PP_BAND_PX", band_px);
         strip = env_int("EVAM_PP_STRIP", strip); strip_th = env_int("EVAM_PP_STRIP_TH", strip_th);
         strip_waves = env_int("EVAM_PP_STRIP_WAVES", strip_waves);
@@ -4075,7 +4073,6 @@ void evam_pp_destroy(evam_pp* h) {
     if (h->ring.have_copy || h->pin.cur >= 0) {
         (void)hipStreamSynchronize(h->stream);
         if (h->ring.have_copy) (void)hipStreamSynchronize(h->ring.copy);
-        if (h->pin.have_copy) (void)hipStreamSynchronize(h->pin.copy);
     }
     HipRings b;
     h->ring.release(b);
@@ -4517,10 +4514,6 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
     {
         HipRings b;
         if (int rc = h->ring.upload(b, h->stream, h->h_block.data(), h->h_block.size(), &d_block)) return rc;
-        // EVAM_PP_ROI_COPY: the records travel to a device mirror of their slot (one small copy on the copy
-        // stream, overlapping the previous call's kernel) instead of being read over PCIe by every workgroup
-        if (any_roi && kn.roi_copy && dyn_bytes > 0)
-            if (int rc = h->pin.mirror(b, h->stream, dyn_bytes, &d_dyn)) return rc;
     }
     HP(9);
 

@@ -38,13 +38,6 @@ struct PinRingT {
     typename B::Event used[N] = {};
     bool used_rec[N] = {};
     int cur = -1;
-    // Optional device mirror (mirror(), EVAM_PP_ROI_COPY): slot k's records copied into dmir[k] on a private copy
-    // stream, so the kernels read them from HBM instead of over PCIe. dmir[k] is reused under slot k's own fence.
-    uint8_t* dmir[N] = {};
-    size_t dcap[N] = {};
-    typename B::Event copied[N] = {};
-    typename B::Stream copy = {};
-    bool have_copy = false;
 
     // Next slot with at least n bytes. Blocks only while a kernel of up to N calls ago may still read it:
     // the fence of the slot's run was recorded after the run's last call of the previous lap.
@@ -82,60 +75,20 @@ struct PinRingT {
         return 0;
     }
 
-    // Copy the current slot's first n bytes into its device mirror; kernels launched next on s see them (s waits
-    // for the copy). The host slot is rewritten only after its run's fence, i.e. after the kernels that followed
-    // this copy, so the copy never reads a slot the host is writing; the same fence frees the mirror.
-    int mirror(B& b, typename B::Stream s, size_t n, const uint8_t** out) {
-        const int k = cur;
-        if (k < 0) return 0;
-        if (!have_copy) {
-            if (int rc = b.stream_create(&copy)) return rc;
-            have_copy = true;
-        }
-        if (!copied[k]) {
-            if (int rc = b.event_create(&copied[k])) return rc;
-        }
-        if (dcap[k] < n) {
-            if (dmir[k]) {
-                if (int rc = b.dev_free(dmir[k])) return rc;
-            }
-            dmir[k] = nullptr;
-            dcap[k] = 0;
-            if (int rc = b.dev_alloc(&dmir[k], cap[k])) return rc;
-            dcap[k] = cap[k];
-        }
-        if (int rc = b.copy_h2d(dmir[k], host[k], n, copy)) return rc;
-        if (int rc = b.event_record(copied[k], copy)) return rc;
-        if (int rc = b.stream_wait(s, copied[k])) return rc;
-        *out = dmir[k];
-        return 0;
-    }
-
     // A call that failed after acquire() may have launched kernels that read its slot, and (when it held
     // a run's last slot) recorded no fence: drain the stream so no slot is still read, whatever the fences say.
-    int abandon(B& b, typename B::Stream s) {
-        if (have_copy) {
-            if (int rc = b.stream_sync(copy)) return rc;
-        }
-        return b.stream_sync(s);
-    }
+    int abandon(B& b, typename B::Stream s) { return b.stream_sync(s); }
 
     void release(B& b) {
         for (int k = 0; k < N; k++) {
             if (host[k]) (void)b.pinned_free(host[k]);
             if (used[k]) (void)b.event_destroy(used[k]);
-            if (dmir[k]) (void)b.dev_free(dmir[k]);
-            if (copied[k]) (void)b.event_destroy(copied[k]);
             host[k] = nullptr;
             dev[k] = nullptr;
-            dmir[k] = nullptr;
             used[k] = typename B::Event{};
-            copied[k] = typename B::Event{};
             used_rec[k] = false;
-            cap[k] = dcap[k] = 0;
+            cap[k] = 0;
         }
-        if (have_copy) (void)b.stream_destroy(copy);
-        have_copy = false;
         cur = -1;
     }
 };

@@ -102,7 +102,7 @@ struct Sim {
     }
 };
 
-static int run(bool sabotage, int calls, bool abandon = true, bool mirror = false) {
+static int run(bool sabotage, int calls, bool abandon = true) {
     Sim sim;
     sim.sabotage = sabotage;
     PinRingT<Sim> pin;
@@ -136,8 +136,6 @@ static int run(bool sabotage, int calls, bool abandon = true, bool mirror = fals
             const size_t n = std::max<size_t>(64, roi_bytes - uni(0, 63) * 64);
             if (pin.acquire(sim, n, &hslot, &dslot)) return -1;
             sim.host_write(hslot, n, "pinned ROI records written while a kernel reads them");
-            // EVAM_PP_ROI_COPY: the kernels read the slot's device mirror, filled by a copy on the pin's stream
-            if (mirror && pin.mirror(sim, stream, n, &dslot)) return -1;
         }
         const uint8_t* dblock = nullptr;
         if (desc.upload(sim, stream, block.data(), block.size(), &dblock)) return -1;
@@ -161,22 +159,17 @@ static int run(bool sabotage, int calls, bool abandon = true, bool mirror = fals
     }
     sim.stream_sync(stream);  // evam_pp_destroy: drain the launch stream and the copy stream first
     if (desc.have_copy) sim.stream_sync(desc.copy);
-    if (pin.have_copy) sim.stream_sync(pin.copy);
     pin.release(sim);
     desc.release(sim);
-    printf("%s%s: %d calls, %d failed calls, %d ROI capacity growths, %d new blocks, %d stream switches, "
-           "%d violations\n", sabotage ? "sabotaged waits" : (abandon ? "rings" : "rings, failed calls not drained"), mirror ? " (device-mirrored ROI records)" : "", calls, failed, grown, uploads, switches,
+    printf("%s: %d calls, %d failed calls, %d ROI capacity growths, %d new blocks, %d stream switches, "
+           "%d violations\n", sabotage ? "sabotaged waits" : (abandon ? "rings" : "rings, failed calls not drained"), calls, failed, grown, uploads, switches,
            sim.violations);
     return sim.violations;
 }
 
 int main() {
-    const int v = run(false, 8000) + run(false, 8000, true, true);
+    const int v = run(false, 8000);
     const int neg = run(true, 2000);
-    if (run(true, 2000, true, true) == 0) {
-        printf("FAIL: the mirrored negative control found no violation\n");
-        return 1;
-    }
     // a call that fails after taking a run's last pinned slot records no fence; without the
     // drain the next lap reuses the run's slots while this lap's kernels may still read them
     const int noab = run(false, 8000, false);
