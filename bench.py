@@ -226,7 +226,8 @@ def via_pipeline(args, evam, torch, wl, device_index):
     S, F = args.streams, args.frames_per_stream
     ps.PipelineServer.start({"pipeline_dir": os.path.join(tmp, "pipelines"), "model_dir": os.path.join(tmp, "models"),
                              "device": device_index, "batch_max": args.hub_batch, "batch_wait_ms": 1.0,
-                             "batch_target": args.hub_batch, "runner": args.runner})
+                             "batch_target": args.hub_batch, "runner": args.runner,
+                             "inflight": args.runner_inflight})
     ps.PipelineServer.register_model("bench_detector/1", ps.InferenceModel(detector, (DW, DH), name="bench"))
     # distinct frames: at least 2 per stream and >= 3x the Infinity Cache, as the direct leg's pool
     W, H = wl["src"]
@@ -260,7 +261,8 @@ def via_pipeline(args, evam, torch, wl, device_index):
     sizes = [b[1] for b in ps.PipelineServer.hub().batches]
     ps.PipelineServer.stop()
     return {"value": round(S * F / el, 1), "elapsed_s": round(el, 4), "streams": S, "frames_per_stream": F,
-            "stream_batch_size": args.stream_batch, "runner": args.runner, "pool_frames": n_pool,
+            "stream_batch_size": args.stream_batch, "runner": args.runner, "runner_inflight": args.runner_inflight,
+            "pool_frames": n_pool,
             "hub_launches": len(sizes),
             "mean_frames_per_launch": round(float(np.mean(sizes)), 2) if sizes else 0.0}
 
@@ -307,6 +309,8 @@ def main():
     ap.add_argument("--inflight", type=int, default=1,
                     help="launches in flight: step t runs on handle/stream t mod N (independent outputs), so launch "
                          "t+1's ramp overlaps launch t's tail; reported as its own line, timed by wall clock")
+    ap.add_argument("--runner-inflight", type=int, default=2,
+                    help="--via pipeline: ticks the device runner keeps in flight (server option inflight)")
     ap.add_argument("--runner", choices=["device", "threads"], default="device",
                     help="--via pipeline: one runner thread per device (default) or one thread per pipeline")
     args = ap.parse_args()
@@ -480,6 +484,21 @@ def main():
     latency = {"items": n_items, "steps": n_lat,
                "ms_p10_p50_p90": [round(float(np.percentile(lat_ms, q)), 4) for q in (10, 50, 90)],
                "note": "host enqueue to kernel completion per launch, device idle before each"}
+    # Host cost of one call, unthrottled: 12 calls enqueued back to back after a synchronize. That is fewer than
+    # the pinned ROI-record ring's 16 slots, so no call waits for the GPU. host_submit_ms_per_step (the timed loop)
+    # includes those waits: once the host runs 16 calls ahead of a GPU-bound stream, each call waits for the
+    # kernel of 16 calls ago, and host_submit approaches ms_per_step however cheap the call is.
+    host_us = None
+    if feed is None:
+        runs = []
+        for _ in range(20):
+            torch.cuda.synchronize()
+            s0 = time.perf_counter()
+            for t in range(12):
+                step(t)
+            runs.append((time.perf_counter() - s0) / 12)
+        torch.cuda.synchronize()
+        host_us = round(float(np.median(runs)) * 1e6, 2)
     # Secondary: the same launches re-reading ONE set (frames and output resident in the Infinity Cache
     # when they fit), for comparison with the pooled headline.
     resident = None
@@ -522,6 +541,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(wall_max / args.steps * 1e3, 4),
             "host_submit_ms_per_step": round(t_submit / args.steps * 1e3, 4),
+            "host_us_per_call": host_us,  # unthrottled host cost of one call (see above)
             "higher_is_better": True,
             "scaling": "strong" if strong else "weak",
             "vs_baseline": None,

@@ -38,6 +38,7 @@ device ``Image``s, or host planes uploaded on arrival.
 from __future__ import annotations
 
 import collections
+import contextlib
 import gc
 import itertools
 import json
@@ -357,8 +358,11 @@ class BatchHub:
     """
 
     def __init__(self, device: int, max_batch: int = 64, max_wait_s: float = 0.002, target: int | None = None,
-                 drain_timeout_s: float = 2.0):
+                 drain_timeout_s: float = 2.0, inflight: int = 1):
         self.device = int(device)
+        # ticks the device runner keeps in flight: tick t runs on handle / stream t mod inflight, so tick t+1's
+        # launch ramp overlaps tick t's tail (bench.py --inflight: C5 +30 %, C2 +14 % at the launch level)
+        self.inflight = max(1, int(inflight))
         self.drain_timeout_s = float(drain_timeout_s)  # runner shutdown: how long held-back results may wait
         self.max_batch = max(1, int(max_batch))
         self.max_wait_s = float(max_wait_s)
@@ -367,17 +371,43 @@ class BatchHub:
         self._units: dict = {}          # pending units per key
         self._cv = threading.Condition()
         self._stop = False
-        self._pp = None
+        self._pps: dict = {}            # slot -> pre-processing handle (bound to the slot's stream)
+        self._streams: list | None = None
         self.batches: list = []        # (key, units, requests) per executed batch (inspection / tests)
         self._thread = threading.Thread(target=self._loop, name=f"evam-hub-{device}", daemon=True)
         self._thread.start()
 
-    def pp(self):
-        if self._pp is None:
+    def stream(self, slot: int = 0):
+        """Slot's torch stream (None: one tick at a time, or no GPU: the thread's current stream)."""
+        if self.inflight == 1:
+            return None
+        if self._streams is None:
+            import torch
+
+            self._streams = ([torch.cuda.Stream(self.device) for _ in range(self.inflight)]
+                             if torch.cuda.is_available() else [None] * self.inflight)
+        return self._streams[slot % self.inflight]
+
+    def stream_ctx(self, slot: int = 0):
+        s = self.stream(slot)
+        if s is None:
+            return contextlib.nullcontext()
+        import torch
+
+        return torch.cuda.stream(s)
+
+    def pp(self, slot: int = 0):
+        """Slot's pre-processing handle. With several ticks in flight each slot owns a handle bound to its own
+        stream: a handle that followed the current stream would order every stream switch behind the previous
+        stream's work (evam_pp_set_stream), and the ticks could not overlap."""
+        h = self._pps.get(slot)
+        if h is None:
             from .preproc import HipPreProcessor
 
-            self._pp = HipPreProcessor(device=self.device)
-        return self._pp
+            s = self.stream(slot)
+            h = self._pps[slot] = HipPreProcessor(device=self.device) if s is None else \
+                HipPreProcessor(device=self.device, stream=s)
+        return h
 
     def submit(self, stage, items, units: int):
         """Queue ``items`` of ``stage`` and block until the batch holding them ran (re-raises its error)."""
@@ -446,9 +476,9 @@ class BatchHub:
             self._stop = True
             self._cv.notify_all()
         self._thread.join(10)
-        if self._pp is not None:
-            self._pp.close()
-            self._pp = None
+        for h in self._pps.values():
+            h.close()
+        self._pps = {}
 
 
 class DeviceRunner:
@@ -468,6 +498,8 @@ class DeviceRunner:
         self.hub = hub
         self._pipes: list = []
         self._draining: list = []  # ended pipelines whose destination still holds back results (queue full)
+        self._ticks = 0            # ticks run; tick t uses the hub's slot t mod hub.inflight
+        self._pending = None       # the last tick, launched but not completed (hub.inflight > 1)
         self._cv = threading.Condition()
         self._stop = False
         self._thread = threading.Thread(target=self._guarded_loop, name=f"evam-runner-{hub.device}", daemon=True)
@@ -553,6 +585,7 @@ class DeviceRunner:
                 stopping = self._stop and not self._pipes
                 pipes = list(self._pipes)
             if stopping:
+                self._complete_pending()
                 self._drain_at_shutdown(self.hub.drain_timeout_s)
                 return
             if self._draining:
@@ -578,6 +611,8 @@ class DeviceRunner:
                     continue
                 n = len(p._pend) - p._head
                 if p._stop.is_set() or (p._eos and not n):
+                    # its results still in flight (the pending tick) go out before its end of stream
+                    self._complete_pending()
                     self._finish(p)
                     done.append(p)
                 elif n >= p._batch or p._eos:
@@ -588,9 +623,11 @@ class DeviceRunner:
                 with self._cv:
                     self._pipes = [p for p in self._pipes if p not in done]
             if not ready:
+                self._complete_pending()
                 time.sleep(idle)
                 continue
             if total < (hub.target or 1) and time.perf_counter() - oldest < hub.max_wait_s:
+                self._complete_pending()
                 time.sleep(idle)
                 continue
             # about max_batch frames per tick, in whole batch-size multiples per pipeline
@@ -609,53 +646,102 @@ class DeviceRunner:
             self._tick(work)
 
     def _tick(self, work):
-        """Run the stage chains of `work` [(pipeline, frames)] stage by stage, batched across pipelines."""
+        """Run the stage chains of `work` [(pipeline, frames)] stage by stage, batched across pipelines, on the
+        hub's next slot (handle and stream). With ``hub.inflight`` > 1 a batch whose stage ends every chain in it
+        and can launch without completing (``launch_batch``: detection) is only enqueued here; its completion,
+        the pipelines' bookkeeping and the tick's results wait until the next tick has been launched, so the
+        next tick's kernels overlap this one's tail. Ticks complete in launch order, so every stream's results
+        keep their order."""
         hub = self.hub
+        slot = self._ticks % hub.inflight
+        self._ticks += 1
         failed = set()
-        depth = max(len(p.stages) for p, _ in work)
-        for k in range(depth):
-            groups: dict = {}
-            for p, items in work:
-                if p in failed or k >= len(p.stages) or not items:
-                    continue
-                st = p.stages[k]
-                try:
-                    if not st.batchable:
-                        st.process(items)
+        deferred = []  # (completion, chunk)
+        with hub.stream_ctx(slot):
+            s = hub.stream(slot)
+            if s is not None:
+                import torch
+
+                # the application's frames were written on its own (default) stream
+                s.wait_stream(torch.cuda.default_stream(hub.device))
+            depth = max(len(p.stages) for p, _ in work)
+            for k in range(depth):
+                groups: dict = {}
+                for p, items in work:
+                    if p in failed or k >= len(p.stages) or not items:
                         continue
-                    w, units = st.prepare(items)
-                except Exception as e:  # noqa: BLE001
+                    st = p.stages[k]
+                    try:
+                        if not st.batchable:
+                            st.process(items)
+                            continue
+                        w, units = st.prepare(items)
+                    except Exception as e:  # noqa: BLE001
+                        self._finish(p, e)
+                        failed.add(p)
+                        continue
+                    if units > 0:
+                        groups.setdefault(st.hub_key(), []).append((p, _Request(st, w, units, event=False)))
+                for key, reqs in groups.items():
+                    i = 0
+                    while i < len(reqs):  # chunks of at most max_batch units (at least one request)
+                        j, n = i, 0
+                        while j < len(reqs) and (j == i or n + reqs[j][1].units <= hub.max_batch):
+                            n += reqs[j][1].units
+                            j += 1
+                        chunk = reqs[i:j]
+                        i = j
+                        stage = chunk[0][1].stage
+                        defer = (hub.inflight > 1 and hasattr(stage, "launch_batch")
+                                 and all(k == len(p.stages) - 1 for p, _ in chunk))
+                        try:
+                            if defer:
+                                deferred.append((stage.launch_batch([r for _, r in chunk], hub.pp(slot)), chunk))
+                            else:
+                                stage.run_batch([r for _, r in chunk], hub.pp(slot))
+                            hub.batches.append((key, n, len(chunk)))
+                            if len(hub.batches) > 4096:
+                                del hub.batches[:2048]
+                        except Exception as e:  # noqa: BLE001 — delivered to every pipeline of the batch
+                            for p, _ in chunk:
+                                self._finish(p, e)
+                                failed.add(p)
+                            continue
+                        if not defer:
+                            self._finish_batch(chunk, failed)
+        tick = (slot, deferred, work, failed)
+        prev, self._pending = self._pending, None
+        if prev is not None:
+            self._complete(prev)
+        if deferred:
+            self._pending = tick
+        else:
+            self._complete(tick)
+
+    def _finish_batch(self, chunk, failed):
+        for p, r in chunk:
+            if p not in failed:
+                try:
+                    r.stage.finish(r.items)
+                except Exception as e:  # noqa: BLE001 — this stream's bookkeeping only
                     self._finish(p, e)
                     failed.add(p)
-                    continue
-                if units > 0:
-                    groups.setdefault(st.hub_key(), []).append((p, _Request(st, w, units, event=False)))
-            for key, reqs in groups.items():
-                i = 0
-                while i < len(reqs):  # chunks of at most max_batch units (at least one request)
-                    j, n = i, 0
-                    while j < len(reqs) and (j == i or n + reqs[j][1].units <= hub.max_batch):
-                        n += reqs[j][1].units
-                        j += 1
-                    chunk = reqs[i:j]
-                    i = j
+
+    def _complete(self, tick):
+        """Complete a tick: its deferred batches (model output to the host, per-stream bookkeeping), then every
+        stream's results of the tick to its destination."""
+        slot, deferred, work, failed = tick
+        if deferred:
+            with self.hub.stream_ctx(slot):
+                for done, chunk in deferred:
                     try:
-                        chunk[0][1].stage.run_batch([r for _, r in chunk], hub.pp())
-                        hub.batches.append((key, n, len(chunk)))
-                        if len(hub.batches) > 4096:
-                            del hub.batches[:2048]
+                        done()
                     except Exception as e:  # noqa: BLE001 — delivered to every pipeline of the batch
                         for p, _ in chunk:
                             self._finish(p, e)
                             failed.add(p)
                         continue
-                    for p, r in chunk:
-                        if p not in failed:
-                            try:
-                                r.stage.finish(r.items)
-                            except Exception as e:  # noqa: BLE001 — this stream's bookkeeping only
-                                self._finish(p, e)
-                                failed.add(p)
+                    self._finish_batch(chunk, failed)
         for p, items in work:
             if p not in failed:
                 try:
@@ -666,6 +752,11 @@ class DeviceRunner:
         if failed:
             with self._cv:
                 self._pipes = [p for p in self._pipes if p not in failed]
+
+    def _complete_pending(self):
+        if self._pending is not None:
+            tick, self._pending = self._pending, None
+            self._complete(tick)
 
 
 class _InferenceStage:
@@ -752,22 +843,32 @@ class DetectStage(_InferenceStage):
         run = [it for it in items if it[0] % self.interval == 0] if self.interval > 1 else items
         return run, len(run)
 
-    def run_batch(self, reqs, pp):
-        """One launch over the frames of every request (hub thread)."""
+    def launch_batch(self, reqs, pp):
+        """Enqueue one launch over the frames of every request and the model call on it; returns the completion
+        (the model output's copy to the host, the detections attached to the frames). The device runner calls it
+        after the next tick's launch when it keeps several ticks in flight."""
         run = [it for r in reqs for it in r.items]
         out = self._tensor(len(run))
         xfs = pp.convert([img for _, img, _ in run], out, self.info, want_transform="lazy")
         raw = self.model.fn(out)
-        raw = raw.detach().float().cpu().numpy() if hasattr(raw, "detach") else raw
-        W, H = self.model.input_size
-        labels = None
-        for pp_ in self.model.postprocs():
-            labels = pp_.get("labels", labels)
-        for k, dets in enumerate(P.parse_ssd_batch(raw, self.threshold)):
-            if dets:
-                _, img, fr = run[k]
-                fr.regions.extend(P.detections_to_regions(dets, xfs[k], img.width, img.height, W, H, labels,
-                                                          model=self.model.name))
+
+        def complete():
+            r = raw.detach().float().cpu().numpy() if hasattr(raw, "detach") else raw
+            W, H = self.model.input_size
+            labels = None
+            for pp_ in self.model.postprocs():
+                labels = pp_.get("labels", labels)
+            for k, dets in enumerate(P.parse_ssd_batch(r, self.threshold)):
+                if dets:
+                    _, img, fr = run[k]
+                    fr.regions.extend(P.detections_to_regions(dets, xfs[k], img.width, img.height, W, H, labels,
+                                                              model=self.model.name))
+        complete.out = out  # the tensor the kernel writes stays alive until its batch completes
+        return complete
+
+    def run_batch(self, reqs, pp):
+        """One launch over the frames of every request, completed before returning."""
+        self.launch_batch(reqs, pp)()
 
 
 class ClassifyStage(_InferenceStage):
@@ -1263,7 +1364,8 @@ class _Server:
                 h = self._hubs[slot] = BatchHub(self.devices[slot], max_batch=int(o.get("batch_max", 64)),
                                                 max_wait_s=float(o.get("batch_wait_ms", 2.0)) / 1e3,
                                                 target=o.get("batch_target"),
-                                                drain_timeout_s=float(o.get("drain_timeout_ms", 2000.0)) / 1e3)
+                                                drain_timeout_s=float(o.get("drain_timeout_ms", 2000.0)) / 1e3,
+                                                inflight=int(o.get("inflight", 2)))
             return h
 
     def runner(self, slot: int = 0) -> DeviceRunner:

@@ -376,3 +376,62 @@ def test_runner_survives_an_internal_error(stubbed, monkeypatch):
     p = _start(ps, pre, 4, queue.Queue())
     st = p.wait(30)
     assert st["state"] == "ERROR" and "runner bug" in st["message"]
+
+
+def test_runner_keeps_two_ticks_in_flight(stubbed, monkeypatch):
+    """with inflight 2 (the default) the device runner launches tick t+1 before it completes tick t
+    (model output to the host, detections, results), on the hub's alternate slot; ticks still complete in launch
+    order and every stream's results are those of inflight 1, in order, end-of-stream marker last."""
+    ps, pre, mdir = stubbed
+    events = []
+    orig = ps.DetectStage.launch_batch
+
+    def launch(self, reqs, pp):
+        tick = len([e for e in events if e[0] == "launch"])
+        events.append(("launch", tick, id(pp)))
+        done = orig(self, reqs, pp)
+
+        def complete():
+            events.append(("complete", tick))
+            done()
+        return complete
+
+    monkeypatch.setattr(ps.DetectStage, "launch_batch", launch)
+
+    def run(inflight):
+        events.clear()
+        ps.PipelineServer.start({"pipeline_dir": PIPES, "model_dir": mdir, "batch_max": 4, "batch_target": 4,
+                                 "batch_wait_ms": 200, "inflight": inflight})
+        register(ps, det_every=1)  # a car in every frame: the results do not depend on how ticks group frames
+        outs, pipes = [], []
+        for k, n in enumerate([9, 6, 11]):
+            qin, qout = queue.Queue(), queue.Queue()
+            for im in frames(pre, n):
+                qin.put(im)
+            qin.put(None)
+            p = ps.PipelineServer.pipeline("detect", "hip")
+            p.start(source={"type": "application", "input": qin},
+                    destination={"metadata": {"type": "application", "output": qout, "mode": "json"}},
+                    parameters={"detection-properties": {"batch-size": 2}})
+            pipes.append(p)
+            outs.append(qout)
+        for p in pipes:
+            assert p.wait(60)["state"] == "COMPLETED"
+        got = [[json.loads(x) for x in _drain(q)] for q in outs]
+        ps.PipelineServer.stop()
+        return got, list(events)
+
+    one, ev1 = run(1)
+    two, ev2 = run(2)
+    assert [len(g) for g in one] == [9, 6, 11]
+    assert one == two
+    # inflight 1: every batch completes before the next launches
+    assert all(ev1[i][0] == "launch" and ev1[i + 1] == ("complete", ev1[i][1]) for i in range(0, len(ev1), 2))
+    # inflight 2: some tick launches before its predecessor completes; completions keep launch order, and
+    # consecutive ticks alternate between the hub's two handles
+    order = [e[1] for e in ev2 if e[0] == "complete"]
+    assert order == sorted(order) and len(order) == len([e for e in ev2 if e[0] == "launch"])
+    pos = {(e[0], e[1]): i for i, e in enumerate(ev2)}
+    assert any(pos[("launch", t + 1)] < pos[("complete", t)] for t in range(len(order) - 1))
+    handles = [e[2] for e in ev2 if e[0] == "launch"]
+    assert len(set(handles)) == 2

@@ -117,7 +117,7 @@ def test_parameter_schema_forms(ps, model_dir, monkeypatch):
         ps.PipelineServer.pipeline("zone", "count").build({}, {"mode": "other"})
     assert ps.PipelineServer.pipeline("nope", "1") is None
     names = {(d["name"], d["version"]) for d in ps.PipelineServer.pipelines()}
-    assert names == {("detect_classify", "hip"), ("action", "general"), ("zone", "count")}
+    assert names == {("detect_classify", "hip"), ("detect", "hip"), ("action", "general"), ("zone", "count")}
     ps.PipelineServer.stop()
 
 
