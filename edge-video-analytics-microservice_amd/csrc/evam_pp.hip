@@ -3165,7 +3165,9 @@ struct Knobs {
     int wide_slot = 0;                             // 1: 256-column staged tiles may take 2 KB row segments
     int stage_r = -1, stage_nbuf = -1;             // staged pipeline: rows per group, staging buffers
     int wth = -1, px = 0, reuse = 1, wave_lds = 40 * 1024;
-    int roi_th = -1, roi_buf = -1, roi_px = 1, roi_sort = 1, roi_xcd = 0;  // roi_buf -1: sized for one round
+    int roi_th = -1, roi_buf = -1, roi_px = 1, roi_xcd = 0;  // roi_buf -1: sized for one round
+    int roi_sort = 0;  // 1: largest estimated bytes first before the stable sort by row groups (C3: equal or
+                       // slower, profiles/r04k_ab_lines.txt; the units are ordered by row groups either way)
     int roi_unit = 0;                              // ROI work-unit size in row groups (0: one unit per base tile)
     int roi_nbuf = 2;                              // ROI staging buffers (3: two groups of DMA in flight)
     int roi_tail = 4;                              // row tiles per ROI of the uneven tail over the CUs (1: no split)
@@ -3983,6 +3985,10 @@ struct evam_pp {
     std::vector<int> sc_members;   // item indices grouped by source format
     std::vector<Geom> sc_geo;
     std::vector<int> sc_units;     // ROI work units: (item, row0, row1, cost)
+    std::vector<int> sc_start;     // ROI unit counting sort: bucket starts
+    std::vector<int> sc_slot;      // ROI units in launch order
+    int memo_key[4] = {-1, -1, -1, -1};  // (format, staging buffer, row cap, DH) of memo_rg
+    std::vector<uint32_t> memo_rg;       // per crop width: rows per group | groups of the whole height << 16
     TParams sc_tparams;            // strip-kernel arguments (3.5 KB: kept off the stack)
 };
 
@@ -4210,7 +4216,36 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
     }
     std::vector<int>& sfmt = h->sc_sfmt;  // per source: format id (looked up once, not per ROI)
     sfmt.resize(n_srcs);
-    for (int i = 0; i < n_srcs; i++) sfmt[i] = fmt_id(srcs[i].fourcc);
+    bool one_fmt = true;
+    for (int i = 0; i < n_srcs; i++) {
+        sfmt[i] = fmt_id(srcs[i].fourcc);
+        one_fmt &= sfmt[i] == sfmt[0];
+    }
+    if (one_fmt && items && n_items > 0 && n_srcs > 0) {
+        // every source in one format (the common case: one decoder): the group's counters live in registers
+        // instead of arrays indexed by the item's format (a store-to-load chain per ROI: C3 pass 1 ~7 -> ~4 us)
+        const int f = sfmt[0];
+        int mcw = 0, mch = 0, rcw = 0, rch = 0;
+        uint32_t xm = 0;
+        bool uni = true;
+        for (int i = 0; i < n_items; i++) {
+            const evam_roi& r = items[i];
+            if ((unsigned)r.src_index >= (unsigned)n_srcs)
+                return fail(EVAM_PP_ERR_INVALID_ARG, "evam_pp_run: items[%d].src_index %d out of range", i, r.src_index);
+            const evam_image& s = srcs[r.src_index];
+            fmt[i] = f;
+            Geom& g = geo[i];
+            if (roi_clip(f, s.width, s.height, true, r.x, r.y, r.w, r.h, g))
+                return fail(EVAM_PP_ERR_EMPTY_ROI, "evam_pp_run: items[%d] ROI (%d,%d,%d,%d) is empty after clipping to %dx%d",
+                            i, r.x, r.y, r.w, r.h, s.width, s.height);
+            mcw = std::max(mcw, g.cw);
+            mch = std::max(mch, g.ch);
+            xm |= 1u << (g.x0 & 31);
+            if (i == 0) { rcw = g.cw; rch = g.ch; }
+            uni &= g.cw == rcw && g.ch == rch;  // geometry = f(cw, ch)
+        }
+        count[f] = n_items; max_cw[f] = mcw; max_ch[f] = mch; x0_mask[f] = xm; rep[f] = 0; uniform[f] = uni;
+    } else
     for (int i = 0; i < n_items; i++) {
         const evam_roi* r = items ? &items[i] : nullptr;
         const int si = items ? r->src_index : i;
@@ -4459,10 +4494,31 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
                 const int ts = roi_tail_tiles(n, h->n_cu, qslots[f], kn.roi_tail, DH, nsplit);
                 un.resize(4 * ((size_t)n + (size_t)nsplit * (ts - 1)));
                 int* u4 = un.data();
+                // rows per group and groups per ROI depend on an ROI only through its crop width: memoised per
+                // handle for this launch's (format, staging buffer, row cap, DH), the divisions run once per
+                // distinct width instead of per ROI and call
+                const int mkey[4] = {f, q.buf_bytes, rcap, DH};
+                if (memcmp(mkey, h->memo_key, sizeof(mkey)) != 0) {
+                    memcpy(h->memo_key, mkey, sizeof(mkey));
+                    h->memo_rg.clear();
+                }
+                if ((int)h->memo_rg.size() <= max_cw[f]) h->memo_rg.resize((size_t)max_cw[f] + 1, 0u);
+                uint32_t* rg = h->memo_rg.data();  // R | groups of the whole height << 16 (0: not yet known)
                 for (int p = 0; p < n; p++) {
                     const int i = ord[p];
-                    const int R = std::max(1, std::min(std::min(q.buf_bytes / row_bytes_bound(f, geo[i].cw), rcap), DH));
-                    const int nt = p >= n - nsplit ? ts : 1;
+                    uint32_t& e = rg[geo[i].cw];
+                    if (!e) {
+                        const int R = std::max(1, std::min(std::min(q.buf_bytes / row_bytes_bound(f, geo[i].cw), rcap), DH));
+                        e = (uint32_t)R | ((uint32_t)((DH + R - 1) / R) << 16);
+                    }
+                    if (p < n - nsplit) {
+                        const int cost = (int)(e >> 16);
+                        maxcost = std::max(maxcost, cost);
+                        u4[0] = i; u4[1] = 0; u4[2] = DH; u4[3] = cost;
+                        u4 += 4;
+                        continue;
+                    }
+                    const int R = (int)(e & 0xFFFF), nt = ts;
                     for (int t = 0; t < nt; t++, u4 += 4) {
                         const int y0 = DH * t / nt, y1 = DH * (t + 1) / nt;
                         const int cost = (y1 - y0 + R - 1) / R;
@@ -4485,17 +4541,21 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
                 }
             }
             HP(7);
-            // stable counting sort of the units by cost, largest first
+            // stable counting sort of the units by cost, largest first; the records then go out in launch order,
+            // one sequential pass over the pinned (write-combined) slot instead of scattered 64-byte writes
             const int nu = (int)(un.size() / 4);
-            std::vector<int> start(maxcost + 2, 0);
+            std::vector<int>& start = h->sc_start;
+            start.assign((size_t)maxcost + 2, 0);
             for (int u = 0; u < nu; u++) start[maxcost - un[4 * u + 3] + 1]++;
             for (int c = 0; c <= maxcost; c++) start[c + 1] += start[c];
-            std::vector<int> slot(nu);
-            for (int u = 0; u < nu; u++) slot[u] = start[maxcost - un[4 * u + 3]]++;
-            for (int u = 0; u < nu; u++) {
+            std::vector<int>& order = h->sc_slot;
+            order.resize(nu);
+            for (int u = 0; u < nu; u++) order[start[maxcost - un[4 * u + 3]]++] = u;
+            for (int pos = 0; pos < nu; pos++) {
+                const int u = order[pos];
                 const int i = un[4 * u];
                 const evam_image& sim = srcs[items ? items[i].src_index : i];
-                RoiRec& r = rr[slot[u]];
+                RoiRec r;  // built in registers, then one 64-byte copy into the write-combined slot
                 r.plane[0] = sim.planes[0]; r.plane[1] = sim.planes[1]; r.plane[2] = sim.planes[2];
                 r.pitch[0] = sim.pitch[0]; r.pitch[1] = sim.pitch[1]; r.pitch[2] = sim.pitch[2];
                 r.width = (uint16_t)sim.width; r.height = (uint16_t)sim.height;
@@ -4504,6 +4564,7 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
                 r.item = i;
                 r.row0 = (uint16_t)un[4 * u + 1];
                 r.row1 = (uint16_t)un[4 * u + 2];
+                memcpy(&rr[pos], &r, sizeof(RoiRec));
             }
             const int nrec = nu;
             qrec[f] = nrec;

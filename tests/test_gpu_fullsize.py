@@ -94,7 +94,7 @@ def test_c2_bench_batch(evam, O, coracle, gpu, shape, monkeypatch):
     pp.close()
 
 
-@pytest.mark.parametrize("kernel", ["dense", "dense_noprio", "roi_tail1", "roi", "roi_noprio"])
+@pytest.mark.parametrize("kernel", ["dense", "dense_noprio", "roi_tail1", "roi", "roi_noprio", "roi_sorted"])
 @pytest.mark.parametrize("seed", [0, 3])
 def test_c3_bench_roi_set(evam, O, coracle, gpu, seed, kernel, monkeypatch):
     """C3: bench.py's seeded ROI set (50 per frame, w 24..400, h 24..300) on 32 bench 1080p NV12 frames ->
@@ -106,6 +106,8 @@ def test_c3_bench_roi_set(evam, O, coracle, gpu, seed, kernel, monkeypatch):
     if kernel.endswith("_noprio"):
         monkeypatch.setenv("EVAM_PP_PRIO", "0")
         kernel = kernel[:-7]
+    if kernel == "roi_sorted":  # largest estimated bytes first before the sort by row groups
+        monkeypatch.setenv("EVAM_PP_ROI_SORT", "1")
     monkeypatch.setenv("EVAM_PP_ROI_DENSE", "1" if kernel == "dense" else "0")
     if kernel != "dense":
         monkeypatch.setenv("EVAM_PP_ROI_TAIL", "1" if kernel == "roi_tail1" else "4")
