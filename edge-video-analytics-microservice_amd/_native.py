@@ -92,7 +92,7 @@ class EvamStats(ctypes.Structure):
 
 # evam_pp_stats.kernels bits (include/evam_pp.h evam_kernel_family)
 KERNEL_GENERIC, KERNEL_ROWS, KERNEL_STAGED, KERNEL_WAVE = 1, 2, 4, 8
-KERNEL_STRIP, KERNEL_BAND, KERNEL_ROI, KERNEL_ROI_DENSE = 16, 32, 64, 128
+KERNEL_STRIP, KERNEL_BAND, KERNEL_ROI = 16, 32, 64
 
 
 STRUCT_SIZES = {EvamImage: 48, EvamRoi: 20, EvamPreproc: 56, EvamTensor: 32, EvamTransform: 40, EvamStats: 32}

@@ -2000,25 +2000,6 @@ __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
 #endif
 }
 
-// ------------------------------------------------------------------------------------------------
-// dense ROI kernel (per-item geometry, 4:2:0 sources: gvaclassify batches, C3)
-// ------------------------------------------------------------------------------------------------
-struct WRParams {
-    const RoiRec* recs;      // one record per workgroup: an ROI (or a row tile of a tall output)
-    const float* lut;        // [3][256]
-    void* dst;
-    int slot_offset, slot_stride;
-    int DW, DH;
-    int mode, placement;     // evam_resize_mode, evam_placement
-    int nbw;                 // the workgroup's waves: row bands of the record's rows
-    int ring_bytes;          // one wave's LDS ring (a multiple of 16)
-    int color_rgb;
-    uint32_t fill;
-    int rt_rows;             // rows of one wave's row table (the most rows of a band, <= 64)
-    int prio;                // progress-based wave priority (as the strip kernel's)
-};
-constexpr int kRingMax = 8;  // most ring entries (rows of DMA in flight) of one wave
-
 // Wait until at most n (0..63, wave-uniform) vector-memory operations of this wave are outstanding: exact over the
 // whole 6-bit vmcnt range (a jump over immediates).
 __device__ __forceinline__ void vmcnt_le(int n) {
@@ -2033,349 +2014,6 @@ __device__ __forceinline__ void vmcnt_le(int n) {
     }
 #undef EVAM_VMC8
 #undef EVAM_VMC
-}
-
-// Dense ROI kernel (per-item geometry, 4:2:0 sources: gvaclassify batches, C3). One workgroup per RoiRec, whose
-// nbw waves each own a band of the record's output rows — every column of them: the band's rows x DW pixels are
-// one flat run, walked 64 pixels per step (pixel p = 64 s + lane), so a 72-wide classifier row keeps every lane
-// busy (a row-per-step layout leaves 56 of 128 lanes idle at 72 columns) and each step's three planar stores are
-// 256 contiguous bytes (whole lines, not a 288-byte row per store with partial lines at both ends).
-//  * Tables: the item's OpenCV column coefficients once per workgroup (colTab, 8 B per output column: tap offsets
-//    inside the staged segments and the packed 11-bit weights), its row coefficients once per wave (rowTab, 16 B per
-//    band row: weights, ring entry, second chroma segment, fill flag); a pixel reads its column and row entry.
-//  * Ring: a ring entry is exactly one visible row's source bytes, packed: [Y tap0][Y tap1] (nY 16-byte chunks each)
-//    then [C tap0][C tap1] per chroma plane (nC chunks each); a row's luma chunks are ONE LDS-DMA instruction (one
-//    chunk per lane, per-lane source offsets; two for footprints over 512 B) and so are its chroma chunks per plane
-//    (a 200-pixel crop's row: 2 DMA instructions, not 4 mostly idle ones). The ring holds as many entries as the wave's
-//    ring_bytes allow (up to kRingMax): narrow crops run deep rings, wide ones shallow, so every wave keeps about the
-//    same bytes in flight whatever the crop width. The waits are exact: the wave counts every vector-memory operation
-//    it issues (pos) and remembers pos after each row's DMA (lane vi of dpos), so step s waits with vmcnt(pos -
-//    dpos[last row it reads]) and the stores and later rows' DMA stay in flight; a row's entry is refilled once no
-//    later step reads it.
-//  * Letterbox rows and columns are pixels of the run like any other (fill flag / pad bit -> the fill value).
-template <int FMT, int OUT>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_num_sgpr(96))) void evam_pp_roid(const WRParams P) {
-    __shared__ __attribute__((aligned(16))) float lut_s[OUT == 1 ? 768 : 4];
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    static_assert(FMT == kNV12 || FMT == kI420, "4:2:0 sources");
-    constexpr int NPC = FMT == kI420 ? 2 : 1;  // chroma planes
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    EVAM_WSTAMP(0);
-    typedef unsigned int u32x16 __attribute__((ext_vector_type(16)));
-    const u32x16 rec = *((const __attribute__((address_space(4))) u32x16*)(P.recs) + blockIdx.x);
-    const int nbw = P.nbw, mode = P.mode, placement = P.placement, DW = P.DW, DH = P.DH;
-    const int RB = P.ring_bytes;
-    int k_rgb = P.color_rgb;
-    const float* k_lut = P.lut;
-    asm volatile("" ::"s"(nbw), "s"(mode), "s"(placement), "s"(DW), "s"(DH), "s"(RB), "s"(P.dst), "s"(P.slot_offset),
-                 "s"(P.slot_stride), "s"(P.fill));
-    asm volatile("" : "+s"(k_lut), "+s"(k_rgb));
-    static_assert(offsetof(RoiRec, pitch) == 24 && offsetof(RoiRec, width) == 36 && offsetof(RoiRec, x) == 40 &&
-                  offsetof(RoiRec, item) == 56 && offsetof(RoiRec, row0) == 60, "RoiRec dword map");
-    const uint8_t* p0 = reinterpret_cast<const uint8_t*>(((uint64_t)rec[1] << 32) | rec[0]);
-    const uint8_t* p1 = reinterpret_cast<const uint8_t*>(((uint64_t)rec[3] << 32) | rec[2]);
-    const uint8_t* p2 = reinterpret_cast<const uint8_t*>(((uint64_t)rec[5] << 32) | rec[4]);
-    const int pitch0 = (int)rec[6], pitch1 = (int)rec[7], pitch2 = (int)rec[8];
-    const int index = (int)rec[14];
-    EVAM_WSTAMP(7);  // the record arrived
-    // One wave per workgroup resolves the item's geometry, scales and footprint (wave blockIdx mod nbw: the waves of a
-    // workgroup sit on different SIMDs, so a SIMD computes about 1/nbw of its workgroups' geometry — double divisions
-    // and the OpenCV coefficient sequence — instead of every one) and broadcasts it through LDS.
-    __shared__ __attribute__((aligned(16))) int geo_s[16];
-    if (wave == (int)(blockIdx.x % (unsigned)nbw)) {
-        Geom g;
-        roi_geometry(FMT, (int)(rec[9] & 0xFFFF), (int)(rec[9] >> 16), true, (int)rec[10], (int)rec[11], (int)rec[12],
-                     (int)rec[13], mode, placement, DW, DH, g);  // never empty: the host validated every item
-        const double sx = 1. / ((double)g.rw / g.cw), sy = 1. / ((double)g.rh / g.ch);
-        // footprint of the visible columns (crop-relative taps of the first and last)
-        const int Xv0 = max(0, g.ox), Xv1 = min(DW, g.ox + g.rw) - 1;
-        int fY = 0, cY = 0, fC = 0, cC = 0;
-        if (Xv0 <= Xv1) {
-            int sa, sb, c0, c1;
-            linear_coef(Xv0 - g.ox, sx, g.cw, true, sa, c0, c1);
-            linear_coef(Xv1 - g.ox, sx, g.cw, true, sb, c0, c1);
-            footprint_chunks(FMT, 1, g.x0 + sa, g.x0 + min(sb + 1, g.cw - 1), fY, cY, fC, cC);
-        }
-        if (lane == 0) {
-            const long long bx = __double_as_longlong(sx), by = __double_as_longlong(sy);
-            *reinterpret_cast<int4*>(geo_s) = int4{g.x0, g.y0, g.cw, g.ch};
-            *reinterpret_cast<int4*>(geo_s + 4) = int4{g.rw, g.rh, g.ox, g.oy};
-            *reinterpret_cast<int4*>(geo_s + 8) = int4{(int)bx, (int)(bx >> 32), (int)by, (int)(by >> 32)};
-            *reinterpret_cast<int4*>(geo_s + 12) = int4{fY, cY, fC, cC};
-        }
-    }
-    lds_barrier();
-    const int4 ga = *reinterpret_cast<const int4*>(geo_s), gb = *reinterpret_cast<const int4*>(geo_s + 4);
-    const int4 gc = *reinterpret_cast<const int4*>(geo_s + 8), gd = *reinterpret_cast<const int4*>(geo_s + 12);
-    const int x0 = __builtin_amdgcn_readfirstlane(ga.x), y0 = __builtin_amdgcn_readfirstlane(ga.y);
-    const int cw = __builtin_amdgcn_readfirstlane(ga.z), ch = __builtin_amdgcn_readfirstlane(ga.w);
-    const int rw = __builtin_amdgcn_readfirstlane(gb.x), rh = __builtin_amdgcn_readfirstlane(gb.y);
-    const int ox = __builtin_amdgcn_readfirstlane(gb.z), oy = __builtin_amdgcn_readfirstlane(gb.w);
-    const double scx = __longlong_as_double(((long long)(unsigned)__builtin_amdgcn_readfirstlane(gc.y) << 32) |
-                                            (unsigned)__builtin_amdgcn_readfirstlane(gc.x));
-    const double scy = __longlong_as_double(((long long)(unsigned)__builtin_amdgcn_readfirstlane(gc.w) << 32) |
-                                            (unsigned)__builtin_amdgcn_readfirstlane(gc.z));
-    const int fsY = __builtin_amdgcn_readfirstlane(gd.x), nY = __builtin_amdgcn_readfirstlane(gd.y);
-    const int fsC = __builtin_amdgcn_readfirstlane(gd.z), nC = __builtin_amdgcn_readfirstlane(gd.w);
-    const bool cols = nY > 0;
-    (void)rw;
-    const int row0 = (int)(rec[15] & 0xFFFF), row1 = (int)(rec[15] >> 16);
-#ifdef EVAM_PP_TRACE
-    asm volatile("" ::"v"(scx), "v"(scy));
-    EVAM_WSTAMP(8);  // geometry and scales
-#endif
-    const int th = (row1 - row0 + nbw - 1) / nbw;
-    const int Y0 = min(row0 + wave * th, row1), Y1 = min(Y0 + th, row1), rows = Y1 - Y0;  // rows <= 64 (host)
-    const int vr0 = max(Y0, oy), vr1 = min(Y1, oy + rh);
-    const int n = cols && vr1 > vr0 ? vr1 - vr0 : 0;  // visible rows (the ring's rows)
-    const int voff = vr0 - Y0;                          // band rows above the first visible row
-    // ring geometry
-    const int nchY = 2 * nY, nchC = 2 * nC;
-    const int segY = 16 * nY, segC = 16 * nC, offC = 16 * nchY;
-    const int E = 16 * (nchY + NPC * nchC);
-    const int niY = (nchY + 63) >> 6, niC = (nchC + 63) >> 6;
-    const int q64 = 64 / DW, m64 = 64 - q64 * DW;  // one step: +64 pixels = q64 rows + m64 columns
-    int Dr = E > 0 ? min(kRingMax, RB / E) : 1;
-    // every wait fits the 6-bit vmcnt: the DMA of Dr - 1 rows and the stores of the steps over Dr rows
-    const int span = (63 + DW - 1) / DW + 1;  // rows one step reads (the host sizes the ring for them)
-    while (Dr > span && (Dr - 1) * (niY + NPC * niC) + 3 * ((Dr * DW + 63) / 64 + 1) > 63) Dr--;
-    Dr = max(Dr, 1);
-    // LDS carve: [colTab DW x 8 B][rowTab rt_rows x 16 B per wave][ring RB per wave]
-    uint2* const colTab = reinterpret_cast<uint2*>(smem);
-    const int ctb = (DW * 8 + 15) & ~15;
-    const int nw = nbw, rtr = P.rt_rows;
-    uint4* const rowTab = reinterpret_cast<uint4*>(smem + ctb) + wave * rtr;
-    uint8_t* const wbuf = smem + ctb + nw * rtr * 16 + wave * RB;
-    // band row table, one row per lane: weights, ring entry, second chroma segment, fill flag; and the source rows
-    // (crop-relative) for the DMA
-    int lr0 = 0, lr1 = 0;
-    if (lane < rows) {
-        uint4 e = uint4{0u, 0u, 0u, 0x80000000u};  // letterbox row: the fill value
-        const int vi = lane - voff;
-        if (vi >= 0 && vi < n) {
-            int sy, b0, b1;
-            linear_coef(Y0 + lane - oy, scy, ch, false, sy, b0, b1);
-            lr0 = min(max(sy, 0), ch - 1);
-            lr1 = min(max(sy + 1, 0), ch - 1);
-            const bool share = ((y0 + lr0) >> 1) == ((y0 + lr1) >> 1);
-            e = uint4{(uint32_t)b0 << 8, (uint32_t)b1 << 8, (uint32_t)((vi % Dr) * E), share ? 0u : (uint32_t)segC};
-        }
-        rowTab[lane] = e;
-    }
-#ifdef EVAM_PP_TRACE
-    asm volatile("" ::"v"(lr0), "v"(lr1));
-    EVAM_WSTAMP(9);  // footprint and row table
-#endif
-    // per-lane DMA source columns of the luma / chroma chunks: chunk q = lane + 64 b -> (tap, chunk c)
-    uint32_t dY[2], dC[2];
-    bool tY[2], tC[2], vY[2], vC[2];
-#pragma unroll
-    for (int b = 0; b < 2; b++) {
-        const int q = lane + 64 * b;
-        tY[b] = q >= nY;
-        vY[b] = q < nchY;
-        dY[b] = (uint32_t)(fsY + 16 * (tY[b] ? q - nY : q));
-        tC[b] = q >= nC;
-        vC[b] = q < nchC;
-        dC[b] = (uint32_t)(fsC + 16 * (tC[b] ? q - nC : q));
-    }
-    const __amdgpu_buffer_rsrc_t rsY = __builtin_amdgcn_make_buffer_rsrc((void*)p0, (short)0, 0x7FFFFFFF, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rsU = __builtin_amdgcn_make_buffer_rsrc((void*)p1, (short)0, 0x7FFFFFFF, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rsV = __builtin_amdgcn_make_buffer_rsrc((void*)(NPC == 2 ? p2 : p1), (short)0, 0x7FFFFFFF, 0x00020000);
-    int pos = 0;   // vector-memory operations this wave issued (wave-uniform)
-    int dpos = 0;  // lane vi: pos right after visible row vi's DMA
-    int issued = 0, e_iss = 0;  // visible rows issued; the ring entry of the next one
-    auto issue = [&]() {  // DMA of visible row `issued` into ring entry e_iss
-        const int lr = issued + voff;
-        const int ya = y0 + __builtin_amdgcn_readlane(lr0, lr), yb = y0 + __builtin_amdgcn_readlane(lr1, lr);
-        const int ca = ya >> 1, cb = yb >> 1;
-        uint8_t* const eb = wbuf + e_iss * E;
-#pragma unroll
-        for (int b = 0; b < 2; b++) {
-            if (b < niY) {
-                if (vY[b])
-                    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsY, (__attribute__((address_space(3))) void*)(eb + 1024 * b), 16,
-                                                             (uint32_t)((tY[b] ? yb : ya) * pitch0) + dY[b], 0, 0, EVAM_PP_LOAD_AUX);
-                pos++;
-            }
-        }
-#pragma unroll
-        for (int b = 0; b < 2; b++) {
-            if (b < niC) {
-                const bool on = vC[b] && !(tC[b] && ca == cb);  // a chroma row both taps share is staged once
-                if (on)
-                    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsU, (__attribute__((address_space(3))) void*)(eb + offC + 1024 * b),
-                                                             16, (uint32_t)((tC[b] ? cb : ca) * pitch1) + dC[b], 0, 0, EVAM_PP_LOAD_AUX);
-                const int k = __builtin_amdgcn_ballot_w64(on) != 0 ? 1 : 0;
-                pos += k;
-                if constexpr (NPC == 2) {
-                    if (on)
-                        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsV, (__attribute__((address_space(3))) void*)(eb + offC + 16 * nchC + 1024 * b),
-                                                                 16, (uint32_t)((tC[b] ? cb : ca) * pitch2) + dC[b], 0, 0, EVAM_PP_LOAD_AUX);
-                    pos += k;
-                }
-            }
-        }
-        dpos = lane == issued ? pos : dpos;
-        issued++;
-        e_iss = e_iss + 1 == Dr ? 0 : e_iss + 1;
-    };
-    const bool lut_early = nw >= 3;
-    if constexpr (OUT == 1) {
-        if (lut_early && wave < 3) {
-            const __amdgpu_buffer_rsrc_t rsL = __builtin_amdgcn_make_buffer_rsrc((void*)k_lut, (short)0, 3072, 0x00020000);
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsL, (__attribute__((address_space(3))) void*)(lut_s + wave * 256), 16,
-                                                     (uint32_t)lane * 16u, (k_rgb ? 2 - wave : wave) * 1024, 0, 0);
-            pos++;
-        }
-    }
-    const int lut_pos = pos;
-    while (issued < min(n, Dr)) issue();
-    EVAM_WSTAMP(1);
-    // the item's column table (shared by the workgroup's waves): tap offsets inside the staged segments, packed
-    // weights; bit 31: a letterbox column
-    for (int X = threadIdx.x; X < DW; X += nw * 64) {
-        uint2 e = uint2{0x80000000u, 0u};
-        const int dx = X - ox;
-        if (cols && dx >= 0 && dx < rw) {
-            int s0, a0, a1;
-            linear_coef(dx, scx, cw, true, s0, a0, a1);
-            const int ca = x0 + s0;  // tap 1 reads ca + 1: at the right edge (s0 = cw - 1) its weight a1 is 0
-            const uint32_t oY = (uint32_t)(ca - fsY);
-            uint32_t oC0, oC1;
-            if constexpr (FMT == kNV12) {
-                oC0 = (uint32_t)(2 * (ca >> 1) - fsC);
-                oC1 = (uint32_t)(2 * ((ca + 1) >> 1) - fsC);
-            } else {
-                oC0 = (uint32_t)((ca >> 1) - fsC);
-                oC1 = (uint32_t)(((ca + 1) >> 1) - fsC);
-            }
-            e = uint2{oY | (oC0 << 11) | ((oC1 - oC0) << 22), (uint32_t)a0 | ((uint32_t)a1 << 16)};
-        }
-        colTab[X] = e;
-    }
-    const size_t esz = OUT == 1 ? 4 : 1;
-    const size_t plane = (size_t)DW * DH;
-    uint8_t* const d0 = reinterpret_cast<uint8_t*>(P.dst) + (size_t)(P.slot_offset + index * P.slot_stride) * 3 * plane * esz;
-    uint8_t* const d1 = d0 + plane * esz;
-    uint8_t* const d2 = d1 + plane * esz;
-    const __amdgpu_buffer_rsrc_t rsO0 = __builtin_amdgcn_make_buffer_rsrc((void*)(k_rgb ? d2 : d0), (short)0, 0x7FFFFFFF, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rsO1 = __builtin_amdgcn_make_buffer_rsrc((void*)d1, (short)0, 0x7FFFFFFF, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rsO2 = __builtin_amdgcn_make_buffer_rsrc((void*)(k_rgb ? d0 : d2), (short)0, 0x7FFFFFFF, 0x00020000);
-    const uint32_t fq0 = P.fill & 0xFF, fq1 = (P.fill >> 8) & 0xFF, fq2 = (P.fill >> 16) & 0xFF;
-    const uint32_t fsh = OUT == 1 ? 2 : 0;
-    const uint32_t fill0 = (k_rgb ? fq2 : fq0) << fsh, fill1 = fq1 << fsh, fill2 = (k_rgb ? fq0 : fq2) << fsh;
-    if constexpr (OUT == 1) {
-        if (lut_early) {
-            vmcnt_le(pos - lut_pos);  // this wave's LUT section landed; the ring's DMA stays in flight
-            lds_barrier();            // ... and the column table is visible
-        } else {  // workgroups of 1-2 waves
-            for (int idx = threadIdx.x; idx < 768; idx += nw * 64)
-                lut_s[idx] = k_lut[k_rgb ? 512 - (idx & ~255) + (idx & 255) : idx];
-            __syncthreads();
-        }
-    } else {
-        lds_barrier();  // the column table is visible
-    }
-    EVAM_WSTAMP(2);
-    const uint8_t* lutb = reinterpret_cast<const uint8_t*>(lut_s);
-    uint32_t kb = kKBs, kg = kKGs, kr = kKRs;
-    int cvg = kCVG, cug = kCUG;
-    asm volatile("" : "+v"(kb), "+v"(kg), "+v"(kr), "+s"(cvg), "+s"(cug));
-    auto uvt = [&](uint32_t U, uint32_t V) {
-        int gu = __mul24((int)U, cug) + (int)kg;
-        asm("" : "+v"(gu));
-        return UVs{__umul24(U, (uint32_t)kCUB) + kb, (uint32_t)(__mul24((int)V, cvg) + gu), __umul24(V, (uint32_t)kCVR) + kr};
-    };
-    // the flat run: pixel p = 64 s + lane of the band is (row r, column c); stores at plane offset Y0 * DW + p
-    const int T = rows * DW;
-    int r = lane / DW, c = lane - (lane / DW) * DW;
-    const int so = (int)((uint32_t)(Y0 * DW) * (uint32_t)esz);
-    // progress-based priority (EVAM_PP_PRIO): 3 -> 0 over the quarters of the wave's pixels
-    const int pq1 = P.prio ? (T / 4) & ~63 : -1, pq2 = P.prio ? (T / 2) & ~63 : -1, pq3 = P.prio ? (3 * T / 4) & ~63 : -1;
-    if (P.prio) __builtin_amdgcn_s_setprio(3);
-    for (int p0s = 0; p0s < T; p0s += 64) {
-        if (p0s == pq1) __builtin_amdgcn_s_setprio(2);
-        else if (p0s == pq2) __builtin_amdgcn_s_setprio(1);
-        else if (p0s == pq3) __builtin_amdgcn_s_setprio(0);
-        // rows this step touches: lane 0's and lane 63's (clamped to the band); wait for the last visible one's DMA
-        const int rlo = __builtin_amdgcn_readfirstlane(r);
-        const int rhi = min(__builtin_amdgcn_readlane(r, 63), rows - 1);
-        const int vhi = min(rhi - voff, n - 1);
-        if (vhi >= 0) vmcnt_le(pos - __builtin_amdgcn_readlane(dpos, vhi));
-#ifdef EVAM_PP_TRACE
-        if (p0s == 0) EVAM_WSTAMP(3);
-#endif
-        const bool live = p0s + lane < T;
-        const int rr = min(r, rows - 1);
-        const uint2 ct = colTab[c];
-        const uint4 rt = rowTab[rr];
-        const uint32_t oY = ct.x & 0x7FF, oC0 = (ct.x >> 11) & 0x7FF, dCo = (ct.x >> 22) & 3;
-        const uint32_t soC = rt.w & 0xFFFF;
-        const uint8_t* const eb = wbuf + rt.z;
-        const uint8_t* ay = eb + oY;
-        const uint8_t* ac0 = eb + offC + oC0;
-        const uint8_t* ac1 = ac0 + dCo;
-        const uint32_t yA = luma_term(ay[0]), yB = luma_term(ay[1]);
-        const uint32_t yC = luma_term(ay[segY]), yD = luma_term(ay[segY + 1]);
-        UVs tA, tB, tC, tE;
-        if constexpr (FMT == kNV12) {
-            tA = uvt(ac0[0], ac0[1]);
-            tB = uvt(ac1[0], ac1[1]);
-            tC = uvt(ac0[soC], ac0[soC + 1]);
-            tE = uvt(ac1[soC], ac1[soC + 1]);
-        } else {
-            const int oV = 16 * nchC;  // the V plane's chunks follow the U plane's
-            tA = uvt(ac0[0], ac0[oV]);
-            tB = uvt(ac1[0], ac1[oV]);
-            tC = uvt(ac0[soC], ac0[oV + soC]);
-            tE = uvt(ac1[soC], ac1[oV + soC]);
-        }
-        const uint32_t wp = ct.y;
-        uint32_t h0[3], h1[3];
-        h0[0] = hpass_sat(yA, tA.b, yB, tB.b, wp);
-        h0[1] = hpass_sat(yA, tA.g, yB, tB.g, wp);
-        h0[2] = hpass_sat(yA, tA.r, yB, tB.r, wp);
-        h1[0] = hpass_sat(yC, tC.b, yD, tE.b, wp);
-        h1[1] = hpass_sat(yC, tC.g, yD, tE.g, wp);
-        h1[2] = hpass_sat(yC, tC.r, yD, tE.r, wp);
-        uint32_t v[3];
-#pragma unroll
-        for (int k = 0; k < 3; k++) v[k] = vfinal<OUT>(h0[k], h1[k], rt.x, rt.y);
-        const bool fl = ((ct.x | rt.w) >> 31) != 0;  // letterbox column or row
-        v[0] = fl ? fill0 : v[0];
-        v[1] = fl ? fill1 : v[1];
-        v[2] = fl ? fill2 : v[2];
-        if (live) {
-            const uint32_t vo = (uint32_t)(p0s + lane) * (uint32_t)esz;
-            if constexpr (OUT == 1) {
-                __builtin_amdgcn_raw_buffer_store_b32(*reinterpret_cast<const uint32_t*>(lutb + v[0]), rsO0, vo, so, EVAM_PP_STORE_AUX);
-                __builtin_amdgcn_raw_buffer_store_b32(*reinterpret_cast<const uint32_t*>(lutb + 1024 + v[1]), rsO1, vo, so, EVAM_PP_STORE_AUX);
-                __builtin_amdgcn_raw_buffer_store_b32(*reinterpret_cast<const uint32_t*>(lutb + 2048 + v[2]), rsO2, vo, so, EVAM_PP_STORE_AUX);
-            } else {
-                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v[0], rsO0, vo, so, EVAM_PP_STORE_AUX);
-                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v[1], rsO1, vo, so, EVAM_PP_STORE_AUX);
-                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v[2], rsO2, vo, so, EVAM_PP_STORE_AUX);
-            }
-        }
-        pos += 3;
-        asm volatile("" ::: "memory");  // issue order is what the counted waits assume
-        // advance every lane by 64 pixels; rows below the next step's first row are done: refill their entries
-        c += m64;
-        r += q64;
-        if (c >= DW) { c -= DW; r++; }
-        const int vlo = __builtin_amdgcn_readfirstlane(r) - voff;  // first visible row the next step reads
-        while (issued < n && issued < vlo + Dr) issue();
-        asm volatile("" ::: "memory");
-        (void)rlo;
-    }
-#ifdef EVAM_PP_TRACE
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    EVAM_WSTAMP(4);
-    EVAM_WTRACE_VAL(5, (unsigned long long)index | ((unsigned long long)Dr << 16) | ((unsigned long long)E << 32) |
-                           ((unsigned long long)n << 48));
-#endif
 }
 
 // Band kernel for uniform 4:2:0 batches whose consecutive output rows share source rows (vertical
@@ -3175,17 +2813,11 @@ struct Knobs {
                                                                               // rows per tile, ring depth, waves, px
     int strip_waves = 16;                          // strip / band kernels: resident waves per CU the tiles are sized for
     int band = 1, band_px = 0;                     // band kernel: allowed (2: forced), pixels per lane
-    int roi_dense = 0, roi_dense_waves = 4;        // 4:2:0 ROI batches on the dense ROI kernel (1) or the ROI kernel (0,
-                                                   // C3: 52.8 vs 61.0 us, profiles/r04k_ab_lines.txt); its waves per workgroup
-    int roi_ring = -1;                             // dense ROI kernel: ring bytes per wave (-1: the LDS budget, <= 8 KB)
     int prio = 1;                                  // progress-based wave priority (strip, band, ROI kernels): C2 +3 %,
                                                    // C4 +3 %, C5 +3-5 %, C1 +9 % (profiles/r04k_ab_lines.txt)
     int band_ahead = 2;                            // band kernel: source rows issued ahead of the current output row's
                                                    // (64: the whole band at once; 2 measured +2 % on C1)
     void read() {
-        roi_dense = env_int("EVAM_PP_ROI_DENSE", roi_dense);
-        roi_dense_waves = env_int("EVAM_PP_ROI_DENSE_WAVES", roi_dense_waves);
-        roi_ring = env_int("EVAM_PP_ROI_RING", roi_ring);
         prio = env_int("EVAM_PP_PRIO", prio);
         band_ahead = env_int("EVAM_PP_BAND_AHEAD", band_ahead);
         band = env_int("EVAM_PP_BAND", band); band_px = env_int("EVAM_PP_BAND_PX", band_px);
@@ -3649,79 +3281,6 @@ hipError_t launch_strip(int f, int out, int d, int px, const TParams& p, dim3 gr
     case (kBGRX * 2 + 1) * 2: return launch_strip_t<kBGRX, 1, 1>(d, p, grid, lds, s);
     default: return launch_strip_t<kBGRX, 1, 2>(d, p, grid, lds, s);
     }
-}
-
-template <int FMT, int OUT>
-hipError_t launch_roid_t(const WRParams& p, int grid, int nw, int lds, hipStream_t s) {
-    if (lds > 64 * 1024) {
-        hipError_t e = hipFuncSetAttribute((const void*)evam_pp_roid<FMT, OUT>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-        if (e != hipSuccess) return e;
-    }
-    hipLaunchKernelGGL((evam_pp_roid<FMT, OUT>), dim3(grid), dim3(64 * nw), lds, s, p);
-    return hipGetLastError();
-}
-const void* roid_fn(int f, int out) {
-    switch (f * 2 + out) {
-    case kNV12 * 2 + 0: return (const void*)evam_pp_roid<kNV12, 0>;
-    case kNV12 * 2 + 1: return (const void*)evam_pp_roid<kNV12, 1>;
-    case kI420 * 2 + 0: return (const void*)evam_pp_roid<kI420, 0>;
-    default: return (const void*)evam_pp_roid<kI420, 1>;
-    }
-}
-hipError_t launch_roid(int f, int out, const WRParams& p, int grid, int nw, int lds, hipStream_t s) {
-    switch (f * 2 + out) {
-    case kNV12 * 2 + 0: return launch_roid_t<kNV12, 0>(p, grid, nw, lds, s);
-    case kNV12 * 2 + 1: return launch_roid_t<kNV12, 1>(p, grid, nw, lds, s);
-    case kI420 * 2 + 0: return launch_roid_t<kI420, 0>(p, grid, nw, lds, s);
-    default: return launch_roid_t<kI420, 1>(p, grid, nw, lds, s);
-    }
-}
-// Dense ROI kernel plan for a 4:2:0 group with per-item geometry (gvaclassify batches: C3).
-struct RoiDensePlan {
-    int nbw, lds, tiles;  // waves (row bands) per workgroup, dynamic LDS, row tiles (units) per ROI
-    int unit_rows;        // output rows of one unit (the last may be shorter)
-    int rt_rows;          // row-table rows per wave (the most rows of one band, <= 64)
-    int ring_bytes;       // one wave's ring
-};
-//  * Waves: nbw row bands of all DW columns (EVAM_PP_ROI_DENSE_WAVES, default 4: 18 rows each at 72 x 72); ROIs taller
-//    than nbw x 64 output rows become several row tiles (units).
-//  * Footprint bound: a row's taps span at most max_cw + 1 source pixels of any crop of the group; it must fit two DMA
-//    instructions per plane (64 16-byte chunks per tap segment).
-//  * Ring: at least the rows one 64-pixel step reads (ceil(63 / DW) + 1) of the widest footprint; the rest of the budget
-//    — the CU's LDS shared by the workgroups one round needs (C3: 1,600 ROIs -> 7 per CU), at most 8 KB per wave —
-//    lets narrow crops run deeper rings.
-// Returns false where the ROI kernel must serve the group (packed formats, wider footprints, DW < 10).
-bool plan_roi_dense(int f, int DW, int DH, int out_dtype, int max_cw, int count, int n_cu, const Knobs& kn,
-                    RoiDensePlan& r) {
-    if ((f != kNV12 && f != kI420) || DH > 65535) return false;
-    const int chunks = (max_cw + 1 + 32) / 16 + 1;  // 16-byte windows of the luma (and NV12 chroma) footprint
-    if (chunks > 64) return false;
-    const int step_rows = (63 + DW - 1) / DW + 1;
-    if (step_rows + 1 > kRingMax) return false;  // DW < 10: 64 pixels span more rows than a ring holds
-    r.nbw = std::max(1, std::min(8, kn.roi_dense_waves));
-    r.unit_rows = std::min(DH, r.nbw * 64);
-    r.tiles = (DH + r.unit_rows - 1) / r.unit_rows;
-    r.rt_rows = (r.unit_rows + r.nbw - 1) / r.nbw;
-    const int npc = f == kI420 ? 2 : 1;
-    const int lut_static = out_dtype == EVAM_DTYPE_F32 ? kLutBytes : 16;
-    const int emax = 16 * (2 * chunks + 2 * npc * chunks);
-    const int fixed = ((DW * 8 + 15) & ~15) + r.nbw * r.rt_rows * 16;  // colTab + rowTabs
-    const int64_t units = (int64_t)count * r.tiles;
-    const int per_cu = (int)std::max<int64_t>(1, std::min<int64_t>(8, (units + n_cu - 1) / n_cu));
-    // LDS is allocated in 1 KB granules per workgroup (static LUT included)
-    int rb = ((((160 * 1024) / per_cu) & ~1023) - lut_static - 16 - fixed) / r.nbw & ~15;
-    if (kn.roi_ring > 0) rb = kn.roi_ring & ~15;
-    rb = std::min(rb, 8 * 1024);
-    const int rmin = step_rows * emax;  // the rows one step reads, of the widest footprint
-    r.ring_bytes = std::max(rb, rmin);
-    r.lds = fixed + r.nbw * r.ring_bytes + 16;  // + 16: a right-edge tap reads past its footprint (weight 0)
-    if (r.lds + lut_static > 160 * 1024) return false;
-    const void* fn = roid_fn(f, out_dtype);
-    while (kn.roi_ring <= 0 && resident_per_cu(fn, r.lds, 64 * r.nbw) < per_cu && r.ring_bytes - 256 >= rmin) {
-        r.ring_bytes -= 256;
-        r.lds = fixed + r.nbw * r.ring_bytes + 16;
-    }
-    return true;
 }
 
 template <int FMT, int OUT>
@@ -4280,11 +3839,9 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
     //   uniform geometry        -> staged / wave / row kernels: host-built tables, items in kernel arguments
     //   per-item geometry       -> ROI kernel: raw ROI rect + source (RoiRec), geometry resolved on the device
     //   ROI plan impossible     -> generic kernel, per-item ItemDesc in the descriptor block
-    //   per-item geometry, 4:2:0 -> dense ROI kernel (RoiRec per row tile, geometry resolved on the device)
-    enum { kPathNone, kPathUniform, kPathRoi, kPathGeneric, kPathRoiDense };
+    enum { kPathNone, kPathUniform, kPathRoi, kPathGeneric };
     int path[4];
     QParams qp[4];
-    RoiDensePlan rsp[4];
     int qlds[4] = {0, 0, 0, 0}, qbase[4] = {1, 1, 1, 1}, qrec[4] = {0, 0, 0, 0};
     int64_t qslots[4] = {0, 0, 0, 0};
     bool any_generic = false, any_roi = false;
@@ -4292,20 +3849,18 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
         path[f] = kPathNone;
         if (!count[f]) continue;
         if (uniform[f] && kn.rows) path[f] = kPathUniform;
-        else if (kn.roi && kn.roi_dense &&
-                 plan_roi_dense(f, DW, DH, cfg->out_dtype, max_cw[f], count[f], h->n_cu, kn, rsp[f])) path[f] = kPathRoiDense;
         else if (kn.roi && plan_roi(f, DW, DH, cfg->out_dtype, kn.roi_px, row_bytes_bound(f, max_cw[f]), count[f], h->n_cu,
                                     kn, qp[f], qbase[f], qlds[f], qslots[f])) path[f] = kPathRoi;
         else path[f] = kPathGeneric;
         any_generic |= path[f] == kPathGeneric;
-        any_roi |= path[f] == kPathRoi || path[f] == kPathRoiDense;
+        any_roi |= path[f] == kPathRoi;
     }
     // Full geometry on the host only where something consumes it.
     const bool all_geo = out_xform != nullptr || h->opt_stats;
     int64_t src_bytes = 0;
     for (int i = 0; i < n_items; i++) {
         const int f = fmt[i];
-        if (!all_geo && (path[f] == kPathRoi || path[f] == kPathRoiDense)) continue;
+        if (!all_geo && path[f] == kPathRoi) continue;
         if (!all_geo && path[f] == kPathUniform && i != rep[f]) continue;  // same crop size: rep's geometry
         Geom& g = geo[i];
         const evam_roi* r = items ? &items[i] : nullptr;
@@ -4345,11 +3900,6 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
     size_t rec_off[4] = {0, 0, 0, 0}, dyn_bytes = 0;
     if (any_roi) {
         for (int f = 0; f < 4; f++) {
-            if (path[f] == kPathRoiDense) {
-                rec_off[f] = dyn_bytes;
-                dyn_bytes += sizeof(RoiRec) * (size_t)count[f] * (size_t)rsp[f].tiles;
-                continue;
-            }
             if (path[f] != kPathRoi) continue;
             rec_off[f] = dyn_bytes;
             // at most ceil(groups / roi_unit) <= DH units per ROI when base tiles are split
@@ -4426,28 +3976,6 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
         std::vector<int>& bucket = h->sc_bucket;
         bucket.resize(n_items);
         for (int f = 0; f < 4; f++) {
-            if (path[f] == kPathRoiDense) {
-                // records in call order, one per row tile: the frame's planes next to the caller's rect (the
-                // kernel resolves the geometry); every ROI does the same output work, so no ordering pass
-                RoiRec* rr = reinterpret_cast<RoiRec*>(dyn + rec_off[f]);
-                const RoiDensePlan& r = rsp[f];
-                for (int m = mfirst[f]; m < mfirst[f + 1]; m++) {
-                    const int i = members[m];
-                    const evam_image& sim = srcs[items ? items[i].src_index : i];
-                    for (int t = 0; t < r.tiles; t++, rr++) {
-                        rr->plane[0] = sim.planes[0]; rr->plane[1] = sim.planes[1]; rr->plane[2] = sim.planes[2];
-                        rr->pitch[0] = sim.pitch[0]; rr->pitch[1] = sim.pitch[1]; rr->pitch[2] = sim.pitch[2];
-                        rr->width = (uint16_t)sim.width; rr->height = (uint16_t)sim.height;
-                        if (items) { rr->x = items[i].x; rr->y = items[i].y; rr->w = items[i].w; rr->h = items[i].h; }
-                        else { rr->x = rr->y = rr->w = rr->h = 0; }  // w <= 0: the full frame
-                        rr->item = i;
-                        rr->row0 = (uint16_t)(t * r.unit_rows);
-                        rr->row1 = (uint16_t)std::min(DH, (t + 1) * r.unit_rows);
-                    }
-                }
-                qrec[f] = count[f] * r.tiles;
-                continue;
-            }
             if (path[f] != kPathRoi) continue;
             RoiRec* rr = reinterpret_cast<RoiRec*>(dyn + rec_off[f]);
             std::vector<int>& ord = h->sc_order;
@@ -4598,28 +4126,6 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
     };
     for (int f = 0; f < 4; f++) {
         if (path[f] == kPathNone) continue;
-        if (path[f] == kPathRoiDense) {
-            const RoiDensePlan& r = rsp[f];
-            WRParams w{};
-            w.recs = reinterpret_cast<const RoiRec*>(d_dyn + rec_off[f]);
-            w.lut = lut_d;
-            w.dst = dst->data;
-            w.slot_offset = dst->slot_offset;
-            w.slot_stride = dst->slot_stride;
-            w.DW = DW; w.DH = DH;
-            w.mode = cfg->resize_mode;
-            w.placement = cfg->placement;
-            w.nbw = r.nbw;
-            w.ring_bytes = r.ring_bytes;
-            w.rt_rows = r.rt_rows;
-            w.prio = kn.prio;
-            w.color_rgb = color_rgb;
-            w.fill = fill;
-            hipError_t e = launch_roid(f, cfg->out_dtype, w, qrec[f], r.nbw, r.lds, h->stream);
-            if (e != hipSuccess) return fail(EVAM_PP_ERR_HIP, "kernel launch failed: %s", hipGetErrorString(e));
-            launches++; kmask |= EVAM_KERNEL_ROI_DENSE;
-            continue;
-        }
         if (path[f] == kPathRoi) {
             QParams& q = qp[f];
             q.recs = reinterpret_cast<const RoiRec*>(d_dyn + rec_off[f]);

@@ -139,7 +139,7 @@ typedef struct evam_pp_stats {
 /* evam_pp_stats.kernels bits (diagnostics: which kernel family served a call). */
 enum evam_kernel_family {
     EVAM_KERNEL_GENERIC = 1, EVAM_KERNEL_ROWS = 2, EVAM_KERNEL_STAGED = 4, EVAM_KERNEL_WAVE = 8,
-    EVAM_KERNEL_STRIP = 16, EVAM_KERNEL_BAND = 32, EVAM_KERNEL_ROI = 64, EVAM_KERNEL_ROI_DENSE = 128
+    EVAM_KERNEL_STRIP = 16, EVAM_KERNEL_BAND = 32, EVAM_KERNEL_ROI = 64
 };
 
 enum evam_pp_option {

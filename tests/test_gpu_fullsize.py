@@ -94,13 +94,13 @@ def test_c2_bench_batch(evam, O, coracle, gpu, shape, monkeypatch):
     pp.close()
 
 
-@pytest.mark.parametrize("kernel", ["dense", "dense_noprio", "roi_tail1", "roi", "roi_noprio", "roi_sorted"])
+@pytest.mark.parametrize("kernel", ["roi_tail1", "roi", "roi_noprio", "roi_sorted"])
 @pytest.mark.parametrize("seed", [0, 3])
 def test_c3_bench_roi_set(evam, O, coracle, gpu, seed, kernel, monkeypatch):
     """C3: bench.py's seeded ROI set (50 per frame, w 24..400, h 24..300) on 32 bench 1080p NV12 frames ->
-    1600x3x72x72 fp32 through the ROI kernel (the default), with and without its tail split (EVAM_PP_ROI_TAIL: the 64
-    ROIs beyond 6 per CU as row tiles), and the dense ROI kernel (EVAM_PP_ROI_DENSE=1); both with and without
-    progress-based priority (EVAM_PP_PRIO)."""
+    1600x3x72x72 fp32 through the ROI kernel, with and without its tail split (EVAM_PP_ROI_TAIL: the 64 ROIs beyond 6
+    per CU as row tiles), without progress-based priority (EVAM_PP_PRIO=0) and with the largest-bytes pre-order
+    (EVAM_PP_ROI_SORT=1)."""
     import torch
 
     if kernel.endswith("_noprio"):
@@ -108,10 +108,7 @@ def test_c3_bench_roi_set(evam, O, coracle, gpu, seed, kernel, monkeypatch):
         kernel = kernel[:-7]
     if kernel == "roi_sorted":  # largest estimated bytes first before the sort by row groups
         monkeypatch.setenv("EVAM_PP_ROI_SORT", "1")
-    monkeypatch.setenv("EVAM_PP_ROI_DENSE", "1" if kernel == "dense" else "0")
-    if kernel != "dense":
-        monkeypatch.setenv("EVAM_PP_ROI_TAIL", "1" if kernel == "roi_tail1" else "4")
-        kernel = "roi"
+    monkeypatch.setenv("EVAM_PP_ROI_TAIL", "1" if kernel == "roi_tail1" else "4")
 
     wl = bench.WORKLOADS["c3"]
     imgs = bench.device_frames(evam, torch, wl, 32, gpu, seed=1234)
@@ -123,7 +120,7 @@ def test_c3_bench_roi_set(evam, O, coracle, gpu, seed, kernel, monkeypatch):
     pp.convert(imgs, out, info, rois=evam.RoiBatch(np.array(rois, dtype=np.int32)))
     torch.cuda.synchronize()
     N = evam.native
-    assert pp.stats().kernels == {"roi": N.KERNEL_ROI, "dense": N.KERNEL_ROI_DENSE}[kernel]
+    assert pp.stats().kernels == N.KERNEL_ROI
     ref = oracle_items(O, coracle, host_frames(O, imgs), rois, out.shape, "f32", info)
     assert_same(out.cpu().numpy(), ref, f"C3 bench ROI set seed {seed} {kernel}")
     pp.close()

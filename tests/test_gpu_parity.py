@@ -140,14 +140,12 @@ def test_roi_batch(evam, O, coracle, gpu, fmt):
     ((17, 5), "f32", "aspect-ratio", "top_left"),        # K=1, nfull=0
     ((64, 64), "f32", "aspect-ratio", "center"),         # R*DW = 256 exactly
 ])
-@pytest.mark.parametrize("roi_kernel", ["dense", "roi", "generic"])
+@pytest.mark.parametrize("roi_kernel", ["roi", "generic"])
 def test_roi_kernels(evam, O, coracle, gpu, fmt, dst, dtype, resize, placement, roi_kernel, monkeypatch):
-    """Per-item-geometry batches through the dense ROI kernel (4:2:0 default), the staged ROI kernel
-    (EVAM_PP_ROI_DENSE=0; packed formats' default) and the generic one (EVAM_PP_ROI=0)."""
+    """Per-item-geometry batches through the staged ROI kernel (the default) and the generic one (EVAM_PP_ROI=0)."""
     import torch
 
     monkeypatch.setenv("EVAM_PP_ROI", "0" if roi_kernel == "generic" else "1")
-    monkeypatch.setenv("EVAM_PP_ROI_DENSE", "1" if roi_kernel == "dense" else "0")
     rng = np.random.default_rng(zlib.crc32(f"{fmt}{dst}{resize}".encode()))
     W, H = 480, 270
     frames = [O.random_frame(rng, fc(O, fmt), W, H, pattern="gradient" if i else "uniform") for i in range(3)]
@@ -463,7 +461,6 @@ def test_roi_kernel_px4(evam, O, coracle, gpu, fmt, dst, dtype, monkeypatch):
     import torch
 
     monkeypatch.setenv("EVAM_PP_ROI_PX", "4")
-    monkeypatch.setenv("EVAM_PP_ROI_DENSE", "0")  # the ROI kernel (the default; pinned against a default change)
     rng = np.random.default_rng(zlib.crc32(f"px4{fmt}{dst}".encode()))
     W, H = 320, 200
     frames = [O.random_frame(rng, fc(O, fmt), W, H, pattern="gradient" if i else "uniform") for i in range(2)]
@@ -486,7 +483,6 @@ def test_roi_kernel_xcd_order(evam, O, coracle, gpu, fmt, monkeypatch):
     import torch
 
     monkeypatch.setenv("EVAM_PP_ROI_XCD", "1")
-    monkeypatch.setenv("EVAM_PP_ROI_DENSE", "0")  # the ROI kernel (the default; pinned against a default change)
     rng = np.random.default_rng(zlib.crc32(f"xcd{fmt}".encode()))
     W, H = 192, 108
     frames = [O.random_frame(rng, fc(O, fmt), W, H, pattern="gradient" if i % 2 else "uniform") for i in range(11)]
@@ -600,7 +596,6 @@ def test_roi_work_units(evam, O, coracle, gpu, unit, monkeypatch):
     import torch
 
     monkeypatch.setenv("EVAM_PP_ROI_UNIT", unit)
-    monkeypatch.setenv("EVAM_PP_ROI_DENSE", "0")  # the ROI kernel (the default; pinned against a default change)
     rng = np.random.default_rng(zlib.crc32(f"unit{unit}".encode()))
     W, H = 640, 360
     frames = [O.random_frame(rng, O.NV12, W, H, pattern="gradient" if i else "uniform") for i in range(2)]
@@ -623,7 +618,6 @@ def test_roi_tail_split(evam, O, coracle, gpu, tail, dst, monkeypatch):
     import torch
 
     monkeypatch.setenv("EVAM_PP_ROI_TAIL", tail)
-    monkeypatch.setenv("EVAM_PP_ROI_DENSE", "0")  # the ROI kernel (the default; pinned against a default change)
     rng = np.random.default_rng(zlib.crc32(f"tail{tail}{dst}".encode()))
     W, H = 640, 360
     frames = [O.random_frame(rng, O.NV12, W, H, pattern="gradient" if i else "uniform") for i in range(2)]
@@ -646,7 +640,6 @@ def test_roi_kernel_three_buffers(evam, O, coracle, gpu, fmt, buf, monkeypatch):
     import torch
 
     monkeypatch.setenv("EVAM_PP_ROI_NBUF", "3")
-    monkeypatch.setenv("EVAM_PP_ROI_DENSE", "0")  # the ROI kernel (the default; pinned against a default change)
     if buf != "0":
         monkeypatch.setenv("EVAM_PP_ROI_BUF", buf)
     rng = np.random.default_rng(zlib.crc32(f"nb3{fmt}{buf}".encode()))
@@ -664,78 +657,3 @@ def test_roi_kernel_three_buffers(evam, O, coracle, gpu, fmt, buf, monkeypatch):
         assert_same(got, ref, f"roi 3 buffers {fmt} buf={buf} dst={dst}")
 
 
-@pytest.mark.parametrize("fmt", ["NV12", "I420"])
-@pytest.mark.parametrize("kernel", ["dense", "dense_ring", "dense_noprio"])
-@pytest.mark.parametrize("dst,waves,resize", [
-    ((72, 72), "4", "no-aspect-ratio"),      # C3 shape: 4 row bands of 18, a 64-pixel step spans 2 rows
-    ((72, 72), "1", "no-aspect-ratio"),      # one wave walks all 72 rows
-    ((72, 72), "8", "aspect-ratio"),         # 8 bands of 9 rows, letterbox rows / columns
-    ((48, 300), "4", "no-aspect-ratio"),     # 300 rows: two row tiles of 256 / 44
-    ((300, 70), "4", "crop"),                # aspect + central crop
-    ((520, 33), "8", "aspect-ratio"),        # narrow letterboxed rows, 8 bands of 4-5 rows
-    ((16, 40), "2", "aspect-ratio"),         # one step spans 5 rows
-    ((12, 20), "4", "no-aspect-ratio"),      # 7 rows per step (the deepest span a ring takes)
-])
-def test_roi_dense_kernel(evam, O, coracle, gpu, fmt, kernel, dst, waves, resize, monkeypatch):
-    """The dense ROI kernel (per-item geometry resolved on the device from each RoiRec; each wave's band rows x DW
-    pixels walked 64 per step): every band layout (EVAM_PP_ROI_DENSE_WAVES), steps spanning up to 7 rows, row tiles
-    for outputs taller than the bands hold, crops whose footprints need two DMA instructions per plane (up to ~900 px
-    wide) next to tiny and partially outside ones, every resize mode, the fewest ring bytes (dense_ring: the widest
-    footprint runs the shallowest ring, narrow crops deeper) and without progress-based priority (dense_noprio); u8 and fp32
-    against the oracle."""
-    import torch
-
-    monkeypatch.setenv("EVAM_PP_ROI_DENSE", "1")
-    monkeypatch.setenv("EVAM_PP_ROI_DENSE_WAVES", waves)
-    if kernel == "dense_ring":
-        monkeypatch.setenv("EVAM_PP_ROI_RING", "16")  # the fewest bytes: the widest footprint runs the shallowest ring
-    if kernel == "dense_noprio":
-        monkeypatch.setenv("EVAM_PP_PRIO", "0")
-    rng = np.random.default_rng(zlib.crc32(f"rs{fmt}{dst}{waves}{resize}".encode()))
-    W, H = 1280, 720
-    frames = [O.random_frame(rng, fc(O, fmt), W, H, pattern="gradient" if i else "uniform") for i in range(3)]
-    rois = []
-    for k in range(45):
-        si = k % 3
-        w, h = int(rng.integers(2, 900 if k % 5 == 0 else 300)), int(rng.integers(2, 600 if k % 7 == 0 else 200))
-        x, y = int(rng.integers(-40, W - 2)), int(rng.integers(-40, H - 2))
-        rois.append((si, x, y, max(w, 2 - x), max(h, 2 - y)))
-    rois += [(0, 0, 0, W, H), (1, W - 2, H - 2, 9, 9), (2, 101, 51, 1, 1), (0, 10, 20, 0, 0)]  # w=0: the full frame
-    kw = {"resize": "aspect-ratio", "crop": "central"} if resize == "crop" else {"resize": resize}
-    for dtype in ("u8", "f32"):
-        info = evam.PreProcInfo(placement="center", fill=(9, 99, 199), color_space="RGB", **kw,
-                                **({"range": (0.0, 1.0), "mean": (0.1, 0.2, 0.3), "std": (0.3, 0.2, 0.1)}
-                                   if dtype == "f32" else {}))
-        shape = (len(rois), 3, dst[1], dst[0])
-        tdt = torch.float32 if dtype == "f32" else torch.uint8
-        got, _ = run_hip(evam, torch, upload(evam, frames, gpu), shape, tdt, info, rois=[evam.Roi(*r) for r in rois])
-        ref, _ = run_oracle(O, coracle, frames, shape, dtype, info, rois=rois)
-        assert_same(got, ref, f"roi dense {kernel} {fmt} {dst} waves={waves} {resize} {dtype}")
-
-
-def test_roi_dense_selected(evam, O, gpu, monkeypatch):
-    """With EVAM_PP_ROI_DENSE=1, 4:2:0 ROI batches run on the dense ROI kernel (one launch) and packed formats keep
-    the ROI kernel; by default (measured faster on C3) every format runs the ROI kernel. Checked through the kernel
-    families the library reports for the call (evam_pp_stats.kernels)."""
-    import torch
-
-    N = evam.native
-    rng = np.random.default_rng(4)
-    rois = [evam.Roi(i % 2, 10 * i, 5 * i, 50 + i, 40 + 2 * i) for i in range(8)]
-    monkeypatch.setenv("EVAM_PP_ROI_DENSE", "1")
-    for fmt, want in (("NV12", N.KERNEL_ROI_DENSE), ("I420", N.KERNEL_ROI_DENSE), ("BGRX", N.KERNEL_ROI)):
-        frames = [O.random_frame(rng, fc(O, fmt), 320, 240) for _ in range(2)]
-        out = torch.zeros((8, 3, 72, 72), dtype=torch.float32, device=gpu)
-        pp = evam.HipPreProcessor(device=0)
-        pp.convert(upload(evam, frames, gpu), out, evam.PreProcInfo(range=(0.0, 1.0)), rois=rois)
-        torch.cuda.synchronize()
-        st = pp.stats()
-        assert st.n_launches == 1 and st.kernels == want, (fmt, st.kernels)
-        pp.close()
-    monkeypatch.delenv("EVAM_PP_ROI_DENSE")
-    pp = evam.HipPreProcessor(device=0)
-    out = torch.zeros((8, 3, 72, 72), dtype=torch.float32, device=gpu)
-    pp.convert(upload(evam, [O.random_frame(rng, O.NV12, 320, 240)] * 2, gpu), out, None, rois=rois)
-    torch.cuda.synchronize()
-    assert pp.stats().kernels == N.KERNEL_ROI
-    pp.close()

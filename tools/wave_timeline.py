@@ -26,7 +26,7 @@ SLOTS = 12  # kTraceSlots of the trace build
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c4", "c5"])
+    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c4", "c5"])  # C3: tools/roi_timeline.py
     ap.add_argument("--steps", type=int, default=40)
     a = ap.parse_args()
     if "trace" not in os.environ.get("EVAM_PP_LIB", ""):
@@ -44,12 +44,7 @@ def main():
     DW, DH = wl["dst"]
     sets = [evam.ImageBatch(bench.device_frames(evam, torch, wl, n, dev, seed=1234 + 7919 * k)) for k in range(5)]
     dt = torch.float32 if wl["dtype"] == "f32" else torch.uint8
-    rois = None
-    if wl.get("rois"):  # C3: the strip kernel's ROI mode (one workgroup of 4 waves per ROI)
-        import numpy as onp
-        rois = [evam.RoiBatch(onp.array(bench.seed_rois(wl["rois"], n, *wl["src"], seed=k), dtype=onp.int32))
-                for k in range(4)]
-    nout = len(rois[0]) if rois else n * (ring or 1)
+    nout = n * (ring or 1)
     outs = [torch.empty((nout, 3, DH, DW), dtype=dt, device=dev) for _ in range(1 if ring else 5)]
     pp = evam.HipPreProcessor(device=0)
     lib = evam.native.load_library()
@@ -61,7 +56,7 @@ def main():
         if ring:
             pp.convert(sets[t % 5], outs[0], info, slot_offset=t % ring, slot_stride=ring)
         else:
-            pp.convert(sets[t % 5], outs[t % 5], info, rois=rois[t % 4] if rois else None)
+            pp.convert(sets[t % 5], outs[t % 5], info)
     torch.cuda.synchronize()
     cap = 16384
     buf = (ctypes.c_ulonglong * (SLOTS * cap))()
@@ -95,13 +90,6 @@ def main():
             "first row landed (absolute)": dist(t[:, 3]),
             "end (absolute)": dist(end)},
         "us_per_row_after_first": dist(loop / np.maximum(rows, 1)),
-        # dense ROI kernel (slots 7-9): record arrived, geometry + scales, footprint + row table
-        **({"prologue_us_entry_to_record_geometry_rowtable_firstdma": [
-            dist((tr[:, 7].astype(np.int64) - tr[:, 0].astype(np.int64)) * 10 / 1000.0),
-            dist((tr[:, 8].astype(np.int64) - tr[:, 7].astype(np.int64)) * 10 / 1000.0),
-            dist((tr[:, 9].astype(np.int64) - tr[:, 8].astype(np.int64)) * 10 / 1000.0),
-            dist((tr[:, 1].astype(np.int64) - tr[:, 9].astype(np.int64)) * 10 / 1000.0)]}
-           if (tr[:, 9] != 0).all() else {}),
         "end_by_xcc": {int(x): round(float(end[xcc == x].max()), 2) for x in sorted(set(xcc.tolist()))},
         # dispatch-order rank of the wave's workgroup on its CU (linear workgroup index // CUs): the older
         # waves of a SIMD win its issue arbitration (MI355X_MICROARCH.md, Two waves per SIMD, item 2)
