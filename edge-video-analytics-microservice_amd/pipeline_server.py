@@ -461,7 +461,14 @@ class BatchHub:
                         break
                     self._cv.wait(timeout=take)
             try:
-                take[0].stage.run_batch(take, self.pp())
+                # slot 0's handle launches on slot 0's stream: the model call must run on the same stream
+                with self.stream_ctx(0):
+                    s = self.stream(0)
+                    if s is not None:
+                        import torch
+
+                        s.wait_stream(torch.cuda.default_stream(self.device))  # the application's frames
+                    take[0].stage.run_batch(take, self.pp())
                 self.batches.append((key, sum(r.units for r in take), len(take)))
                 if len(self.batches) > 4096:
                     del self.batches[:2048]

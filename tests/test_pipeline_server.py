@@ -311,7 +311,66 @@ def test_end_to_end_action_ring(ps, evam, model_dir, gpu, O):
 
 
 @pytest.mark.gpu
-def test_hub_batches_across_pipelines(ps, evam, model_dir, gpu, O):
+def test_runner_inflight_on_gpu_streams(ps, evam, model_dir, gpu, O):
+    """Two ticks in flight on real HIP streams (the device runner's default): a detector that reads the
+    pre-processed tensor on the GPU (per-frame mean -> confidence) gives every stream the same results, in the same
+    order, as one tick at a time, and the per-frame means equal the oracle's pre-processing of that frame."""
+    import torch
+
+    rng = np.random.default_rng(23)
+    frames = [O.random_frame(rng, O.NV12, 320, 180) for _ in range(3 * 7)]
+    c = O.COracle()
+    ref = np.zeros((len(frames), 3, 64, 64), np.float32)
+    for i, f in enumerate(frames):
+        c.preprocess_item(f, None, ref, i, lut=O.np_norm_lut(0))
+
+    def detector(t):  # stays on the device until the runner copies the output back
+        n = t.shape[0]
+        out = torch.full((n, 1, 7), -1.0, device=t.device)
+        out[:, 0, 0] = 0
+        out[:, 0, 1] = 1
+        out[:, 0, 2] = 0.6 + t.float().mean(dim=(1, 2, 3)) / 1000.0
+        out[:, 0, 3:] = torch.tensor([0.25, 0.25, 0.5, 0.75], device=t.device)
+        return out
+
+    def run(inflight):
+        ps.PipelineServer.start({"pipeline_dir": PIPES, "model_dir": model_dir, "inflight": inflight,
+                                 "batch_target": 4, "batch_max": 4, "batch_wait_ms": 50})
+        ps.PipelineServer.register_model("det_alias/det_ver", ps.InferenceModel(detector, (64, 64), name="det"))
+        pipes, outs = [], []
+        for k in range(3):
+            qin, qout = queue.Queue(), queue.Queue()
+            for f in frames[k::3]:
+                qin.put({"fourcc": f.fourcc, "width": f.width, "height": f.height, "planes": f.planes})
+            qin.put(None)
+            p = ps.PipelineServer.pipeline("detect", "hip")
+            p.start(source={"type": "application", "input": qin},
+                    destination={"metadata": {"type": "application", "output": qout, "mode": "json"}},
+                    parameters={"detection-properties": {"batch-size": 1}})
+            pipes.append(p)
+            outs.append(qout)
+        for p in pipes:
+            assert p.wait(120)["state"] == "COMPLETED"
+        got = []
+        for q in outs:
+            rows = []
+            while (x := q.get(timeout=5)) is not None:
+                rows.append(json.loads(x))
+            got.append(rows)
+        ps.PipelineServer.stop()
+        return got
+
+    one, two = run(1), run(2)
+    assert one == two and [len(g) for g in two] == [7, 7, 7]
+    for k, rows in enumerate(two):
+        for j, d in enumerate(rows):
+            conf = d["objects"][0]["detection"]["confidence"]
+            assert abs(conf - (0.6 + float(ref[k + 3 * j].mean()) / 1000.0)) < 1e-6
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("runner", ["device", "threads"])
+def test_hub_batches_across_pipelines(ps, evam, model_dir, gpu, O, runner):
     """Four application-source pipelines on one device: the batching hub runs ONE detection launch over the
     four streams' frames and ONE ROI launch over their vehicles per tick (the reference runs one pipeline
     per stream, evas/manager.py:127-141, and never batches across them), and every classifier input row is
@@ -335,7 +394,7 @@ def test_hub_batches_across_pipelines(ps, evam, model_dir, gpu, O):
         return {"color": torch.stack([1 - m, m], 1)}
 
     ps.PipelineServer.start({"pipeline_dir": PIPES, "model_dir": model_dir, "batch_target": 4,
-                             "batch_wait_ms": 20000})
+                             "batch_wait_ms": 20000, "runner": runner})
     ps.PipelineServer.register_model("det_alias/det_ver", ps.InferenceModel(detector, (64, 64), name="det"))
     ps.PipelineServer.register_model("cls_alias/cls_ver", ps.InferenceModel(classifier, (24, 24), name="cls"))
     rng = np.random.default_rng(17)
