@@ -664,6 +664,12 @@ class DeviceRunner:
         self._ticks += 1
         failed = set()
         deferred = []  # (completion, chunk)
+        errors = []    # (pipeline, error) of this tick: reported after the previous tick's results went out
+
+        def fail(p, e):
+            failed.add(p)
+            errors.append((p, e))
+
         with hub.stream_ctx(slot):
             s = hub.stream(slot)
             if s is not None:
@@ -684,8 +690,7 @@ class DeviceRunner:
                             continue
                         w, units = st.prepare(items)
                     except Exception as e:  # noqa: BLE001
-                        self._finish(p, e)
-                        failed.add(p)
+                        fail(p, e)
                         continue
                     if units > 0:
                         groups.setdefault(st.hub_key(), []).append((p, _Request(st, w, units, event=False)))
@@ -711,28 +716,32 @@ class DeviceRunner:
                                 del hub.batches[:2048]
                         except Exception as e:  # noqa: BLE001 — delivered to every pipeline of the batch
                             for p, _ in chunk:
-                                self._finish(p, e)
-                                failed.add(p)
+                                fail(p, e)
                             continue
                         if not defer:
-                            self._finish_batch(chunk, failed)
+                            self._finish_batch(chunk, failed, fail)
         tick = (slot, deferred, work, failed)
         prev, self._pending = self._pending, None
         if prev is not None:
             self._complete(prev)
+        for p, e in errors:  # a stream's earlier results (the previous tick) precede its error
+            self._finish(p, e)
         if deferred:
             self._pending = tick
         else:
             self._complete(tick)
 
-    def _finish_batch(self, chunk, failed):
+    def _finish_batch(self, chunk, failed, fail=None):
         for p, r in chunk:
             if p not in failed:
                 try:
                     r.stage.finish(r.items)
                 except Exception as e:  # noqa: BLE001 — this stream's bookkeeping only
-                    self._finish(p, e)
-                    failed.add(p)
+                    if fail is not None:
+                        fail(p, e)
+                    else:
+                        self._finish(p, e)
+                        failed.add(p)
 
     def _complete(self, tick):
         """Complete a tick: its deferred batches (model output to the host, per-stream bookkeeping), then every
@@ -1505,9 +1514,12 @@ class PipelineServer:
 
         ``device``: the model serves only the pipelines placed on that logical device (option ``devices``: its
         weights live on that GPU); register one per device. Without it the model serves every device, and its
-        ``fn`` receives each device's input tensors (it must accept any of them)."""
+        ``fn`` receives each device's input tensors (it must accept any of them); it also replaces the per-device
+        registrations of that key, so the latest registration wins everywhere until a device is bound again."""
         if device is None:
             _SERVER.registry[network_or_key] = model
+            for k in [k for k in _SERVER.registry_dev if k[0] == network_or_key]:
+                del _SERVER.registry_dev[k]
         else:
             _SERVER.registry_dev[(network_or_key, int(device))] = model
 

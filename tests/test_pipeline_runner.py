@@ -435,3 +435,34 @@ def test_runner_keeps_two_ticks_in_flight(stubbed, monkeypatch):
     assert any(pos[("launch", t + 1)] < pos[("complete", t)] for t in range(len(order) - 1))
     handles = [e[2] for e in ev2 if e[0] == "launch"]
     assert len(set(handles)) == 2
+
+
+@pytest.mark.parametrize("inflight", [1, 2])
+def test_runner_error_follows_earlier_results(stubbed, inflight):
+    """A stream whose model fails in a later tick first receives every result of the ticks before it, then its end of
+    stream, in that order, also while a tick is still in flight (inflight 2: the failing tick's error waits for the
+    previous tick's completion)."""
+    ps, pre, mdir = stubbed
+    ps.PipelineServer.start({"pipeline_dir": PIPES, "model_dir": mdir, "batch_max": 2, "batch_target": 2,
+                             "batch_wait_ms": 200, "inflight": inflight})
+    n_calls = [0]
+
+    def detector(t):
+        n_calls[0] += 1
+        if n_calls[0] == 2:
+            raise RuntimeError("model failed on the second batch")
+        return torch.full((t.shape[0], 1, 7), -1.0)
+
+    ps.PipelineServer.register_model("det_alias/det_ver", ps.InferenceModel(detector, (64, 64), name="det"))
+    qin, qout = queue.Queue(), queue.Queue()
+    for im in frames(pre, 6):
+        qin.put(im)
+    qin.put(None)
+    p = ps.PipelineServer.pipeline("detect", "hip")
+    p.start(source={"type": "application", "input": qin},
+            destination={"metadata": {"type": "application", "output": qout, "mode": "json"}},
+            parameters={"detection-properties": {"batch-size": 2}})
+    st = p.wait(30)
+    assert st["state"] == "ERROR" and "second batch" in st.get("message", ""), st
+    got = _drain(qout)
+    assert len(got) == 2  # the first batch's two frames, then the end-of-stream marker
