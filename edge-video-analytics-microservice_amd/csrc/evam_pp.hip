@@ -3337,7 +3337,12 @@ bool plan_band(int f, const Geom& g, int DW, int DH, int count, int out_dtype, i
     const int lut_static = out_dtype == EVAM_DTYPE_F32 ? kLutBytes : 16;
     const int per_launch = std::min(count, kArgItems);
     const int64_t want = (int64_t)std::max(1, std::min(64, kn.strip_waves)) * n_cu;
-    int th = (int)std::max<int64_t>(2, ((int64_t)per_launch * nstrips * DH + want - 1) / want);
+    const int64_t band_rows = (int64_t)per_launch * nstrips * DH;
+    // Small batches (fewer band rows than the waves the chip is sized for: C1 at 1-4 frames) run faster on the wave
+    // kernel: 7.4 vs 8.1 us per launch at 1, 2 and 4 frames, while at 8 frames the band kernel is 19 % ahead
+    // (profiles/r04i_c1_small_batch_ab.txt)
+    if (band_rows <= want && kn.band != 2 && kn.strip_th <= 0) return false;
+    int th = (int)std::max<int64_t>(2, (band_rows + want - 1) / want);
     if (kn.strip_th > 0) th = kn.strip_th;
     th = std::max(1, std::min(std::min(DH, 64), th));
     for (;; th--) {

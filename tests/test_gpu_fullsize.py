@@ -56,6 +56,27 @@ def test_c1_bench_batch(evam, O, coracle, gpu, shape, monkeypatch):
     pp.close()
 
 
+@pytest.mark.parametrize("frames,family", [(1, "WAVE"), (4, "WAVE"), (8, "BAND")])
+def test_c1_small_batches(evam, O, coracle, gpu, frames, family):
+    """C1 at the reference's own batch (1 frame per launch, pipelines/object_detection/vehicle/pipeline.json:5) and
+    other small batches: launches with fewer band rows than the band kernel's wave target run on the wave kernel
+    (faster there, profiles/r04i_c1_small_batch_ab.txt), larger ones on the band kernel; both bit-exact."""
+    import torch
+
+    wl = bench.WORKLOADS["c1"]
+    imgs = bench.device_frames(evam, torch, wl, frames, gpu, seed=77)
+    info = bench.make_info(evam, wl)
+    out = torch.full((frames, 3, 512, 512), 7, dtype=torch.uint8, device=gpu)
+    pp = evam.HipPreProcessor(device=0)
+    pp.convert(imgs, out, info)
+    torch.cuda.synchronize()
+    N = evam.native
+    assert pp.stats().kernels == getattr(N, "KERNEL_" + family), pp.stats().kernels
+    ref = oracle_items(O, coracle, host_frames(O, imgs), [(i, 0, 0, 0, 0) for i in range(frames)], out.shape, "u8", info)
+    assert_same(out.cpu().numpy(), ref, f"C1 batch {frames}")
+    pp.close()
+
+
 # kernel shapes forced on the full-size workloads: the default choice (the strip kernel for C2 / C4 / C5),
 # the strip kernel's other ring depths and tile heights, and the staged kernel's pipeline shapes
 STAGED_SHAPES = {"default": {},
