@@ -2000,20 +2000,29 @@ __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
 #endif
 }
 
-// Wait until at most n (0..63, wave-uniform) vector-memory operations of this wave are outstanding: exact over the
-// whole 6-bit vmcnt range (a jump over immediates).
+// Wait until at most n (>= 0, wave-uniform) vector-memory operations of this wave are outstanding, rounded down to
+// 0-4, 6, 8, 12, 16 or 32: waiting for a few more operations than needed is always safe, and the four-level branch
+// tree costs a third of the scalar instructions of an exact 64-case jump. Same box (profiles/r04k2_vmcnt_coarse_ab.txt):
+// C1 +2 %, C1/I420 +3 % against the exact jump.
 __device__ __forceinline__ void vmcnt_le(int n) {
     n = __builtin_amdgcn_readfirstlane(n);
-#define EVAM_VMC(k) case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
-#define EVAM_VMC8(k) EVAM_VMC(k) EVAM_VMC(k + 1) EVAM_VMC(k + 2) EVAM_VMC(k + 3) EVAM_VMC(k + 4) EVAM_VMC(k + 5) \
-                     EVAM_VMC(k + 6) EVAM_VMC(k + 7)
-    switch (n) {
-        EVAM_VMC8(0) EVAM_VMC8(8) EVAM_VMC8(16) EVAM_VMC8(24) EVAM_VMC8(32) EVAM_VMC8(40) EVAM_VMC8(48)
-        EVAM_VMC(56) EVAM_VMC(57) EVAM_VMC(58) EVAM_VMC(59) EVAM_VMC(60) EVAM_VMC(61) EVAM_VMC(62)
-        default: asm volatile("s_waitcnt vmcnt(63)" ::: "memory"); break;
+    if (n >= 16) {
+        if (n >= 32) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    } else if (n >= 8) {
+        if (n >= 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    } else if (n >= 4) {
+        if (n >= 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else if (n >= 2) {
+        if (n >= 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    } else if (n == 1) {
+        asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+    } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-#undef EVAM_VMC8
-#undef EVAM_VMC
 }
 
 // Band kernel for uniform 4:2:0 batches whose consecutive output rows share source rows (vertical
