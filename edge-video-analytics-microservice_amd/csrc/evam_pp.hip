@@ -34,12 +34,14 @@
 #include <string>
 #include <type_traits>
 #include <vector>
+#include <immintrin.h>
 
 #include "../../include/evam_pp.h"
 
 #define EVAM_HD __host__ __device__
 #include "evam_geom.h"
 #include "evam_rings.h"
+#include "evam_clip_simd.h"
 
 namespace {
 
@@ -2826,7 +2828,9 @@ struct Knobs {
                                                    // C4 +3 %, C5 +3-5 %, C1 +9 % (profiles/r04k_ab_lines.txt)
     int band_ahead = 2;                            // band kernel: source rows issued ahead of the current output row's
                                                    // (64: the whole band at once; 2 measured +2 % on C1)
+    int host_simd = 1;                             // ROI calls: pass 1 on AVX2 (0: scalar)
     void read() {
+        host_simd = env_int("EVAM_PP_HOST_SIMD", host_simd);
         prio = env_int("EVAM_PP_PRIO", prio);
         band_ahead = env_int("EVAM_PP_BAND_AHEAD", band_ahead);
         band = env_int("EVAM_PP_BAND", band); band_px = env_int("EVAM_PP_BAND_PX", band_px);
@@ -3560,6 +3564,7 @@ struct evam_pp {
     std::vector<int> sc_units;     // ROI work units: (item, row0, row1, cost)
     std::vector<int> sc_start;     // ROI unit counting sort: bucket starts
     std::vector<int> sc_slot;      // ROI units in launch order
+    std::vector<int> sc_xq[8];     // ROI units per XCD (EVAM_PP_ROI_XCD)
     int memo_key[4] = {-1, -1, -1, -1};  // (format, staging buffer, row cap, DH) of memo_rg
     std::vector<uint32_t> memo_rg;       // per crop width: rows per group | groups of the whole height << 16
     TParams sc_tparams;            // strip-kernel arguments (3.5 KB: kept off the stack)
@@ -3789,12 +3794,20 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
     }
     std::vector<int>& sfmt = h->sc_sfmt;  // per source: format id (looked up once, not per ROI)
     sfmt.resize(n_srcs);
-    bool one_fmt = true;
+    bool one_fmt = true, one_size = true;
     for (int i = 0; i < n_srcs; i++) {
         sfmt[i] = fmt_id(srcs[i].fourcc);
         one_fmt &= sfmt[i] == sfmt[0];
+        one_size &= srcs[i].width == srcs[0].width && srcs[i].height == srcs[0].height;
     }
-    if (one_fmt && items && n_items > 0 && n_srcs > 0) {
+    static const bool has_avx2 = __builtin_cpu_supports("avx2");
+    if (one_fmt && one_size && items && n_items >= 8 && has_avx2 && kn.host_simd &&
+        clip_rois_avx2(items, n_items, n_srcs, srcs[0].width, srcs[0].height, sfmt[0] == kNV12 || sfmt[0] == kI420,
+                       geo.data(), max_cw[sfmt[0]], max_ch[sfmt[0]], x0_mask[sfmt[0]], uniform[sfmt[0]])) {
+        const int f = sfmt[0];
+        std::fill(fmt.begin(), fmt.end(), f);
+        count[f] = n_items; rep[f] = 0;
+    } else if (one_fmt && items && n_items > 0 && n_srcs > 0) {
         // every source in one format (the common case: one decoder): the group's counters live in registers
         // instead of arrays indexed by the item's format (a store-to-load chain per ROI: C3 pass 1 ~7 -> ~4 us)
         const int f = sfmt[0];
@@ -3995,21 +4008,6 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
             std::vector<int>& ord = h->sc_order;
             roi_largest_first(members.data() + mfirst[f], count[f], geo.data(), DH, sort, bucket.data(), ord);
             HP(6);
-            if (xcd_group) {
-                // Record p runs on XCD p % 8: deal each frame's ROIs (frame s -> XCD s % 8, largest
-                // first within the XCD) so overlapping crops of one frame share one L2.
-                std::vector<int> q[8];
-                for (int i : ord) q[(items ? items[i].src_index : i) & 7].push_back(i);
-                size_t head[8] = {0};
-                for (size_t p = 0; p < ord.size(); p++) {
-                    int x = (int)(p & 7);
-                    if (head[x] == q[x].size())  // this XCD's frames are done: take the largest head left
-                        for (int y = 0, best = -1; y < 8; y++)
-                            if (head[y] < q[y].size() &&
-                                (best < 0 || bucket[q[y][head[y]]] < bucket[q[best][head[best]]])) x = best = y;
-                    ord[p] = q[x][head[x]++];
-                }
-            }
             // Work units (one workgroup each): row tiles of each ROI of about kn.roi_unit row groups (a
             // group is one DMA round trip: the per-workgroup critical path), so the widest crops no
             // longer bound the launch. Units launch largest first; beyond the resident workgroups the
@@ -4093,6 +4091,26 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
             std::vector<int>& order = h->sc_slot;
             order.resize(nu);
             for (int u = 0; u < nu; u++) order[start[maxcost - un[4 * u + 3]]++] = u;
+            if (xcd_group) {
+                // Record p runs on XCD p % 8 (blocks are dealt round-robin): deal the units of frame s to
+                // positions = s (mod 8), largest first within each XCD, so the overlapping crops of one frame
+                // share one L2; a position whose XCD has no units left takes the largest head of another.
+                std::vector<int>* q = h->sc_xq;
+                for (int x = 0; x < 8; x++) q[x].clear();
+                for (int u : order) {
+                    const int i = un[4 * u];
+                    q[(items ? items[i].src_index : i) & 7].push_back(u);
+                }
+                size_t head[8] = {0};
+                for (int p = 0; p < nu; p++) {
+                    int x = p & 7;
+                    if (head[x] == q[x].size())
+                        for (int y = 0, best = -1; y < 8; y++)
+                            if (head[y] < q[y].size() &&
+                                (best < 0 || un[4 * q[y][head[y]] + 3] > un[4 * q[best][head[best]] + 3])) x = best = y;
+                    order[p] = q[x][head[x]++];
+                }
+            }
             for (int pos = 0; pos < nu; pos++) {
                 const int u = order[pos];
                 const int i = un[4 * u];

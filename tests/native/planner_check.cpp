@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "../../edge-video-analytics-microservice_amd/csrc/evam_geom.h"
+#include "../../edge-video-analytics-microservice_amd/csrc/evam_clip_simd.h"
 
 extern "C" {
 typedef struct { int x0, y0, cw, ch, rw, rh, ox, oy; } orc_geom;
@@ -281,7 +282,64 @@ static void check_roi_tail() {
     }
 }
 
+// Pass 1 on AVX2 (csrc/evam_clip_simd.h) against roi_clip item by item: the same (x0, y0, cw, ch) and reductions
+// when it accepts a set, and a refusal (the scalar pass then runs) whenever any item is one it does not cover:
+// full-frame, out-of-range source, empty clip, or a coordinate beyond 2^20.
+static void check_clip_simd() {
+    if (!__builtin_cpu_supports("avx2")) {
+        printf("clip_simd: no AVX2 on this CPU, skipped\n");
+        return;
+    }
+    int accepted = 0, refused = 0;
+    for (int it = 0; it < 4000; it++) {
+        const int f = uni(0, 3);
+        const bool even = f == kNV12 || f == kI420;
+        int W = uni(1, 5000), H = uni(1, 3000);
+        if (even) { W = (W + 1) & ~1; H = (H + 1) & ~1; }
+        const int n = uni(8, 300), n_srcs = uni(1, 40);
+        const int mix = uni(0, 3);  // 0: plain ROIs only; else a few drawn from every class
+        std::vector<evam_roi> r(n);
+        bool cover = true;
+        for (int i = 0; i < n; i++) {
+            int x, y, w, h;
+            if (mix == 0 || uni(0, 40) != 0) { w = uni(1, W); h = uni(1, H); x = uni(-8, W - 1); y = uni(-8, H - 1); }
+            else random_rect(W, H, x, y, w, h);
+            if (uni(0, 2) == 0 && i == 0) { w = W; h = H; x = 0; y = 0; }  // uniform sets too
+            r[i] = {uni(0, 200) == 0 && mix ? n_srcs : uni(0, n_srcs - 1), x, y, w, h};
+            if (it % 7 == 0) r[i] = r[0];
+        }
+        std::vector<Geom> a(n), b(n);
+        int mcw = -1, mch = -1;
+        uint32_t xm = 0;
+        bool un = false;
+        const bool ok = clip_rois_avx2(r.data(), n, n_srcs, W, H, even, a.data(), mcw, mch, xm, un);
+        int emcw = 0, emch = 0;
+        uint32_t exm = 0;
+        bool eun = true;
+        for (int i = 0; i < n; i++) {
+            const evam_roi& q = r[i];
+            const bool in = (unsigned)q.src_index < (unsigned)n_srcs && q.w > 0 && q.h > 0 && q.w <= (1 << 20) &&
+                            q.h <= (1 << 20) && q.x >= -(1 << 20) && q.x <= (1 << 20) && q.y >= -(1 << 20) &&
+                            q.y <= (1 << 20);
+            if (!in || roi_clip(f, W, H, true, q.x, q.y, q.w, q.h, b[i])) { cover = false; continue; }
+            emcw = std::max(emcw, b[i].cw); emch = std::max(emch, b[i].ch); exm |= 1u << (b[i].x0 & 31);
+            eun &= b[i].cw == b[0].cw && b[i].ch == b[0].ch;
+        }
+        CHECK(ok == cover, "clip_simd it %d: accepted %d, scalar coverage %d", it, ok, cover);
+        if (!ok || !cover) { refused++; continue; }
+        accepted++;
+        for (int i = 0; i < n; i++)
+            CHECK(a[i].x0 == b[i].x0 && a[i].y0 == b[i].y0 && a[i].cw == b[i].cw && a[i].ch == b[i].ch,
+                  "clip_simd it %d item %d rect(%d,%d,%d,%d) in %dx%d: (%d %d %d %d) vs (%d %d %d %d)", it, i, r[i].x,
+                  r[i].y, r[i].w, r[i].h, W, H, a[i].x0, a[i].y0, a[i].cw, a[i].ch, b[i].x0, b[i].y0, b[i].cw, b[i].ch);
+        CHECK(mcw == emcw && mch == emch && xm == exm && un == eun, "clip_simd it %d reductions", it);
+    }
+    printf("clip_simd: %d ROI sets equal to roi_clip, %d refused as the scalar pass would handle them\n", accepted,
+           refused);
+}
+
 int main() {
+    check_clip_simd();
     check_roi_tail();
     check_geometry();
     check_linear_tables();
