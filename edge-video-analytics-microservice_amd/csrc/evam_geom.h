@@ -239,6 +239,10 @@ inline void build_tables_into(const Geom& g, int DW, int DH, XTab* x, YTab* y) {
 // rows, stable within a bucket). idx: the group's item indices; bucket: scratch indexed by item index.
 inline void roi_largest_first(const int* idx, int n, const Geom* geo, int DH, bool sort, int* bucket,
                               std::vector<int>& ord) {
+    if (!sort) {  // call order (the default: the units are ordered by row groups afterwards); bucket is not written
+        ord.assign(idx, idx + n);
+        return;
+    }
     int64_t maxw = 1;
     if (sort)
         for (int m = 0; m < n; m++) {

@@ -3857,7 +3857,9 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
     members.resize(n_items);
     int mfirst[5] = {0, 0, 0, 0, 0};
     for (int f = 0; f < 4; f++) mfirst[f + 1] = mfirst[f] + count[f];
-    {
+    if (n_items == count[fmt[0]]) {  // one format: call order
+        for (int i = 0; i < n_items; i++) members[i] = i;
+    } else {
         int fill_at[4] = {mfirst[0], mfirst[1], mfirst[2], mfirst[3]};
         for (int i = 0; i < n_items; i++) members[fill_at[fmt[i]]++] = i;
     }
