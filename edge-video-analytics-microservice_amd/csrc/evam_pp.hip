@@ -220,6 +220,13 @@ __device__ __forceinline__ uint32_t vfinal(uint32_t D0s, uint32_t D1s, uint32_t 
     const uint32_t x = mulhi_u24(b0s, D0s & 0xFFFF00u) + mulhi_u24(b1s, D1s & 0xFFFF00u) + 2u;
     return OUT == 1 ? (x & ~3u) : (x >> 2);
 }
+// Same, for horizontal results already masked with kVMask (a kernel that reuses a source row's results).
+constexpr uint32_t kVMask = 0xFFFF00u;
+template <int OUT>
+__device__ __forceinline__ uint32_t vfinal_masked(uint32_t D0m, uint32_t D1m, uint32_t b0s, uint32_t b1s) {
+    const uint32_t x = mulhi_u24(b0s, D0m) + mulhi_u24(b1s, D1m) + 2u;
+    return OUT == 1 ? (x & ~3u) : (x >> 2);
+}
 
 template <int FMT>
 struct FmtTraits {
@@ -2251,9 +2258,10 @@ __global__ __launch_bounds__(256) void evam_pp_band(const TParams P) {
 #pragma unroll
         for (int j = 0; j < PX; j++) {
             const uint32_t yA = luma_term(yb[lY[j] & 0xFFFF]), yB = luma_term(yb[lY[j] >> 16]);
-            H[j][0] = hpass_sat(yA, tA[j].b, yB, tB[j].b, wp[j]);
-            H[j][1] = hpass_sat(yA, tA[j].g, yB, tB[j].g, wp[j]);
-            H[j][2] = hpass_sat(yA, tA[j].r, yB, tB[j].r, wp[j]);
+            // masked once per source row here rather than per output row in vfinal (each row serves ~2.4 output rows)
+            H[j][0] = hpass_sat(yA, tA[j].b, yB, tB[j].b, wp[j]) & kVMask;
+            H[j][1] = hpass_sat(yA, tA[j].g, yB, tB[j].g, wp[j]) & kVMask;
+            H[j][2] = hpass_sat(yA, tA[j].r, yB, tB[j].r, wp[j]) & kVMask;
         }
     };
     uint32_t HA[PX][3], HB[PX][3];
@@ -2301,7 +2309,7 @@ __global__ __launch_bounds__(256) void evam_pp_band(const TParams P) {
 #pragma unroll
         for (int j = 0; j < PX; j++)
 #pragma unroll
-            for (int c = 0; c < 3; c++) v[c][j] = vfinal<OUT>(HA[j][c], HB[j][c], wb0, wb1);
+            for (int c = 0; c < 3; c++) v[c][j] = vfinal_masked<OUT>(HA[j][c], HB[j][c], wb0, wb1);
         if (anypad) {
 #pragma unroll
             for (int j = 0; j < PX; j++) {
