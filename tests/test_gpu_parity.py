@@ -498,6 +498,39 @@ def test_roi_kernel_xcd_order(evam, O, coracle, gpu, fmt, monkeypatch):
 
 
 @pytest.mark.parametrize("fmt", FORMATS)
+@pytest.mark.parametrize("kind", ["inside", "mixed"])
+@pytest.mark.parametrize("simd", ["1", "0"])
+def test_roi_host_pass1_simd(evam, O, coracle, gpu, fmt, kind, simd, monkeypatch):
+    """The host's ROI pass 1 on AVX2 (csrc/evam_clip_simd.h, EVAM_PP_HOST_SIMD=1, the default) and the scalar pass
+    against the oracle: 61 ROIs (not a multiple of 8) on frames of one size. "inside" sets take the AVX2 pass;
+    "mixed" sets add rects straddling or beyond the frame edges and a full-frame item (w = 0), which the AVX2 pass
+    hands back to the scalar one."""
+    import torch
+
+    monkeypatch.setenv("EVAM_PP_HOST_SIMD", simd)
+    rng = np.random.default_rng(zlib.crc32(f"simd{fmt}{kind}".encode()))
+    W, H = 160, 96
+    frames = [O.random_frame(rng, fc(O, fmt), W, H, pattern="gradient" if i % 2 else "uniform") for i in range(5)]
+    rois = []
+    for k in range(61):
+        w, h = int(rng.integers(2, W)), int(rng.integers(2, H))
+        x, y = int(rng.integers(0, W - w + 1)), int(rng.integers(0, H - h + 1))
+        if kind == "mixed" and k % 5 == 1:
+            x, y = int(rng.integers(-40, W)), int(rng.integers(-30, H))
+            w, h = int(rng.integers(41, 2 * W)), int(rng.integers(31, 2 * H))
+        if kind == "mixed" and k == 37:
+            x = y = w = h = 0  # the full frame
+        rois.append((int(rng.integers(0, len(frames))), x, y, w, h))
+    info = evam.PreProcInfo(resize="aspect-ratio", placement="center", fill=(1, 2, 3),
+                            range=(0.0, 1.0), mean=(0.1, 0.2, 0.3), std=(0.3, 0.2, 0.1))
+    shape = (len(rois), 3, 24, 32)
+    got, _ = run_hip(evam, torch, upload(evam, frames, gpu), shape, torch.float32, info,
+                     rois=[evam.Roi(*r) for r in rois])
+    ref, _ = run_oracle(O, coracle, frames, shape, "f32", info, rois=rois)
+    assert_same(got, ref, f"roi host pass 1 simd={simd} {kind} {fmt}")
+
+
+@pytest.mark.parametrize("fmt", FORMATS)
 @pytest.mark.parametrize("variant", ["wave", "staged", "strip"])
 def test_uniform_rois_varied_x0(evam, O, coracle, gpu, fmt, variant, monkeypatch):
     """Equal-size ROIs (one uniform-geometry group) at crop origins covering every x0 mod 32 residue, upscaled
