@@ -408,10 +408,12 @@ def main():
         out = outs[k % n_out]
         pp = pps[t % len(pps)] if inflight else pps[0]
         if feed is not None:
+            # the copy wait and the consumed mark go on the stream the handle launches on
+            st = inflight_streams[t % len(pps)] if inflight else None
             j = feed.acquire()
             feed.submit(j)
-            pp.convert(feed.batch(j), out, info)
-            feed.release(j)
+            pp.convert(feed.batch(j, stream=st), out, info)
+            feed.release(j, stream=st)
             return
         if ring:
             pp.convert(batches[k], out, info, slot_offset=t % ring, slot_stride=ring)

@@ -40,10 +40,24 @@ _HIP = None
 
 
 def _hip():
-    """The HIP runtime the process already loaded (torch's), for hipMemcpy2DAsync."""
+    """The HIP runtime the process already loaded (torch's, which libevam_pp.so is bound to: ``_native``), for
+    hipMemcpy2DAsync. Opened by its mapped path with RTLD_NOLOAD, so a name lookup can never load a second HIP
+    runtime (``/opt/rocm``'s) whose streams and pointers would not be torch's; more than one mapped runtime, or
+    none, raises."""
     global _HIP
     if _HIP is None:
-        lib = ctypes.CDLL("libamdhip64.so")
+        import os
+
+        import torch  # noqa: F401 — loads the HIP runtime torch was built against
+
+        N.load_library()
+        with open("/proc/self/maps") as f:
+            paths = {ln.split(None, 5)[5].strip() for ln in f
+                     if len(ln.split(None, 5)) == 6 and os.path.basename(ln.split(None, 5)[5].strip())
+                     .startswith("libamdhip64.so")}
+        if len(paths) != 1:
+            raise RuntimeError(f"expected exactly one loaded HIP runtime (libamdhip64.so), found {sorted(paths)}")
+        lib = ctypes.CDLL(paths.pop(), mode=os.RTLD_NOLOAD | os.RTLD_LOCAL)
         lib.hipMemcpy2DAsync.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t,
                                          ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]
         lib.hipMemcpy2DAsync.restype = ctypes.c_int

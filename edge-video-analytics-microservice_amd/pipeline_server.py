@@ -534,9 +534,20 @@ class DeviceRunner:
         except BaseException as e:  # noqa: BLE001
             with self._cv:
                 pipes, self._pipes = list(self._pipes), []
+                draining, self._draining = list(self._draining), []
                 self._stop = True
-            for p in pipes:
-                p._fail(e)
+            for p in pipes + draining:
+                try:
+                    p._fail(e)
+                except Exception:  # noqa: BLE001 — the destination's own error; the pipeline ends either way
+                    pass
+                if p._out_backlog:
+                    # no thread is left to hand the held-back results over: report them, never block wait()
+                    n = len(p._out_backlog)
+                    p.error = f"{p.error or type(e).__name__ + ': ' + str(e)}; {n} result(s) undelivered"
+                    p.state = p.ERROR
+                    p._out_backlog.clear()
+                p._done.set()
 
     def _drain(self):
         """Hand held-back results to destinations that have room again. A pipeline whose last result (the
@@ -726,6 +737,10 @@ class DeviceRunner:
             self._complete(prev)
         for p, e in errors:  # a stream's earlier results (the previous tick) precede its error
             self._finish(p, e)
+        if errors:
+            # out of the runner now, not when this tick completes: a deferred tick may stay pending, and the
+            # loop must not ingest or schedule a stream whose end-of-stream marker is already out
+            self._drop({p for p, _ in errors})
         if deferred:
             self._pending = tick
         else:
@@ -766,8 +781,11 @@ class DeviceRunner:
                     self._finish(p, e)
                     failed.add(p)
         if failed:
-            with self._cv:
-                self._pipes = [p for p in self._pipes if p not in failed]
+            self._drop(failed)
+
+    def _drop(self, pipes):
+        with self._cv:
+            self._pipes = [p for p in self._pipes if p not in pipes]
 
     def _complete_pending(self):
         if self._pending is not None:
@@ -1072,6 +1090,7 @@ class Pipeline:
         self._eos = False
         self._batch = 1
         self._done = threading.Event()
+        self._ended = False  # end of stream (or error) delivered: nothing of this stream may follow its marker
         self._runner = False
         self._out_backlog = collections.deque()  # runner mode: results a full destination queue could not take
         self._out_limit = 1  # held-back results at which the runner stops ingesting / running this stream
@@ -1192,6 +1211,8 @@ class Pipeline:
         self.frames += len(got)
 
     def _emit_all(self, items):
+        if self._ended:  # results of a tick completed after the stream failed: never after its end marker
+            return
         dst = self.destination.get("metadata", self.destination)
         if dst.get("output") is None:
             return
@@ -1204,8 +1225,9 @@ class Pipeline:
         self._end()
 
     def _end(self):
-        if self._done.is_set():
+        if self._ended or self._done.is_set():
             return
+        self._ended = True
         if self.state == self.RUNNING:
             self.state = self.ABORTED if self._stop.is_set() else self.COMPLETED
         for st in self.stages:

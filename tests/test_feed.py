@@ -50,6 +50,8 @@ def test_feed_rejects_oversize_batch(evam, O, gpu):
 @pytest.mark.parametrize("fmt,resize,src,dst", [("NV12", "aspect-ratio", (384, 216), (64, 64)),
                                                 ("I420", "no-aspect-ratio", (200, 120), (40, 20)),
                                                 ("NV12", "crop", (320, 192), (48, 48)),
+                                                ("NV12", "crop", (192, 320), (48, 48)),   # vertical crop, top > 0
+                                                ("I420", "aspect-ratio", (200, 360), (40, 40)),
                                                 ("BGRX", "no-aspect-ratio", (120, 96), (30, 24))])
 def test_feed_touched_rows_only(evam, O, coracle, gpu, fmt, resize, src, dst):
     """set_geometry: only the rows the resize reads cross PCIe (strided 2-D copies); the device slots start

@@ -44,3 +44,17 @@ def test_copy_runs_cover_rows(evam, seed):
         assert got == set(rows)
     if seed % 3 == 0:
         assert cmds == [(1, 2, 5, 40)]
+
+
+@pytest.mark.parametrize("src,dst,mode", [((192, 320), (48, 48), 2), ((1080, 1920), (224, 224), 2),
+                                          ((320, 192), (48, 48), 2), ((200, 360), (40, 40), 1),
+                                          ((3840, 2160), (640, 640), 1), ((64, 48), (16, 16), 0)])
+def test_resized_height_matches_oracle_geometry(evam, O, src, dst, mode):
+    """feed.resized_height (the rows the strided plan copies) against the oracle's own item geometry
+    (rh and the central crop's row offset -oy), portrait sources with a vertical central crop included."""
+    (W, H), (DW, DH) = src, dst
+    g = O.item_geometry(O.NV12, W, H, 0, 0, 0, 0, mode, 0, DW, DH)
+    rh, top = evam.feed.resized_height(W, H, DW, DH, mode)
+    assert rh == g["rh"] and top == (-g["oy"] if mode == 2 else 0)
+    if src == (192, 320):
+        assert top == 16  # 320 * 48/192 = 80 resized rows, the middle 48 visible

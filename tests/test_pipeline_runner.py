@@ -466,3 +466,68 @@ def test_runner_error_follows_earlier_results(stubbed, inflight):
     assert st["state"] == "ERROR" and "second batch" in st.get("message", ""), st
     got = _drain(qout)
     assert len(got) == 2  # the first batch's two frames, then the end-of-stream marker
+
+
+def test_runner_failed_stream_gets_nothing_after_its_marker(stubbed):
+    """stream A fails in tick t (its pre-processing prepare raises) while stream B's detection batch of the
+    same tick is deferred (inflight 2), so tick t stays pending. A must leave the runner at once: no later tick may
+    ingest or run its frames, and nothing may reach A's destination after its end-of-stream marker."""
+    import time
+
+    ps, pre, mdir = stubbed
+    ps.PipelineServer.start({"pipeline_dir": PIPES, "model_dir": mdir, "batch_max": 4, "batch_target": 4,
+                             "batch_wait_ms": 500, "inflight": 2})
+    register(ps, det_every=1)
+    qa, qb, outa, outb = queue.Queue(), queue.Queue(), queue.Queue(), queue.Queue()
+    pa, pb = (ps.PipelineServer.pipeline("detect", "hip") for _ in range(2))
+    for p, qin, qout in ((pa, qa, outa), (pb, qb, outb)):
+        p.start(source={"type": "application", "input": qin},
+                destination={"metadata": {"type": "application", "output": qout, "mode": "json"}},
+                parameters={"detection-properties": {"batch-size": 2}})
+    st = pa.stages[0]
+    orig, calls = st.prepare, [0]
+
+    def prepare(items):
+        calls[0] += 1
+        if calls[0] == 2:
+            raise RuntimeError("prepare failed on A's second tick")
+        return orig(items)
+
+    st.prepare = prepare
+    for qin in (qa, qb):
+        for im in frames(pre, 8):
+            qin.put(im)
+        qin.put(None)
+    assert pb.wait(30)["state"] == "COMPLETED"
+    sa = pa.wait(30)
+    assert sa["state"] == "ERROR" and "second tick" in sa.get("message", ""), sa
+    assert len(_drain(outb)) == 8
+    got = _drain(outa)
+    time.sleep(0.1)
+    assert len(got) == 2 and outa.empty()  # the first tick's frames, the marker, and nothing after it
+    assert calls[0] == 2                   # no tick ran A's frames after it failed
+
+
+def test_runner_death_with_held_back_results(stubbed, monkeypatch):
+    """a runner thread that dies while a pipeline holds results back for a full bounded destination
+    still ends that pipeline: wait() returns, in ERROR, with the undelivered results counted (no thread is left
+    to hand them over)."""
+    import time
+
+    ps, pre, mdir = stubbed
+    ps.PipelineServer.start({"pipeline_dir": PIPES, "model_dir": mdir, "batch_max": 8, "batch_target": 2})
+    register(ps)
+    q = queue.Queue(maxsize=1)
+    p = _start(ps, pre, 12, q)
+    t0 = time.time()
+    while len(p._out_backlog) < 1 and time.time() - t0 < 30:
+        time.sleep(0.01)
+    assert p._out_backlog
+
+    def boom(self):
+        raise RuntimeError("runner bug")
+
+    monkeypatch.setattr(ps.DeviceRunner, "_complete_pending", boom)
+    st = p.wait(30)
+    assert p._done.is_set(), "wait() timed out behind a dead runner"
+    assert st["state"] == "ERROR" and "runner bug" in st["message"] and "undelivered" in st["message"], st

@@ -65,6 +65,13 @@ PY
       for c in $cfgs; do
         PMC_GROUPS="SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVES" bash tools/pmc.sh "${TAG}_valu_$c" "$c"
       done ;;
+    stall)
+      # Stall attribution: WAIT_ANY (parked on s_waitcnt / barrier) + WAIT_INST_ANY (issue stall; WAIT_INST_LDS is
+      # its LDS sub-bucket) + ACTIVE_INST_ANY ~ WAVE_CYCLES; LDS bank conflicts against all LDS-array cycles.
+      for c in $cfgs; do
+        PMC_GROUPS="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU;SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_LDS SQ_INSTS_LDS SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VMEM SQ_INSTS_VMEM_RD" \
+          bash tools/pmc.sh "${TAG}_stall_$c" "$c"
+      done ;;
     ab)
       c="${arg%%:*}"; sets="${arg#*:}"
       bash tools/gpu_env_ab.sh "$TAG" "$c" "$sets" ;;

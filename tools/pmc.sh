@@ -26,3 +26,5 @@ done
 FR=$(python3 -c "import json;print(json.load(open('$OUT/p1.json'))['config']['frames_per_gpu_per_step'])")
 PS=$(python3 -c "import json;print(json.load(open('$OUT/p1.json'))['config']['pool_sets'])")
 python3 "$ROOT/tools/pmc_summary.py" "$OUT" "$CFG" "$FR" "$ROOT/gpurun_out/pmc_traffic.json" "$PS" | tee "$OUT/summary.txt"
+# the raw per-dispatch CSVs run to tens of MB per pass; the summary keeps what is used (gpurun copies back <= 64 MiB)
+rm -rf "$OUT"/p*/
