@@ -796,7 +796,8 @@ __global__ __launch_bounds__(kThreads) void evam_pp_staged(const SParams P) {
     constexpr int SPW = NSEGX > 4 ? NSEGX / 4 : 1;                   // column segments per wave
     constexpr int RSTEP = NSEGX >= 4 ? 1 : 4 / NSEGX;                // waves sharing a column segment
     constexpr int RPW = R / RSTEP;                                   // rows per wave per group
-    constexpr int SLOT_MAX = NSEGX >= 4 ? 2 * kSlot : kSlot;         // largest staged row segment
+    static_assert(NSEGX <= 4 && NBUF == 2, "retired shapes (round 5): full-width tiles, 2 KB slots, 3 buffers");
+    constexpr int SLOT_MAX = kSlot;                                  // largest staged row segment
     const int SLOT = P.slot_bytes;                                   // this launch's segment (<= SLOT_MAX)
     static_assert(R % RSTEP == 0, "R must be a multiple of 4 / NSEGX");
     static_assert(NSEGX <= 4 || R == 1, "full-width (2 KB slot) tiles stage one row per group");
@@ -1595,7 +1596,6 @@ struct TParams {
     int wave_bytes;              // one wave's ring: D entries of strip_slot(PX)-byte segments
     int color_rgb;
     uint32_t fill;
-    int xcd_remap;               // 1: consecutive tiles land on one XCD
     int2 sfoot[kSfoot];          // per strip: crop-relative source columns of the first visible column's
                                  // first tap and the last visible column's last tap; (-1, -1): padding only
                                  // (band kernel: per strip; strip kernel: per tile column x 8 + wave)
@@ -1626,7 +1626,7 @@ static_assert(sizeof(TParams) <= 4000, "strip / band kernel arguments must fit t
 // bytes), the copy floor of those bytes on the same box (profiles/r03c_strip_bw.txt).
 // Letterbox rows are plain fill stores outside the ring; letterbox columns are a per-lane select in the
 // strips that have any. D = ring depth (rows of DMA in flight).
-template <int FMT, int OUT, int D, int PX>
+template <int FMT, int OUT, int D, int PX, int PR>
 __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
     // the LUT at a static LDS address (folds into the reads' immediate offsets); the rings after it
     __shared__ __attribute__((aligned(16))) float lut_s[OUT == 1 ? 768 : 4];
@@ -1637,7 +1637,11 @@ __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
     constexpr int SLOT = strip_slot(FMT, PX);
     constexpr bool PK = FMT == kBGRX;                 // packed BGRx: one plane, 4 bytes a pixel, no conversion
     constexpr int NPC = FMT == kI420 ? 2 : (PK ? 0 : 1);  // chroma planes
-    constexpr int NMIN = 2 + NPC;              // fewest DMA instructions of one row (chroma row shared)
+    // PR (paired taps): both source rows of a plane go out in ONE LDS-DMA instruction, lanes 0-31 the first
+    // row's chunks and lanes 32-63 the second's (I420: U tap0 / U tap1 / V tap0 / V tap1 in lane quarters), so
+    // every row costs exactly NI instructions. Without PR a row costs 2 + NPC (chroma row shared) or 2 + 2 NPC.
+    static_assert(PR == 0 || PR == 1, "paired taps");
+    constexpr int NMIN = PR ? (PK ? 1 : 2) : 2 + NPC;  // fewest DMA instructions of one row (PR: exact)
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (kAblate & 128) return;  // diagnostics: launch cost only
@@ -1698,14 +1702,46 @@ __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
     const __amdgpu_buffer_rsrc_t rsU = __builtin_amdgcn_make_buffer_rsrc((void*)p1, (short)0, 0x7FFFFFFF, 0x00020000);
     const __amdgpu_buffer_rsrc_t rsV = __builtin_amdgcn_make_buffer_rsrc((void*)(NPC == 2 ? p2 : p1), (short)0, 0x7FFFFFFF, 0x00020000);
     uint8_t* const wbuf = smem + wave * P.wave_bytes;
-    // ring entry: [Y tap0][Y tap1][C tap0][C tap1] (+ [V tap0][V tap1] for I420), SLOT bytes each; BGRx:
-    // [row tap0][row tap1]
-    constexpr int SY = SLOT, SC = SLOT, GRP = 2 * SY + 2 * NPC * SC;
-    constexpr int segY = SY, segC = SC;
+    // Ring entry layout. Without PR: [Y tap0][Y tap1][C tap0][C tap1] (+ [V tap0][V tap1] for I420), SLOT bytes
+    // each; BGRx: [row tap0][row tap1]. With PR: [Y tap0 | Y tap1] (512 B halves) then, for 4:2:0,
+    // [C tap0 | C tap1] (NV12, 512 B halves) or [U tap0 | U tap1 | V tap0 | V tap1] (I420, 256 B quarters).
+    //   SY: Y tap1 - Y tap0; CB: chroma region; SC: C tap1 - C tap0; SV: I420 V tap0 - U tap0.
+    constexpr int SY = PR ? 512 : SLOT;
+    constexpr int CB = PR ? 1024 : 2 * SLOT;
+    constexpr int SC = PR ? (NPC == 2 ? 256 : 512) : SLOT;
+    constexpr int SV = PR ? 512 : 2 * SLOT;
+    constexpr int GRP = PR ? (PK ? 1024 : 2048) : 2 * SLOT + 2 * NPC * SLOT;
+    constexpr int segY = SY;
+    // I420 with PR: one buffer resource over both chroma planes, based at the lower one (the host checks that
+    // both lie within 2 GiB of it)
+    const uint8_t* const pcl = NPC == 2 && PR ? (p1 < p2 ? p1 : p2) : p1;
+    const uint32_t dU = (uint32_t)(p1 - pcl), dV = (uint32_t)(p2 - pcl);
+    const __amdgpu_buffer_rsrc_t rsC2 = __builtin_amdgcn_make_buffer_rsrc((void*)pcl, (short)0, 0x7FFFFFFF, 0x00020000);
     auto issue = [&](int i, int k) {
         if (kAblate & 16) return;  // diagnostics: no DMA
         const int ya = y0 + __builtin_amdgcn_readlane(lr0, i), yb = y0 + __builtin_amdgcn_readlane(lr1, i);
         uint8_t* e = wbuf + k * GRP;
+        if constexpr (PR) {
+            const int hi = lane >> 5, c = lane & 31;
+            if (c < nY)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rsY, (__attribute__((address_space(3))) void*)e, 16,
+                                                         (uint32_t)((hi ? yb : ya) * pitch0 + fsY + c * 16), 0,
+                                                         EVAM_PP_LOAD_AUX, 0);
+            if constexpr (NPC == 1) {
+                const int ca = ya >> 1, cb = yb >> 1;
+                if (c < nC && (!hi || ca != cb))
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsU, (__attribute__((address_space(3))) void*)(e + CB), 16,
+                                                             (uint32_t)((hi ? cb : ca) * pitch1 + fsC + c * 16), 0,
+                                                             EVAM_PP_LOAD_AUX, 0);
+            } else if constexpr (NPC == 2) {
+                const int ca = ya >> 1, cb = yb >> 1, q = lane >> 4, c4 = lane & 15, r = (q & 1) ? cb : ca;
+                const uint32_t off = (q & 2) ? dV + (uint32_t)(r * pitch2) : dU + (uint32_t)(r * pitch1);
+                if (c4 < nC && (!(q & 1) || ca != cb))
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsC2, (__attribute__((address_space(3))) void*)(e + CB), 16,
+                                                             off + (uint32_t)(fsC + c4 * 16), 0, EVAM_PP_LOAD_AUX, 0);
+            }
+            return;
+        }
         const uint32_t vo = (uint32_t)lane * 16u;
         if (lane < nY) {
             __builtin_amdgcn_raw_ptr_buffer_load_lds(rsY, (__attribute__((address_space(3))) void*)e, 16, vo,
@@ -1716,17 +1752,17 @@ __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
         if constexpr (NPC == 0) return;
         const int ca = ya >> 1, cb = yb >> 1;
         if (lane < nC) {
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsU, (__attribute__((address_space(3))) void*)(e + 2 * segY), 16, vo,
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsU, (__attribute__((address_space(3))) void*)(e + CB), 16, vo,
                                                      ca * pitch1 + fsC, EVAM_PP_LOAD_AUX, 0);
             if constexpr (NPC == 2)
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(rsV, (__attribute__((address_space(3))) void*)(e + 2 * segY + 2 * segC),
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rsV, (__attribute__((address_space(3))) void*)(e + CB + SV),
                                                          16, vo, ca * pitch2 + fsC, EVAM_PP_LOAD_AUX, 0);
         }
         if (ca != cb && lane < nC) {
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsU, (__attribute__((address_space(3))) void*)(e + 2 * segY + segC), 16,
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsU, (__attribute__((address_space(3))) void*)(e + CB + SC), 16,
                                                      vo, cb * pitch1 + fsC, EVAM_PP_LOAD_AUX, 0);
             if constexpr (NPC == 2)
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(rsV, (__attribute__((address_space(3))) void*)(e + 2 * segY + 3 * segC),
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rsV, (__attribute__((address_space(3))) void*)(e + CB + SV + SC),
                                                          16, vo, cb * pitch2 + fsC, EVAM_PP_LOAD_AUX, 0);
         }
     };
@@ -1827,8 +1863,8 @@ __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
 #pragma unroll
     for (int j = 0; j < PX; j++) {
         aY[j] = wbuf + lY[j];
-        aC0[j] = wbuf + 2 * SY + lC0[j];
-        aC1[j] = wbuf + 2 * SY + lC1[j];
+        aC0[j] = wbuf + CB + lC0[j];
+        aC1[j] = wbuf + CB + lC1[j];
     }
     // BT.601 chroma-term constants: the additive ones in VGPRs so every term is one v_mad (a VOP3 reads one
     // scalar operand: the multiplier)
@@ -1933,7 +1969,7 @@ __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
             uint32_t rY[PX][4], rC[PX][2][2], rE[PX][2][2];
             auto raw_c = [&](const uint8_t* a, int o, uint32_t (&c)[2]) {
                 c[0] = a[o];
-                c[1] = FMT == kNV12 ? a[o + 1] : a[o + 2 * SC];  // NV12: interleaved UV; I420: the V slot
+                c[1] = FMT == kNV12 ? a[o + 1] : a[o + SV];  // NV12: interleaved UV; I420: the V slot
             };
 #pragma unroll
             for (int j = 0; j < PX; j++) {
@@ -2819,8 +2855,7 @@ struct Knobs {
     int staged = 1, wave = 1, rows = 1, roi = 1;   // kernel families allowed (wave 2 = force)
     int th = -1, tw = -1, xcd = -1;                // staged / generic tiles, XCD-contiguous order
     int nsegx = 0;                                 // staged tile width in 64-column segments (0: widest that fits)
-    int wide_slot = 0;                             // 1: 256-column staged tiles may take 2 KB row segments
-    int stage_r = -1, stage_nbuf = -1;             // staged pipeline: rows per group, staging buffers
+    int stage_r = -1;                              // staged pipeline: rows per group
     int wth = -1, px = 0, reuse = 1, wave_lds = 40 * 1024;
     int roi_th = -1, roi_buf = -1, roi_px = 1, roi_xcd = 0;  // roi_buf -1: sized for one round
     int roi_sort = 0;  // 1: largest estimated bytes first before the stable sort by row groups (C3: equal or
@@ -2828,8 +2863,9 @@ struct Knobs {
     int roi_unit = 0;                              // ROI work-unit size in row groups (0: one unit per base tile)
     int roi_nbuf = 2;                              // ROI staging buffers (3: two groups of DMA in flight)
     int roi_tail = 4;                              // row tiles per ROI of the uneven tail over the CUs (1: no split)
-    int strip = 1, strip_th = -1, strip_d = -1, strip_nw = -1, strip_px = 0;  // strip kernel: allowed (2: forced),
-                                                                              // rows per tile, ring depth, waves, px
+    int strip = 1, strip_th = -1, strip_nw = -1, strip_px = 0;  // strip kernel: allowed (2: forced), rows per
+                                                                // tile, waves, px
+    int strip_pair = 1;                            // strip kernel: paired-tap DMA where the footprints allow it
     int strip_waves = 16;                          // strip / band kernels: resident waves per CU the tiles are sized for
     int band = 1, band_px = 0;                     // band kernel: allowed (2: forced), pixels per lane
     int prio = 1;                                  // progress-based wave priority (strip, band, ROI kernels): C2 +3 %,
@@ -2844,13 +2880,13 @@ struct Knobs {
         band = env_int("EVAM_PP_BAND", band); band_px = env_int("EVAM_PP_BAND_PX", band_px);
         strip = env_int("EVAM_PP_STRIP", strip); strip_th = env_int("EVAM_PP_STRIP_TH", strip_th);
         strip_waves = env_int("EVAM_PP_STRIP_WAVES", strip_waves);
-        strip_d = env_int("EVAM_PP_STRIP_D", strip_d); strip_nw = env_int("EVAM_PP_STRIP_NW", strip_nw);
+        strip_pair = env_int("EVAM_PP_STRIP_PAIR", strip_pair); strip_nw = env_int("EVAM_PP_STRIP_NW", strip_nw);
         strip_px = env_int("EVAM_PP_STRIP_PX", strip_px);
         staged = env_int("EVAM_PP_STAGED", staged); wave = env_int("EVAM_PP_WAVE", wave);
         rows = env_int("EVAM_PP_ROWS", rows); roi = env_int("EVAM_PP_ROI", roi);
         th = env_int("EVAM_PP_TH", th); tw = env_int("EVAM_PP_TW", tw); xcd = env_int("EVAM_PP_XCD", xcd);
-        nsegx = env_int("EVAM_PP_NSEGX", nsegx); wide_slot = env_int("EVAM_PP_WIDE_SLOT", wide_slot);
-        stage_r = env_int("EVAM_PP_STAGE_R", stage_r); stage_nbuf = env_int("EVAM_PP_STAGE_NBUF", stage_nbuf);
+        nsegx = env_int("EVAM_PP_NSEGX", nsegx);
+        stage_r = env_int("EVAM_PP_STAGE_R", stage_r);
         wth = env_int("EVAM_PP_WTH", wth); px = env_int("EVAM_PP_PX", px);
         reuse = env_int("EVAM_PP_REUSE", reuse); wave_lds = env_int("EVAM_PP_WAVE_LDS", wave_lds);
         roi_th = env_int("EVAM_PP_ROI_TH", roi_th); roi_buf = env_int("EVAM_PP_ROI_BUF", roi_buf);
@@ -2917,7 +2953,9 @@ RowCfg choose_row_tiles(int DW, int DH, const Knobs& k) {
 // Staged-kernel pipeline shapes: (output rows per group R, staging buffers NBUF). One variant per
 // (format, dtype, column segments) is instantiated for each shape listed here.
 struct StagedShape { int R, nbuf; };
-constexpr StagedShape kStagedShapes[] = {{2, 2}, {1, 2}, {2, 3}};
+// (Three staging buffers, 512-column tiles and 2 KB row slots measured neutral or slower for two rounds and were
+// retired in round 5.)
+constexpr StagedShape kStagedShapes[] = {{2, 2}, {1, 2}};
 
 // Valid (column segments, rows per group): four waves split NSEGX x R evenly.
 constexpr bool staged_valid(int nsegx, int R) { return nsegx > 4 ? R == 1 : (nsegx == 4 ? true : R % (4 / nsegx) == 0); }
@@ -2939,7 +2977,7 @@ hipError_t launch_staged_t(const SParams& p, int grid, int lds, hipStream_t s) {
 
 template <int FMT, int OUT, int NSEGX>
 hipError_t launch_staged_s(int R, int nbuf, const SParams& p, int grid, int lds, hipStream_t s) {
-    if (R == 2 && nbuf == 3) return launch_staged_t<FMT, OUT, NSEGX, 2, 3>(p, grid, lds, s);
+    (void)nbuf;
     if (R == 2) return launch_staged_t<FMT, OUT, NSEGX, 2, 2>(p, grid, lds, s);
     if (R == 1) return launch_staged_t<FMT, OUT, NSEGX, 1, 2>(p, grid, lds, s);
     return hipErrorInvalidValue;
@@ -2948,7 +2986,6 @@ hipError_t launch_staged_s(int R, int nbuf, const SParams& p, int grid, int lds,
 template <int FMT, int OUT>
 hipError_t launch_staged_n(int nsegx, int R, int nbuf, const SParams& p, int grid, int lds, hipStream_t s) {
     switch (nsegx) {
-    case 8: return launch_staged_s<FMT, OUT, 8>(R, nbuf, p, grid, lds, s);
     case 4: return launch_staged_s<FMT, OUT, 4>(R, nbuf, p, grid, lds, s);
     case 2: return launch_staged_s<FMT, OUT, 2>(R, nbuf, p, grid, lds, s);
     default: return launch_staged_s<FMT, OUT, 1>(R, nbuf, p, grid, lds, s);
@@ -3170,26 +3207,27 @@ bool plan_wave(int f, const Geom& g, int DW, int DH, int count, int out_dtype, i
     return true;
 }
 
+// Ring depth: D = 2 (D 1 / 3 / 4 measured slower on C2 and C5, rounds 2-3: profiles/r03f_bench_lines.txt, C2 D 3
+// +2.7 us; the other depths were retired in round 5).
+constexpr int kStripD = 2;
 template <int FMT, int OUT, int PX>
-const void* strip_fn_p(int d) {
-    return d == 4 ? (const void*)evam_pp_strip<FMT, OUT, 4, PX>
-         : d == 3 ? (const void*)evam_pp_strip<FMT, OUT, 3, PX>
-         : d == 2 ? (const void*)evam_pp_strip<FMT, OUT, 2, PX> : (const void*)evam_pp_strip<FMT, OUT, 1, PX>;
+const void* strip_fn_p(int pr) {
+    return pr ? (const void*)evam_pp_strip<FMT, OUT, kStripD, PX, 1> : (const void*)evam_pp_strip<FMT, OUT, kStripD, PX, 0>;
 }
-const void* strip_fn(int f, int out, int d, int px) {
+const void* strip_fn(int f, int out, int pr, int px) {
     switch ((f * 2 + out) * 2 + (px == 2)) {
-    case (kNV12 * 2 + 0) * 2: return strip_fn_p<kNV12, 0, 1>(d);
-    case (kNV12 * 2 + 0) * 2 + 1: return strip_fn_p<kNV12, 0, 2>(d);
-    case (kNV12 * 2 + 1) * 2: return strip_fn_p<kNV12, 1, 1>(d);
-    case (kNV12 * 2 + 1) * 2 + 1: return strip_fn_p<kNV12, 1, 2>(d);
-    case (kI420 * 2 + 0) * 2: return strip_fn_p<kI420, 0, 1>(d);
-    case (kI420 * 2 + 0) * 2 + 1: return strip_fn_p<kI420, 0, 2>(d);
-    case (kI420 * 2 + 1) * 2: return strip_fn_p<kI420, 1, 1>(d);
-    case (kI420 * 2 + 1) * 2 + 1: return strip_fn_p<kI420, 1, 2>(d);
-    case (kBGRX * 2 + 0) * 2: return strip_fn_p<kBGRX, 0, 1>(d);
-    case (kBGRX * 2 + 0) * 2 + 1: return strip_fn_p<kBGRX, 0, 2>(d);
-    case (kBGRX * 2 + 1) * 2: return strip_fn_p<kBGRX, 1, 1>(d);
-    default: return strip_fn_p<kBGRX, 1, 2>(d);
+    case (kNV12 * 2 + 0) * 2: return strip_fn_p<kNV12, 0, 1>(pr);
+    case (kNV12 * 2 + 0) * 2 + 1: return strip_fn_p<kNV12, 0, 2>(pr);
+    case (kNV12 * 2 + 1) * 2: return strip_fn_p<kNV12, 1, 1>(pr);
+    case (kNV12 * 2 + 1) * 2 + 1: return strip_fn_p<kNV12, 1, 2>(pr);
+    case (kI420 * 2 + 0) * 2: return strip_fn_p<kI420, 0, 1>(pr);
+    case (kI420 * 2 + 0) * 2 + 1: return strip_fn_p<kI420, 0, 2>(pr);
+    case (kI420 * 2 + 1) * 2: return strip_fn_p<kI420, 1, 1>(pr);
+    case (kI420 * 2 + 1) * 2 + 1: return strip_fn_p<kI420, 1, 2>(pr);
+    case (kBGRX * 2 + 0) * 2: return strip_fn_p<kBGRX, 0, 1>(pr);
+    case (kBGRX * 2 + 0) * 2 + 1: return strip_fn_p<kBGRX, 0, 2>(pr);
+    case (kBGRX * 2 + 1) * 2: return strip_fn_p<kBGRX, 1, 1>(pr);
+    default: return strip_fn_p<kBGRX, 1, 2>(pr);
     }
 }
 
@@ -3203,12 +3241,16 @@ const void* strip_fn(int f, int out, int d, int px) {
 //  * Tile height: about EVAM_PP_STRIP_WAVES (16) waves per CU over the whole launch (the data-movement
 //    microbenchmark's best: fewer, longer-lived waves beat a full 32), at most 64 rows (the lane-held row
 //    table).
-//  * Ring depth D: 2 (D 3 / 4 measured slower on C2, D 1 slower on C2 and C5).
+//  * Ring depth: kStripD = 2.
+//  * Paired taps (pr): both source rows of a plane in one LDS-DMA instruction when every strip's footprint is at
+//    most 32 chunks (512 B) per row (I420 chroma: 16, four segments per instruction): 2 instructions per row
+//    instead of 4 (NV12) or 6 (I420), 1 instead of 2 (BGRx). EVAM_PP_STRIP_PAIR=0 keeps one row per instruction.
 // Returns false when the geometry does not suit it: outputs wider than kMaxStrips strips, footprints over
 // 1 KB per strip, or consecutive output rows that share source rows (vertical upscales: the wave kernel's
 // REUSE path).
 bool plan_strip(int f, const Geom& g, int DW, int DH, int count, int out_dtype, int n_cu, const XTab* xt,
-                const YTab* yt, uint32_t x0_mask, const Knobs& kn, TParams& p, int& D, int& px, int& lds, int& grid) {
+                const YTab* yt, uint32_t x0_mask, const Knobs& kn, bool pair_ok, TParams& p, int& pr, int& px, int& lds,
+                int& grid) {
     if (f != kNV12 && f != kI420 && f != kBGRX) return false;
     int shared = 0, vis = 0;
     for (int Y = 0; Y + 1 < DH; Y++) {
@@ -3235,7 +3277,9 @@ bool plan_strip(int f, const Geom& g, int DW, int DH, int count, int out_dtype, 
     if (!px) return false;
     const int nstrips = (DW + 64 * px - 1) / (64 * px);
     if (nstrips > kMaxStrips) return false;
-    const int grp_bytes = (2 + 2 * npc) * strip_slot(f, px);  // one ring entry: 2 luma + 2 x npc chroma segments
+    pr = kn.strip_pair && pair_ok && mY <= 32 && (npc == 0 || (npc == 1 && mC <= 32) || (npc == 2 && mC <= 16)) ? 1 : 0;
+    // one ring entry: 2 luma + 2 x npc chroma segments (paired: 1 KB per plane group)
+    const int grp_bytes = pr ? (npc ? 2048 : 1024) : (2 + 2 * npc) * strip_slot(f, px);
     int nw = 4, best = 1 << 30;
     for (int c = 4; c <= 8; c++) {
         const int idle = (nstrips + c - 1) / c * c - nstrips;
@@ -3247,16 +3291,14 @@ bool plan_strip(int f, const Geom& g, int DW, int DH, int count, int out_dtype, 
     p.tiles_x = (nstrips + nw - 1) / nw;
     const int lut_static = out_dtype == EVAM_DTYPE_F32 ? kLutBytes : 16;  // the kernel's static LDS
     const int wg_target = std::max(1, std::min(32, kn.strip_waves) / nw);
-    D = 2;  // deeper rings measured slower (profiles/r03f_bench_lines.txt: C2 D 3 +2.7 us)
-    if (kn.strip_d >= 1 && kn.strip_d <= 4) D = kn.strip_d;
-    p.wave_bytes = D * grp_bytes;
+    p.wave_bytes = kStripD * grp_bytes;
     lds = nw * p.wave_bytes + 16;  // dynamic LDS; + 16: a right-edge tap reads past its footprint (weight 0)
     if (lds + lut_static > 64 * 1024) return false;
-    const int res = std::max(1, std::min(wg_target, resident_per_cu(strip_fn(f, out_dtype, D, px), lds)));
+    const int res = std::max(1, std::min(wg_target, resident_per_cu(strip_fn(f, out_dtype, pr, px), lds)));
     const int64_t slots = (int64_t)n_cu * res;
     const int64_t work = (int64_t)std::min(count, kArgItems) * p.tiles_x * DH;
     int th = (int)std::max<int64_t>(1, (work + slots - 1) / slots);
-    th = std::max(th, std::min(DH, D));
+    th = std::max(th, std::min(DH, kStripD));
     if (kn.strip_th > 0) th = kn.strip_th;
     p.TH = std::max(1, std::min(std::min(DH, 64), th));
     p.tiles_per_item = p.tiles_x * ((DH + p.TH - 1) / p.TH);
@@ -3278,29 +3320,27 @@ bool plan_strip(int f, const Geom& g, int DW, int DH, int count, int out_dtype, 
 }
 
 template <int FMT, int OUT, int PX>
-hipError_t launch_strip_t(int d, const TParams& p, dim3 grid, int lds, hipStream_t s) {
+hipError_t launch_strip_t(int pr, const TParams& p, dim3 grid, int lds, hipStream_t s) {
     const dim3 blk(64 * p.nw);
-    if (d == 4) hipLaunchKernelGGL((evam_pp_strip<FMT, OUT, 4, PX>), grid, blk, lds, s, p);
-    else if (d == 3) hipLaunchKernelGGL((evam_pp_strip<FMT, OUT, 3, PX>), grid, blk, lds, s, p);
-    else if (d == 2) hipLaunchKernelGGL((evam_pp_strip<FMT, OUT, 2, PX>), grid, blk, lds, s, p);
-    else hipLaunchKernelGGL((evam_pp_strip<FMT, OUT, 1, PX>), grid, blk, lds, s, p);
+    if (pr) hipLaunchKernelGGL((evam_pp_strip<FMT, OUT, kStripD, PX, 1>), grid, blk, lds, s, p);
+    else hipLaunchKernelGGL((evam_pp_strip<FMT, OUT, kStripD, PX, 0>), grid, blk, lds, s, p);
     return hipGetLastError();
 }
 
-hipError_t launch_strip(int f, int out, int d, int px, const TParams& p, dim3 grid, int lds, hipStream_t s) {
+hipError_t launch_strip(int f, int out, int pr, int px, const TParams& p, dim3 grid, int lds, hipStream_t s) {
     switch ((f * 2 + out) * 2 + (px == 2)) {
-    case (kNV12 * 2 + 0) * 2: return launch_strip_t<kNV12, 0, 1>(d, p, grid, lds, s);
-    case (kNV12 * 2 + 0) * 2 + 1: return launch_strip_t<kNV12, 0, 2>(d, p, grid, lds, s);
-    case (kNV12 * 2 + 1) * 2: return launch_strip_t<kNV12, 1, 1>(d, p, grid, lds, s);
-    case (kNV12 * 2 + 1) * 2 + 1: return launch_strip_t<kNV12, 1, 2>(d, p, grid, lds, s);
-    case (kI420 * 2 + 0) * 2: return launch_strip_t<kI420, 0, 1>(d, p, grid, lds, s);
-    case (kI420 * 2 + 0) * 2 + 1: return launch_strip_t<kI420, 0, 2>(d, p, grid, lds, s);
-    case (kI420 * 2 + 1) * 2: return launch_strip_t<kI420, 1, 1>(d, p, grid, lds, s);
-    case (kI420 * 2 + 1) * 2 + 1: return launch_strip_t<kI420, 1, 2>(d, p, grid, lds, s);
-    case (kBGRX * 2 + 0) * 2: return launch_strip_t<kBGRX, 0, 1>(d, p, grid, lds, s);
-    case (kBGRX * 2 + 0) * 2 + 1: return launch_strip_t<kBGRX, 0, 2>(d, p, grid, lds, s);
-    case (kBGRX * 2 + 1) * 2: return launch_strip_t<kBGRX, 1, 1>(d, p, grid, lds, s);
-    default: return launch_strip_t<kBGRX, 1, 2>(d, p, grid, lds, s);
+    case (kNV12 * 2 + 0) * 2: return launch_strip_t<kNV12, 0, 1>(pr, p, grid, lds, s);
+    case (kNV12 * 2 + 0) * 2 + 1: return launch_strip_t<kNV12, 0, 2>(pr, p, grid, lds, s);
+    case (kNV12 * 2 + 1) * 2: return launch_strip_t<kNV12, 1, 1>(pr, p, grid, lds, s);
+    case (kNV12 * 2 + 1) * 2 + 1: return launch_strip_t<kNV12, 1, 2>(pr, p, grid, lds, s);
+    case (kI420 * 2 + 0) * 2: return launch_strip_t<kI420, 0, 1>(pr, p, grid, lds, s);
+    case (kI420 * 2 + 0) * 2 + 1: return launch_strip_t<kI420, 0, 2>(pr, p, grid, lds, s);
+    case (kI420 * 2 + 1) * 2: return launch_strip_t<kI420, 1, 1>(pr, p, grid, lds, s);
+    case (kI420 * 2 + 1) * 2 + 1: return launch_strip_t<kI420, 1, 2>(pr, p, grid, lds, s);
+    case (kBGRX * 2 + 0) * 2: return launch_strip_t<kBGRX, 0, 1>(pr, p, grid, lds, s);
+    case (kBGRX * 2 + 0) * 2 + 1: return launch_strip_t<kBGRX, 0, 2>(pr, p, grid, lds, s);
+    case (kBGRX * 2 + 1) * 2: return launch_strip_t<kBGRX, 1, 1>(pr, p, grid, lds, s);
+    default: return launch_strip_t<kBGRX, 1, 2>(pr, p, grid, lds, s);
     }
 }
 
@@ -3393,7 +3433,6 @@ bool plan_band(int f, const Geom& g, int DW, int DH, int count, int out_dtype, i
     p.scale_y = 1. / ((double)g.rh / g.ch);
     p.nw = nw;
     p.tiles_x = (nstrips + nw - 1) / nw;  // strip groups
-    p.xcd_remap = 0;
     if ((p.tiles_x - 1) * 8 + nw > kSfoot) return false;
     const int sw = 64 * px;
     for (int k = 0; k < kSfoot; k++) {  // entry strip group x 8 + wave
@@ -4194,10 +4233,20 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
             const int per_launch = std::min(count[f], kArgItems);
             if (kn.strip && kn.wave != 2) {
                 TParams* tp = &h->sc_tparams;
-                int D = 0, spx = 0, lds = 0, grid = 0;
+                int pr = 0, spx = 0, lds = 0, grid = 0;
                 const XTab* hx = reinterpret_cast<const XTab*>(h->h_block.data() + tab_off[f]);
+                // I420 paired chroma addresses both chroma planes from one buffer resource based at the lower one:
+                // every item's U and V planes must lie within 1 GiB of each other (else no pairing for the group)
+                bool pair_ok = true;
+                if (f == kI420 && kn.strip_pair)
+                    for (int m = mfirst[f]; m < mfirst[f + 1] && pair_ok; m++) {
+                        const int i = members[m];
+                        const evam_image& sr = srcs[items ? items[i].src_index : i];
+                        const int64_t d = (int64_t)((intptr_t)sr.planes[2] - (intptr_t)sr.planes[1]);
+                        pair_ok = d > -(int64_t(1) << 30) && d < (int64_t(1) << 30);
+                    }
                 if (plan_strip(f, g0, DW, DH, count[f], cfg->out_dtype, h->n_cu, hx, reinterpret_cast<const YTab*>(hx + DW),
-                               x0_mask[f], kn, *tp, D, spx, lds, grid)) {
+                               x0_mask[f], kn, pair_ok, *tp, pr, spx, lds, grid)) {
                     tp->lut = lut_d;
                     tp->dst = dst->data;
                     tp->slot_offset = dst->slot_offset;
@@ -4211,9 +4260,8 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
                         // grid (tile column, tile row, item), dispatched in that order (the C2 data movement in
                         // the strip pattern takes 1.7 us longer with each XCD on its own run of tiles,
                         // profiles/r03c_strip_bw.txt)
-                        tp->xcd_remap = 0;
                         const dim3 gr((unsigned)tp->tiles_x, (unsigned)((DH + tp->TH - 1) / tp->TH), (unsigned)nm);
-                        hipError_t e = launch_strip(f, cfg->out_dtype, D, spx, *tp, gr, lds, h->stream);
+                        hipError_t e = launch_strip(f, cfg->out_dtype, pr, spx, *tp, gr, lds, h->stream);
                         if (e != hipSuccess) return fail(EVAM_PP_ERR_HIP, "kernel launch failed: %s", hipGetErrorString(e));
                         launches++; kmask |= EVAM_KERNEL_STRIP;
                     }
@@ -4277,9 +4325,8 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
                     continue;
                 }
             }
-            // Tile width: the widest of 256 / 128 / 64 columns whose staged row segment (the exact widest
-            // footprint of any tile and crop origin of this group) fits the kernel's slot: 2 KB at 256
-            // columns (two DMA instructions per segment above 1 KB), 1 KB below.
+            // Tile width: the widest of 256 / 128 columns whose staged row segment (the exact widest footprint of
+            // any tile and crop origin of this group) fits the kernel's 1 KB slot.
             const XTab* hx = reinterpret_cast<const XTab*>(h->h_block.data() + tab_off[f]);
             auto seg_bytes = [&](int tw) {
                 int mY = 0, mC = 0;
@@ -4289,17 +4336,13 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
             int nsegx = 0;
             if (kn.staged)
                 for (int n : {4, 2}) {  // (64 columns would need R % 4 == 0: the row kernel serves those)
-                    if (seg_bytes(64 * n) <= (n == 4 && kn.wide_slot ? 2 * kSlot : kSlot)) { nsegx = n; break; }
+                    if (seg_bytes(64 * n) <= kSlot) { nsegx = n; break; }
                 }
             if (nsegx && kn.nsegx > 0 && kn.nsegx < nsegx && 2 % (4 / kn.nsegx) == 0) nsegx = kn.nsegx;
-            // Full-width tiles (512 columns, 2 KB row slots, one row per group): whole source rows per DMA
-            // and whole output rows per store sweep (EVAM_PP_NSEGX=8).
-            if (nsegx == 4 && kn.nsegx == 8 && DW > 256 && seg_bytes(512) <= 2 * kSlot) nsegx = 8;
             if (nsegx) {
                 // Pipeline shape: R output rows per group, NBUF staging buffers (NBUF - 1 groups of DMA in
                 // flight).
-                int R = kn.stage_r > 0 ? kn.stage_r : 2, nbuf = kn.stage_nbuf > 0 ? kn.stage_nbuf : 2;
-                if (nsegx == 8) R = 1;
+                int R = kn.stage_r > 0 ? kn.stage_r : 2, nbuf = 2;
                 bool shape_ok = false;
                 for (const StagedShape& ss : kStagedShapes) shape_ok |= ss.R == R && ss.nbuf == nbuf;
                 if (!shape_ok || !staged_valid(nsegx, R)) { R = 2; nbuf = 2; }

@@ -78,19 +78,16 @@ def test_c1_small_batches(evam, O, coracle, gpu, frames, family):
 
 
 # kernel shapes forced on the full-size workloads: the default choice (the strip kernel for C2 / C4 / C5),
-# the strip kernel's other ring depths and tile heights, and the staged kernel's pipeline shapes
+# the strip kernel with one row per DMA instruction (unpaired taps) and other tile heights, and the staged kernel's
+# pipeline shapes
 STAGED_SHAPES = {"default": {},
-                 "strip_d1": {"EVAM_PP_STRIP_D": "1"},
-                 "strip_d2": {"EVAM_PP_STRIP_D": "2"},
-                 "strip_d3": {"EVAM_PP_STRIP_D": "3"},
+                 "strip_unpaired": {"EVAM_PP_STRIP_PAIR": "0"},
                  "strip_th32": {"EVAM_PP_STRIP_TH": "32"},
                  "strip_px1": {"EVAM_PP_STRIP_PX": "1"},
-                 "strip_xcd": {"EVAM_PP_XCD": "1"},
+                 "strip_px1_unpaired": {"EVAM_PP_STRIP_PX": "1", "EVAM_PP_STRIP_PAIR": "0"},
                  "staged": {"EVAM_PP_STRIP": "0"},
                  "r2": {"EVAM_PP_STRIP": "0", "EVAM_PP_STAGE_R": "2", "EVAM_PP_NSEGX": "4"},
-                 "r1": {"EVAM_PP_STRIP": "0", "EVAM_PP_STAGE_R": "1", "EVAM_PP_NSEGX": "4"},
-                 "wide": {"EVAM_PP_STRIP": "0", "EVAM_PP_NSEGX": "8"},
-                 "b3": {"EVAM_PP_STRIP": "0", "EVAM_PP_STAGE_NBUF": "3"}}
+                 "r1": {"EVAM_PP_STRIP": "0", "EVAM_PP_STAGE_R": "1", "EVAM_PP_NSEGX": "4"}}
 
 
 @pytest.mark.parametrize("shape", sorted(STAGED_SHAPES))
@@ -148,7 +145,7 @@ def test_c3_bench_roi_set(evam, O, coracle, gpu, seed, kernel, monkeypatch):
 
 
 @pytest.mark.parametrize("placement", ["top_left", "center"])
-@pytest.mark.parametrize("shape", ["default", "strip_d2", "strip_th32", "strip_px1", "staged", "r2", "wide", "b3"])
+@pytest.mark.parametrize("shape", ["default", "strip_unpaired", "strip_th32", "strip_px1", "staged", "r2"])
 def test_c4_random_4k_letterbox(evam, O, coracle, gpu, placement, shape, monkeypatch):
     """C4: random (not constant) 3840x2160 NV12 bench frames letterboxed to 640x640 fp32: every 6x gather
     (column taps 6dx+2, weights 1024/1024) on the real 4K pitch is checked, in both placements."""
@@ -170,7 +167,7 @@ def test_c4_random_4k_letterbox(evam, O, coracle, gpu, placement, shape, monkeyp
     pp.close()
 
 
-@pytest.mark.parametrize("shape", ["default", "strip_d2", "strip_px1", "staged", "b3"])
+@pytest.mark.parametrize("shape", ["default", "strip_unpaired", "strip_px1", "staged"])
 def test_c5_ring_step(evam, O, coracle, gpu, shape, monkeypatch):
     """C5: a 32-stream clip-ring step (1080p NV12 -> aspect(max) 398x224 -> central crop 224x224 fp32 into
     slot t % 16 of a [32, 16, 3, 224, 224] ring), two steps with different frames and slots."""
@@ -197,15 +194,15 @@ def test_c5_ring_step(evam, O, coracle, gpu, shape, monkeypatch):
     pp.close()
 
 
-@pytest.mark.parametrize("variant", ["strip", "strip_d1", "wave"])
+@pytest.mark.parametrize("variant", ["strip", "strip_unpaired", "wave"])
 def test_c5_bgrx_ring_step(evam, O, coracle, gpu, variant, monkeypatch):
     """C5 with BGRx sources (bench.py c5_bgrx: 32 x 768x432 BGRx -> aspect(max) -> central crop 224x224 fp32 into
     ring slot t % 16): the strip kernel's packed-format path (the default), and the wave kernel it replaced."""
     import torch
 
     monkeypatch.setenv("EVAM_PP_STRIP", "0" if variant == "wave" else "1")
-    if variant == "strip_d1":
-        monkeypatch.setenv("EVAM_PP_STRIP_D", "1")
+    if variant == "strip_unpaired":
+        monkeypatch.setenv("EVAM_PP_STRIP_PAIR", "0")
     N = evam.native
     wl = bench.WORKLOADS["c5_bgrx"]
     info = bench.make_info(evam, wl)

@@ -362,10 +362,9 @@ def test_stats_and_timing(evam, O, gpu):
     ((480, 270), (224, 224), "aspect-crop"),        # C5 shape: central crop
 ])
 @pytest.mark.parametrize("variant", ["auto", "wave", "px1", "px2", "noreuse", "staged", "staged_xcd", "staged_r1",
-                                     "staged_wide", "staged_b3", "staged_slot2k", "strip", "strip_d1", "strip_d2", "strip_d3",
-                                     "strip_th5", "strip_nw8", "strip_xcd", "strip_px1", "strip_px2",
-                                     "strip_px2_d4_th7", "strip_noprio", "band", "band_px1", "band_px2", "band_th5",
-                                     "band_th64", "band_ahead64", "band_noprio"])
+                                     "strip", "strip_unpaired", "strip_th5", "strip_nw8", "strip_px1", "strip_px2",
+                                     "strip_px1_unpaired", "strip_px2_unpaired_th7", "strip_noprio", "band", "band_px1",
+                                     "band_px2", "band_th5", "band_th64", "band_ahead64", "band_noprio"])
 def test_wave_kernel_variants(evam, O, coracle, gpu, fmt, src, dst, resize, variant, monkeypatch):
     """Uniform-geometry batches through the default kernel choice, the wave-row kernel forced
     (EVAM_PP_WAVE=2; every PX / REUSE choice), the staged kernel (EVAM_PP_WAVE=0 EVAM_PP_STRIP=0; with the
@@ -379,19 +378,14 @@ def test_wave_kernel_variants(evam, O, coracle, gpu, fmt, src, dst, resize, vari
            "px2": {"EVAM_PP_WAVE": "2", "EVAM_PP_PX": "2"}, "noreuse": {"EVAM_PP_WAVE": "2", "EVAM_PP_REUSE": "0"},
            "staged": {"EVAM_PP_WAVE": "0"}, "staged_xcd": {"EVAM_PP_WAVE": "0", "EVAM_PP_XCD": "1"},
            "staged_r1": {"EVAM_PP_WAVE": "0", "EVAM_PP_STAGE_R": "1"},
-           "staged_wide": {"EVAM_PP_WAVE": "0", "EVAM_PP_NSEGX": "8"},
-           "staged_b3": {"EVAM_PP_WAVE": "0", "EVAM_PP_STAGE_NBUF": "3"},
-           "staged_slot2k": {"EVAM_PP_WAVE": "0", "EVAM_PP_WIDE_SLOT": "1"},
-           "strip": {"EVAM_PP_STRIP": "2"}, "strip_d2": {"EVAM_PP_STRIP": "2", "EVAM_PP_STRIP_D": "2"},
-           "strip_d1": {"EVAM_PP_STRIP": "2", "EVAM_PP_STRIP_D": "1"},
-           "strip_d3": {"EVAM_PP_STRIP": "2", "EVAM_PP_STRIP_D": "3"},
+           "strip": {"EVAM_PP_STRIP": "2"}, "strip_unpaired": {"EVAM_PP_STRIP": "2", "EVAM_PP_STRIP_PAIR": "0"},
            "strip_th5": {"EVAM_PP_STRIP": "2", "EVAM_PP_STRIP_TH": "5"},
            "strip_nw8": {"EVAM_PP_STRIP": "2", "EVAM_PP_STRIP_NW": "8"},
-           "strip_xcd": {"EVAM_PP_STRIP": "2", "EVAM_PP_XCD": "1", "EVAM_PP_STRIP_TH": "3"},
            "strip_px1": {"EVAM_PP_STRIP": "2", "EVAM_PP_STRIP_PX": "1"},
            "strip_px2": {"EVAM_PP_STRIP": "2", "EVAM_PP_STRIP_PX": "2"},
-           "strip_px2_d4_th7": {"EVAM_PP_STRIP": "2", "EVAM_PP_STRIP_PX": "2", "EVAM_PP_STRIP_D": "4",
-                                "EVAM_PP_STRIP_TH": "7"},
+           "strip_px1_unpaired": {"EVAM_PP_STRIP": "2", "EVAM_PP_STRIP_PX": "1", "EVAM_PP_STRIP_PAIR": "0"},
+           "strip_px2_unpaired_th7": {"EVAM_PP_STRIP": "2", "EVAM_PP_STRIP_PX": "2", "EVAM_PP_STRIP_PAIR": "0",
+                                      "EVAM_PP_STRIP_TH": "7"},
            "band": {"EVAM_PP_BAND": "2"}, "band_px1": {"EVAM_PP_BAND": "2", "EVAM_PP_BAND_PX": "1"},
            "band_px2": {"EVAM_PP_BAND": "2", "EVAM_PP_BAND_PX": "2"},
            "band_th5": {"EVAM_PP_BAND": "2", "EVAM_PP_STRIP_TH": "5"},
@@ -690,3 +684,44 @@ def test_roi_kernel_three_buffers(evam, O, coracle, gpu, fmt, buf, monkeypatch):
         assert_same(got, ref, f"roi 3 buffers {fmt} buf={buf} dst={dst}")
 
 
+
+
+@pytest.mark.parametrize("layout", ["v_first", "u_first", "far_apart"])
+def test_i420_paired_chroma_plane_layouts(evam, O, coracle, gpu, layout):
+    """Strip kernel with paired taps on I420: both chroma planes are read through one buffer resource based at the
+    lower plane (U and V segments of both source rows in one LDS-DMA instruction). V below U, U below V, and planes
+    more than 1 GiB apart (no pairing for that group: one row per instruction) all equal the oracle."""
+    import torch
+
+    rng = np.random.default_rng(2024)
+    W, H = 960, 540
+    frames = [O.random_frame(rng, O.I420, W, H, pattern=p) for p in ("uniform", "gradient")]
+    imgs = []
+    for f in frames:
+        y, u, v = (np.ascontiguousarray(p) for p in f.planes)
+        gap = (1 << 30) + 4096 if layout == "far_apart" else 4096
+        total = y.nbytes + u.nbytes + v.nbytes + gap + 3 * 256
+        buf = torch.zeros(total, dtype=torch.uint8, device=gpu)
+
+        def put(off, a):
+            t = buf[off:off + a.nbytes].view(a.shape)
+            t.copy_(torch.from_numpy(a))
+            return t, (off + a.nbytes + 255) // 256 * 256
+
+        o = 0
+        if layout == "v_first":
+            vt, o = put(o, v)
+            ut, o = put(o, u)
+        else:
+            ut, o = put(o, u)
+            o = (o + gap) // 256 * 256 if layout == "far_apart" else o
+            vt, o = put(o, v)
+        yt, o = put(o, y)
+        imgs.append(evam.Image(O.I420, W, H, [yt, ut, vt]))
+    info = evam.PreProcInfo(range=(0.0, 1.0), mean=(0.406, 0.456, 0.485), std=(0.225, 0.224, 0.229))
+    pp = evam.HipPreProcessor(device=0)
+    got, _ = run_hip(evam, torch, imgs, (2, 3, 256, 256), torch.float32, info, pp=pp)
+    assert pp.stats().kernels == evam.native.KERNEL_STRIP
+    pp.close()
+    ref, _ = run_oracle(O, coracle, frames, (2, 3, 256, 256), "f32", info)
+    assert_same(got, ref, f"I420 paired chroma, {layout}")
