@@ -114,3 +114,17 @@ def test_variant_library_override_is_confined(evam, monkeypatch, tmp_path):
         native.load_library()
     monkeypatch.delenv("EVAM_PP_LIB")
     assert native.load_library() is not None
+
+
+def test_library_has_no_undefined_kernel_symbols():
+    """Every kernel the host code launches has its host-side stub in the library: a kernel whose stub clang did not
+    emit loads lazily on CPU but fails at dlopen on the GPU box (round 5: a local struct inside a kernel template)."""
+    import shutil
+    import subprocess
+
+    if shutil.which("nm") is None:
+        pytest.skip("needs nm")
+    lib = os.path.join(ROOT, "edge-video-analytics-microservice_amd", "libevam_pp.so")
+    out = subprocess.run(["nm", "-D", "--undefined-only", lib], capture_output=True, text=True, check=True).stdout
+    bad = [ln.split()[-1] for ln in out.splitlines() if "evam" in ln]
+    assert not bad, bad
