@@ -263,87 +263,6 @@ inline void roi_largest_first(const int* idx, int n, const Geom* geo, int DH, bo
 }
 
 
-// Persistent ROI kernel plan (evam_pp_roip): n ROIs (item indices idx[0..n), their clipped geometry geo, source frame
-// frame_of[item]) dealt to G workgroups x K slots, slot[b * K + k] = item or -1 (a workgroup's ROIs fill its slots
-// from 0). Cost of a ROI = cw * min(ch, 2 DH), the shape of its staged source bytes (every ROI writes the same output).
-// Largest first, in snake order over the workgroups (0 .. G-1, then G-1 .. 0, ...), so every workgroup gets a similar
-// total. With xcd, the ROIs of one frame go to the workgroups of one XCD (b % 8 == x: the dispatcher deals workgroups
-// round-robin over the 8 XCDs; a locality hint only, nothing depends on it): frames are dealt largest total first onto
-// the least loaded XCD, then each XCD's ROIs go largest first in snake order over its workgroups. Returns K (<= kcap),
-// or 0 when the XCD deal would need more than kcap slots (the caller then plans without it).
-inline int roi_persist_assign(const int* idx, int n, const Geom* geo, const int* frame_of, int n_frames, int DH, int G,
-                              int kcap, bool xcd, std::vector<int>& slot, std::vector<int>& ord,
-                              std::vector<int64_t>& fcost, std::vector<int>& fx) {
-    if (n <= 0 || G <= 0) return 0;
-    // largest cost first: stable counting sort on 64 buckets
-    int64_t maxw = 1;
-    for (int m = 0; m < n; m++) {
-        const Geom& g = geo[idx[m]];
-        maxw = std::max(maxw, (int64_t)g.cw * std::min(g.ch, 2 * DH));
-    }
-    const double to_bucket = 63.0 / (double)maxw;
-    int start[65] = {0};
-    auto bucket_of = [&](int i) {
-        const int64_t w = (int64_t)geo[i].cw * std::min(geo[i].ch, 2 * DH);
-        return 63 - std::min(63, (int)((double)w * to_bucket));  // 0 = largest
-    };
-    for (int m = 0; m < n; m++) start[bucket_of(idx[m]) + 1]++;
-    for (int b = 0; b < 64; b++) start[b + 1] += start[b];
-    ord.assign(n, 0);
-    for (int m = 0; m < n; m++) ord[start[bucket_of(idx[m])]++] = idx[m];
-    auto deal = [&](const int* list, int cnt, int g0, int step, int gx, int K) {
-        // list[p] -> workgroup g0 + step * j, slot r (snake over the gx workgroups)
-        for (int p = 0; p < cnt; p++) {
-            const int r = p / gx, j0 = p % gx, j = (r & 1) ? gx - 1 - j0 : j0;
-            slot[(size_t)(g0 + step * j) * K + r] = list[p];
-        }
-    };
-    if (xcd && G >= 8 && n_frames > 1) {
-        fcost.assign(n_frames, 0);
-        for (int m = 0; m < n; m++) {
-            const Geom& g = geo[idx[m]];
-            fcost[frame_of[idx[m]]] += (int64_t)g.cw * std::min(g.ch, 2 * DH) + 1;
-        }
-        std::vector<int> fr(n_frames);
-        for (int i = 0; i < n_frames; i++) fr[i] = i;
-        std::stable_sort(fr.begin(), fr.end(), [&](int a, int b) { return fcost[a] > fcost[b]; });
-        int64_t load[8] = {0};
-        int cnt[8] = {0};
-        fx.assign(n_frames, 0);
-        for (int fi : fr) {
-            if (!fcost[fi]) continue;
-            int x = 0;
-            for (int y = 1; y < 8; y++)
-                if (load[y] < load[x]) x = y;
-            fx[fi] = x;
-            load[x] += fcost[fi];
-        }
-        for (int m = 0; m < n; m++) cnt[fx[frame_of[ord[m]]]]++;
-        int K = 1;
-        for (int x = 0; x < 8; x++) {
-            const int gx = (G - x + 7) / 8;
-            K = std::max(K, (cnt[x] + gx - 1) / gx);
-        }
-        if (K <= kcap) {
-            slot.assign((size_t)G * K, -1);
-            std::vector<int> lst;
-            lst.reserve(n);
-            for (int x = 0; x < 8; x++) {
-                lst.clear();
-                for (int m = 0; m < n; m++)
-                    if (fx[frame_of[ord[m]]] == x) lst.push_back(ord[m]);
-                deal(lst.data(), (int)lst.size(), x, 8, (G - x + 7) / 8, K);
-            }
-            return K;
-        }
-        return 0;
-    }
-    const int K = (n + G - 1) / G;
-    if (K > kcap) return 0;
-    slot.assign((size_t)G * K, -1);
-    deal(ord.data(), n, 0, 1, G, K);
-    return K;
-}
 }  // namespace evam
 
 // ROI tail split (evam_pp_run's one-unit-per-ROI plan): every ROI does the same DW x DH pixel work, so when n ROIs

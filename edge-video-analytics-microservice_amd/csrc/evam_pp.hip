@@ -2428,6 +2428,7 @@ __device__ __forceinline__ void wait_vmcnt_stores(int nk) {
 template <int FMT, int OUT, int PX, int NB>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(96))) void evam_pp_roi(const QParams P) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    static_assert(NB == 2, "two staging buffers (three were retired in round 5)");
     using T = FmtTraits<FMT>;
     constexpr bool kYUV = FMT == kNV12 || FMT == kI420;
     constexpr int NP = FMT == kI420 ? 3 : (FMT == kNV12 ? 2 : 1);
@@ -2570,7 +2571,6 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(96))) void
             bool on = q < nq && (e.b0 | e.b1) != 0;           // padding rows stage nothing
             if (pl > 0) on = on && !(tap && (ya >> 1) == (yb >> 1));  // chroma row shared by both taps
             __attribute__((address_space(3))) void* dstl = (__attribute__((address_space(3))) void*)(base + q0 * 16);
-            if constexpr (NB == 3) cnt += __builtin_amdgcn_ballot_w64(on) != 0 ? 1 : 0;
             if (on) {
                 const int yr = tap ? yb : ya;
                 if (pl == 0)
@@ -2593,7 +2593,6 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(96))) void
     };
     uint8_t* const buf0 = smem + P.offBuf;
     uint8_t* const buf1 = buf0 + P.buf_bytes;
-    uint8_t* const buf2 = buf1 + P.buf_bytes;  // NB == 3 only
     issue(0, buf0);
     for (int X = tid; X < DW; X += kThreads) {
         XTab e;
@@ -2741,7 +2740,6 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(96))) void
         else if (grp == pg2) __builtin_amdgcn_s_setprio(1);
         else if (grp == pg3) __builtin_amdgcn_s_setprio(0);
     };
-    if constexpr (NB == 2) {
     for (int grp = 0; grp < ngroups; grp++) {
         step_prio(grp);
         // Wait for this wave's share of group grp's DMA. Group grp-1 was full (only the last group can
@@ -2757,381 +2755,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(96))) void
         compute(grp, (grp & 1) ? buf1 : buf0);
         asm volatile("" ::: "memory");
     }
-    } else {
-    // Three buffers: two groups of DMA in flight while one is converted (the widest crops walk ~15 groups
-    // of ~2.4 us DMA round trips under load with two buffers). In issue order, after group grp's DMA this
-    // wave issued: group grp-2's stores (grp >= 2), group grp+1's DMA (nd_ahead instructions), group
-    // grp-1's stores; groups before the last are full, so each store step counts 3.
-    int nd_ahead = ngroups > 1 ? issue(1, buf1) : 0;
-    uint8_t* bc = buf0;  // buffer of group grp
-    uint8_t* bn = buf2;  // buffer of group grp + 2
-    for (int grp = 0; grp < ngroups; grp++) {
-        step_prio(grp);
-        vmcnt_at_most(nd_ahead + (grp >= 1 ? 3 * nk_w : 0) + (grp >= 2 ? 3 * nk_w : 0));
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();  // every wave's DMA for grp landed; every wave done reading grp-1
-        nd_ahead = grp + 2 < ngroups ? issue(grp + 2, bn) : 0;
-        asm volatile("" ::: "memory");  // later groups' DMA stays ahead of this group's stores
-        compute(grp, bc);
-        asm volatile("" ::: "memory");
-        uint8_t* const t = bc;  // rotate: grp+1 -> current, grp (read by now) -> grp+3's slot
-        bc = bc == buf0 ? buf1 : (bc == buf1 ? buf2 : buf0);
-        bn = t;
-    }
-    }
     EVAM_STAMP(3);
-}
-
-// ------------------------------------------------------------------------------------------------
-// persistent ROI kernel (gvaclassify batches; round 5)
-// ------------------------------------------------------------------------------------------------
-// evam_pp_roi runs one workgroup per ROI, all resident at once, so every workgroup's prologue — its 64-byte
-// record read over PCIe, the geometry, the coefficient tables and group 0's DMA — runs in the same opening
-// window: 14.6 us of a 49.7 us C3 launch (profiles/r05e_c3_prologue_ablation_rocprof.txt: a build that returns
-// once group 0 has landed takes 14.6 us, one that returns after the record and geometry 7.9 us, against 2.1 us
-// for an empty launch). This kernel keeps a few workgroups per CU resident for the whole launch and gives each a
-// list of K ROIs (host-assigned, largest first, snake order; each frame's ROIs on one XCD, so the crops of a
-// frame that overlap share that XCD's L2):
-//  * the workgroup's K records arrive in LDS by one LDS-DMA instruction (one PCIe round trip for all of them);
-//  * ROI k+1's geometry and coefficient tables are built into the second table slot while ROI k's first row
-//    group converts, and its group 0 DMA goes out while ROI k's last group converts: the row-group pipeline
-//    (wait -> barrier -> next group's DMA -> convert and store) runs on across ROIs without a prologue gap;
-//  * the per-pixel arithmetic, staging layout and counted waits are evam_pp_roi's (PX = 1, two buffers).
-struct PParams {
-    const RoiRec* recs;        // G x K records, workgroup-major (item < 0: no ROI in that slot)
-    const float* lut;          // [3][256]
-    void* dst;
-    int DW, DH, K;
-    int mode, placement;       // evam_resize_mode, evam_placement
-    int slot_offset, slot_stride;
-    int offRec, offXT, offYT, offBuf;  // LDS: [LUT][records x K][XTab x DW x 2][YTab x DH x 2][buf0][buf1]
-    int buf_bytes;             // one staging buffer
-    int color_rgb;
-    uint32_t fill;
-    int prio;                  // progress-based priority over the workgroup's ROIs
-};
-
-// Per-ROI state of evam_pp_roip, all wave-uniform.
-struct RoipState {
-    int item;  // < 0: no ROI
-    int x0, y0, cw, ch, rw, rh, ox, oy;
-    const uint8_t *p0, *p1, *p2;
-    int pitch0, pitch1, pitch2;
-    int fsY, nY, fsC, nC, segY, segC, offC;
-    int R, ngroups, nq, Ks;
-    uint32_t mY, mC;
-    double scx;
-};
-
-template <int FMT, int OUT>
-__global__ __launch_bounds__(kThreads) void evam_pp_roip(const PParams P) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    using T = FmtTraits<FMT>;
-    constexpr bool kYUV = FMT == kNV12 || FMT == kI420;
-    constexpr int NP = FMT == kI420 ? 3 : (FMT == kNV12 ? 2 : 1);
-    constexpr int KQ = kRoiK;  // pixels per lane per row group (PX = 1)
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int K = P.K, DW = P.DW, DH = P.DH;
-    asm volatile("" ::"s"(P.recs), "s"(P.lut), "s"(P.color_rgb), "s"(K), "s"(P.offRec), "s"(DW), "s"(DH));
-    // This workgroup's K records: 16 B per lane of wave 0 by LDS-DMA, one round trip over PCIe for all of them.
-    if (wave == 0) {
-        const __amdgpu_buffer_rsrc_t rsR = __builtin_amdgcn_make_buffer_rsrc(
-            (void*)(P.recs + (size_t)blockIdx.x * K), (short)0, K * (int)sizeof(RoiRec), 0x00020000);
-        if (lane < 4 * K)
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsR, (__attribute__((address_space(3))) void*)(smem + P.offRec), 16,
-                                                     (uint32_t)lane * 16u, 0, 0, 0);
-    }
-    // The LUT (fp32), one 1 KB section per wave 1-3, in source channel order (RGB swaps the output planes).
-    const float* lut_s = reinterpret_cast<const float*>(smem);
-    if constexpr (OUT == 1) {
-        if (wave >= 1) {
-            const int sec = wave - 1;
-            const __amdgpu_buffer_rsrc_t rsL = __builtin_amdgcn_make_buffer_rsrc((void*)P.lut, (short)0, 3072, 0x00020000);
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsL, (__attribute__((address_space(3))) void*)(smem + sec * 1024), 16,
-                                                     (uint32_t)lane * 16u, (P.color_rgb ? 2 - sec : sec) * 1024, 0, 0);
-        }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    lds_barrier();
-
-    using St = RoipState;
-    auto xt_of = [&](int s) { return reinterpret_cast<XTab*>(smem + P.offXT + s * DW * (int)sizeof(XTab)); };
-    auto yt_of = [&](int s) { return reinterpret_cast<YTab*>(smem + P.offYT + s * DH * (int)sizeof(YTab)); };
-    auto ptr_of = [](unsigned lo, unsigned hi) { return reinterpret_cast<const uint8_t*>(((uint64_t)hi << 32) | lo); };
-    static_assert(offsetof(RoiRec, pitch) == 24 && offsetof(RoiRec, width) == 36 && offsetof(RoiRec, x) == 40 &&
-                  offsetof(RoiRec, item) == 56, "RoiRec dword map");
-    // Record k -> geometry, footprint, group shape; row table into slot s.
-    auto resolve_rows = [&](int k, int s) -> St {
-        St r;
-        const uint32_t* rec = reinterpret_cast<const uint32_t*>(smem + P.offRec + k * (int)sizeof(RoiRec));
-        uint32_t d[16];
-#pragma unroll
-        for (int j = 0; j < 16; j++) d[j] = __builtin_amdgcn_readfirstlane(rec[j]);
-        r.item = (int)d[14];
-        if (r.item < 0) return r;
-        const int fw = d[9] & 0xFFFF, fh = d[9] >> 16;
-        r.p0 = ptr_of(d[0], d[1]);
-        r.p1 = ptr_of(d[2], d[3]);
-        r.p2 = ptr_of(d[4], d[5]);
-        r.pitch0 = (int)d[6]; r.pitch1 = (int)d[7]; r.pitch2 = (int)d[8];
-        Geom g;
-        roi_geometry(FMT, fw, fh, true, (int)d[10], (int)d[11], (int)d[12], (int)d[13], P.mode, P.placement, DW, DH,
-                     g);  // never empty: the host validated every item
-        r.x0 = __builtin_amdgcn_readfirstlane(g.x0); r.y0 = __builtin_amdgcn_readfirstlane(g.y0);
-        r.cw = __builtin_amdgcn_readfirstlane(g.cw); r.ch = __builtin_amdgcn_readfirstlane(g.ch);
-        r.rw = __builtin_amdgcn_readfirstlane(g.rw); r.rh = __builtin_amdgcn_readfirstlane(g.rh);
-        r.ox = __builtin_amdgcn_readfirstlane(g.ox); r.oy = __builtin_amdgcn_readfirstlane(g.oy);
-        r.scx = 1. / ((double)r.rw / r.cw);
-        const double scy = 1. / ((double)r.rh / r.ch);
-        YTab* yt = yt_of(s);
-        for (int ly = tid; ly < DH; ly += kThreads) {
-            YTab e;
-            e.r0 = 0; e.r1 = 0; e.b0 = 0; e.b1 = 0;
-            const int dy = ly - r.oy;
-            if (dy >= 0 && dy < r.rh) {
-                int sy, b0, b1;
-                linear_coef(dy, scy, r.ch, false, sy, b0, b1);
-                e.r0 = min(max(sy, 0), r.ch - 1);
-                e.r1 = min(max(sy + 1, 0), r.ch - 1);
-                e.b0 = b0 << 8;
-                e.b1 = b1 << 8;
-            }
-            yt[ly] = e;
-        }
-        int fsY, nY, fsC, nC;
-        item_footprint(FMT, T::bpp, r.x0, r.cw, r.rw, r.ox, r.scx, DW, fsY, nY, fsC, nC);
-        r.fsY = __builtin_amdgcn_readfirstlane(fsY); r.nY = __builtin_amdgcn_readfirstlane(nY);
-        r.fsC = __builtin_amdgcn_readfirstlane(fsC); r.nC = __builtin_amdgcn_readfirstlane(nC);
-        r.segY = r.nY * 16;
-        r.segC = r.nC * 16;
-        const int rowb = 2 * r.segY + 2 * (NP - 1) * r.segC;
-        int R = rowb > 0 ? P.buf_bytes / rowb : DH;
-        R = min(R, (KQ * kThreads) / DW);
-        R = max(1, min(R, DH));
-        r.R = R;
-        r.offC = 2 * R * r.segY;
-        r.nq = R * DW;
-        r.Ks = (r.nq + kThreads - 1) / kThreads;
-        r.ngroups = (DH + R - 1) / R;
-        r.mY = r.nY > 1 ? (uint32_t)((0x100000000ull + r.nY - 1) / r.nY) : 0u;
-        r.mC = r.nC > 1 ? (uint32_t)((0x100000000ull + r.nC - 1) / r.nC) : 0u;
-        return r;
-    };
-    auto resolve_cols = [&](const St& r, int s) {
-        XTab* xt = xt_of(s);
-        for (int X = tid; X < DW; X += kThreads) {
-            XTab e;
-            e.s0 = 0; e.s1 = 0; e.a0 = 0; e.a1 = 0; e.pad = 0;
-            const int dx = X - r.ox;
-            if (dx >= 0 && dx < r.rw) {
-                int sx, a0, a1;
-                linear_coef(dx, r.scx, r.cw, true, sx, a0, a1);
-                e.s0 = sx;
-                e.s1 = min(sx + 1, r.cw - 1);
-                e.a0 = (uint16_t)(a0 << 4);
-                e.a1 = (uint16_t)(a1 << 4);
-            }
-            xt[X] = e;
-        }
-    };
-    // Group grp of ROI r into buffer buf: every plane region's 16-byte chunks, 64 per wave-wide LDS-DMA instruction
-    // (chunk q -> (segment, chunk) -> (row, tap) -> source offset), as in evam_pp_roi.
-    auto issue = [&](const St& r, const YTab* yt, int grp, uint8_t* buf) {
-        if (r.nY == 0) return;  // no visible columns: every pixel is fill
-        const int nr = min(r.R, DH - grp * r.R);
-        const __amdgpu_buffer_rsrc_t rsY = __builtin_amdgcn_make_buffer_rsrc((void*)r.p0, (short)0, 0x7FFFFFFF, 0x00020000);
-        const __amdgpu_buffer_rsrc_t rsC = __builtin_amdgcn_make_buffer_rsrc((void*)(r.p1 ? r.p1 : r.p0), (short)0, 0x7FFFFFFF, 0x00020000);
-        const __amdgpu_buffer_rsrc_t rsV = __builtin_amdgcn_make_buffer_rsrc((void*)(r.p2 ? r.p2 : r.p0), (short)0, 0x7FFFFFFF, 0x00020000);
-        auto plane = [&](uint8_t* base, int n, uint32_t m, int pl) {
-            const int nq = 2 * nr * n;
-            for (int q0 = wave * 64; q0 < nq; q0 += 4 * 64) {
-                const int q = q0 + lane;
-                const int seg = n > 1 ? (int)__umulhi((uint32_t)q, m) : q;
-                const int c = q - seg * n;
-                const int rr = seg >> 1, tap = seg & 1;
-                const YTab e = yt[min(grp * r.R + rr, DH - 1)];
-                const int ya = r.y0 + e.r0, yb = r.y0 + e.r1;
-                bool on = q < nq && (e.b0 | e.b1) != 0;               // padding rows stage nothing
-                if (pl > 0) on = on && !(tap && (ya >> 1) == (yb >> 1));  // chroma row shared by both taps
-                __attribute__((address_space(3))) void* dstl = (__attribute__((address_space(3))) void*)(base + q0 * 16);
-                if (on) {
-                    const int yr = tap ? yb : ya;
-                    if (pl == 0)
-                        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsY, dstl, 16, yr * r.pitch0 + r.fsY + c * 16, 0, EVAM_PP_LOAD_AUX, 0);
-                    else if (pl == 1)
-                        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsC, dstl, 16, (yr >> 1) * r.pitch1 + r.fsC + c * 16, 0, EVAM_PP_LOAD_AUX, 0);
-                    else
-                        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsV, dstl, 16, (yr >> 1) * r.pitch2 + r.fsC + c * 16, 0, EVAM_PP_LOAD_AUX, 0);
-                }
-            }
-        };
-        plane(buf, r.nY, r.mY, 0);
-        if constexpr (NP >= 2) plane(buf + r.offC, r.nC, r.mC, 1);
-        if constexpr (NP >= 3) plane(buf + r.offC + 2 * r.R * r.segC, r.nC, r.mC, 2);
-    };
-
-    const uint32_t fsh = OUT == 1 ? 2 : 0;
-    const uint32_t fq0 = P.fill & 0xFF, fq1 = (P.fill >> 8) & 0xFF, fq2 = (P.fill >> 16) & 0xFF;
-    const uint32_t f0 = (P.color_rgb ? fq2 : fq0) << fsh, f1 = fq1 << fsh, f2 = (P.color_rgb ? fq0 : fq2) << fsh;
-    const size_t plane_px = (size_t)DW * DH;
-    const size_t esz = OUT == 1 ? 4 : 1;
-    // per-lane state of the current ROI (identical for every group): row of the pixel inside the group, packed LDS tap
-    // offsets (tap 0 low, tap 1 high half), horizontal weights
-    uint32_t lY[KQ], lC[KQ], wa[KQ];
-    int rr[KQ];
-    auto lane_setup = [&](const St& r, const XTab* xt) {
-#pragma unroll
-        for (int k = 0; k < KQ; k++) {
-            const int q = tid + k * kThreads;
-            const bool v = k < r.Ks && q < r.nq;
-            const int row = v ? q / DW : 0;
-            const int col = v ? q - row * DW : 0;
-            rr[k] = v ? row : -1;
-            const XTab e = xt[col];
-            wa[k] = (uint32_t)e.a0 | ((uint32_t)e.a1 << 16);
-            lY[k] = lC[k] = 0;
-            if (v && wa[k] != 0) {
-                const int ca = r.x0 + e.s0, cb = r.x0 + e.s1;
-                lY[k] = (uint32_t)(ca * T::bpp - r.fsY) | ((uint32_t)(cb * T::bpp - r.fsY) << 16);
-                if constexpr (FMT == kNV12)
-                    lC[k] = (uint32_t)(2 * (ca >> 1) - r.fsC) | ((uint32_t)(2 * (cb >> 1) - r.fsC) << 16);
-                else if constexpr (FMT == kI420)
-                    lC[k] = (uint32_t)((ca >> 1) - r.fsC) | ((uint32_t)((cb >> 1) - r.fsC) << 16);
-            }
-        }
-    };
-    // Convert and store group grp of ROI r from buf. Returns the store steps this wave issued (3 stores each), for the
-    // counted wait of the next group.
-    auto compute = [&](const St& r, const YTab* yt, int grp, const uint8_t* buf) -> int {
-        const size_t slot = (size_t)(P.slot_offset + r.item * P.slot_stride);
-        uint8_t* const d0 = reinterpret_cast<uint8_t*>(P.dst) + slot * 3 * plane_px * esz;
-        uint8_t* const d1 = d0 + plane_px * esz;
-        uint8_t* const d2 = d1 + plane_px * esz;
-        const __amdgpu_buffer_rsrc_t rsD0 = __builtin_amdgcn_make_buffer_rsrc((void*)(P.color_rgb ? d2 : d0), (short)0, 0x7FFFFFFF, 0x00020000);
-        const __amdgpu_buffer_rsrc_t rsD1 = __builtin_amdgcn_make_buffer_rsrc((void*)d1, (short)0, 0x7FFFFFFF, 0x00020000);
-        const __amdgpu_buffer_rsrc_t rsD2 = __builtin_amdgcn_make_buffer_rsrc((void*)(P.color_rgb ? d0 : d2), (short)0, 0x7FFFFFFF, 0x00020000);
-        const uint32_t gbase = (uint32_t)(grp * r.R * DW);
-        const uint8_t* lb = reinterpret_cast<const uint8_t*>(lut_s);
-        int ns = 0;
-#pragma unroll
-        for (int k = 0; k < KQ; k++) {
-            if (k >= r.Ks) break;
-            const int ly = grp * r.R + rr[k];
-            const bool act = rr[k] >= 0 && ly < DH;
-            ns += __builtin_amdgcn_ballot_w64(act) != 0 ? 1 : 0;
-            if (!act) continue;
-            const YTab e = yt[ly];
-            const bool padrow = (e.b0 | e.b1) == 0;  // letterbox padding row
-            const uint8_t* sy0 = buf + 2 * rr[k] * r.segY;
-            const uint8_t* sy1 = sy0 + r.segY;
-            const uint8_t* sc0 = buf + r.offC + 2 * rr[k] * r.segC;
-            const uint8_t* sc1 = sc0;
-            if constexpr (kYUV) {
-                const int ya = r.y0 + e.r0, yb = r.y0 + e.r1;
-                sc1 = (ya >> 1) == (yb >> 1) ? sc0 : sc0 + r.segC;
-            }
-            const uint32_t wb0 = (uint32_t)e.b0, wb1 = (uint32_t)e.b1;
-            uint32_t v[3][1];
-            if (padrow || wa[k] == 0) {
-                v[0][0] = f0; v[1][0] = f1; v[2][0] = f2;
-            } else {
-                const uint32_t a0 = wa[k] & 0xFFFF, a1 = wa[k] >> 16;
-                const uint32_t tY0 = lY[k] & 0xFFFF, tY1 = lY[k] >> 16;
-                if constexpr (kYUV) {
-                    const uint32_t tC0 = lC[k] & 0xFFFF, tC1 = lC[k] >> 16;
-                    const uint8_t* sv0 = FMT == kNV12 ? sc0 + 1 : sc0 + 2 * r.R * r.segC;
-                    const uint8_t* sv1 = FMT == kNV12 ? sc1 + 1 : sc1 + 2 * r.R * r.segC;
-                    const uint32_t wp = (wa[k] >> 4) & 0x0FFF0FFFu;
-                    uint32_t H0[3], H1[3];
-                    hrow_sat(sy0[tY0], sy0[tY1], uv_terms_sat(sc0[tC0], sv0[tC0]), uv_terms_sat(sc0[tC1], sv0[tC1]), wp, H0);
-                    hrow_sat(sy1[tY0], sy1[tY1], uv_terms_sat(sc1[tC0], sv1[tC0]), uv_terms_sat(sc1[tC1], sv1[tC1]), wp, H1);
-#pragma unroll
-                    for (int c3 = 0; c3 < 3; c3++) v[c3][0] = vfinal<OUT>(H0[c3], H1[c3], wb0, wb1);
-                } else {
-                    int c[4][3];
-                    const uint8_t* tap[4] = {sy0 + tY0, sy0 + tY1, sy1 + tY0, sy1 + tY1};
-#pragma unroll
-                    for (int q = 0; q < 4; q++) {
-                        if constexpr (FMT == kBGRX) {
-                            const uint32_t px = *reinterpret_cast<const uint32_t*>(tap[q]);
-                            c[q][0] = px & 0xFF; c[q][1] = (px >> 8) & 0xFF; c[q][2] = (px >> 16) & 0xFF;
-                        } else {
-                            c[q][0] = tap[q][0]; c[q][1] = tap[q][1]; c[q][2] = tap[q][2];
-                        }
-                    }
-#pragma unroll
-                    for (int c3 = 0; c3 < 3; c3++) {
-                        const uint32_t D0 = __umul24(c[0][c3], a0) + __umul24(c[1][c3], a1);
-                        const uint32_t D1 = __umul24(c[2][c3], a0) + __umul24(c[3][c3], a1);
-                        v[c3][0] = vfinal<OUT>(D0, D1, wb0, wb1);
-                    }
-                }
-            }
-            // soffset 0: the row offset is in voffset (store-data hazard of wide stores with an SGPR soffset, see
-            // evam_pp_wave)
-            const uint32_t vo = (gbase + (uint32_t)(tid + k * kThreads)) * (uint32_t)esz;
-            store_off<OUT, 1>(rsD0, vo, lb, v[0]);
-            store_off<OUT, 1>(rsD1, vo, lb + 1024, v[1]);
-            store_off<OUT, 1>(rsD2, vo, lb + 2048, v[2]);
-        }
-        return ns;
-    };
-
-    // ROIs of this workgroup (slots 0 .. nroi-1 hold one; the host fills them in order)
-    int nroi = 0;
-    for (int k = 0; k < K; k++) {
-        const int it = (int)__builtin_amdgcn_readfirstlane(
-            reinterpret_cast<const uint32_t*>(smem + P.offRec + k * (int)sizeof(RoiRec))[14]);
-        nroi += it >= 0 ? 1 : 0;
-    }
-    if (nroi == 0) return;
-    uint8_t* const buf0 = smem + P.offBuf;
-    uint8_t* const buf1 = buf0 + P.buf_bytes;
-    // ROI 0: row table, group 0's DMA, then the column table (its latency overlaps the DMA)
-    St cur = resolve_rows(0, 0);
-    lds_barrier();
-    issue(cur, yt_of(0), 0, buf0);
-    resolve_cols(cur, 0);
-    lds_barrier();
-    St nxt = cur;
-    int slot = 0, b = 0, prev_st = -1;
-    if (P.prio) __builtin_amdgcn_s_setprio(3);
-    for (int k = 0; k < nroi; k++) {
-        // progress-based priority over the workgroup's ROIs (EVAM_PP_PRIO): the workgroups behind get the issue slots
-        if (P.prio && k > 0) {
-            const int q = (4 * k) / nroi;
-            if (q == 1) __builtin_amdgcn_s_setprio(2);
-            else if (q == 2) __builtin_amdgcn_s_setprio(1);
-            else if (q >= 3) __builtin_amdgcn_s_setprio(0);
-        }
-        const XTab* xt = xt_of(slot);
-        const YTab* yt = yt_of(slot);
-        lane_setup(cur, xt);
-        const bool more = k + 1 < nroi;
-        for (int grp = 0; grp < cur.ngroups; grp++) {
-            // This wave's share of group grp's DMA: issued after it were only the previous group's stores.
-            if (prev_st < 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            else wait_vmcnt_stores<3>(prev_st);
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            __builtin_amdgcn_s_barrier();  // every wave's DMA for grp landed; every wave done reading grp-1
-            if (grp == 0 && more) {
-                // next ROI's tables into the other slot (its previous ROI finished with it before this barrier)
-                nxt = resolve_rows(k + 1, slot ^ 1);
-                resolve_cols(nxt, slot ^ 1);
-                if (cur.ngroups == 1) lds_barrier();  // its group 0 DMA goes out right below
-            }
-            if (grp + 1 < cur.ngroups) issue(cur, yt, grp + 1, b ? buf0 : buf1);
-            else if (more) issue(nxt, yt_of(slot ^ 1), 0, b ? buf0 : buf1);
-            asm volatile("" ::: "memory");  // the next group's DMA stays ahead of this group's stores
-            prev_st = compute(cur, yt, grp, b ? buf1 : buf0);
-            asm volatile("" ::: "memory");
-            b ^= 1;
-        }
-        cur = nxt;
-        slot ^= 1;
-    }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -3209,15 +2833,10 @@ struct Knobs {
     int nsegx = 0;                                 // staged tile width in 64-column segments (0: widest that fits)
     int stage_r = -1;                              // staged pipeline: rows per group
     int wth = -1, px = 0, reuse = 1, wave_lds = 40 * 1024;
-    int roi_th = -1, roi_buf = -1, roi_px = 1, roi_xcd = 0;  // roi_buf -1: sized for one round
+    int roi_th = -1, roi_buf = -1, roi_px = 1;     // roi_buf -1: sized for one round
     int roi_sort = 0;  // 1: largest estimated bytes first before the stable sort by row groups (C3: equal or
                        // slower, profiles/r04k_ab_lines.txt; the units are ordered by row groups either way)
-    int roi_unit = 0;                              // ROI work-unit size in row groups (0: one unit per base tile)
-    int roi_nbuf = 2;                              // ROI staging buffers (3: two groups of DMA in flight)
     int roi_tail = 4;                              // row tiles per ROI of the uneven tail over the CUs (1: no split)
-    int roi_persist = 0;                           // 1: ROI batches on the persistent kernel (evam_pp_roip)
-    int roi_wgs = 4;                               // persistent ROI kernel: resident workgroups per CU
-    int roi_frames_xcd = 1;                        // persistent ROI kernel: each frame's ROIs on one XCD
     int strip = 1, strip_th = -1, strip_nw = -1, strip_px = 0;  // strip kernel: allowed (2: forced), rows per
                                                                 // tile, waves, px
     int strip_pair = 1;                            // strip kernel: paired-tap DMA where the footprints allow it
@@ -3246,10 +2865,7 @@ struct Knobs {
         reuse = env_int("EVAM_PP_REUSE", reuse); wave_lds = env_int("EVAM_PP_WAVE_LDS", wave_lds);
         roi_th = env_int("EVAM_PP_ROI_TH", roi_th); roi_buf = env_int("EVAM_PP_ROI_BUF", roi_buf);
         roi_px = env_int("EVAM_PP_ROI_PX", roi_px); roi_sort = env_int("EVAM_PP_ROI_SORT", roi_sort);
-        roi_xcd = env_int("EVAM_PP_ROI_XCD", roi_xcd); roi_unit = env_int("EVAM_PP_ROI_UNIT", roi_unit);
-        roi_nbuf = env_int("EVAM_PP_ROI_NBUF", roi_nbuf); roi_tail = env_int("EVAM_PP_ROI_TAIL", roi_tail);
-        roi_persist = env_int("EVAM_PP_ROI_PERSIST", roi_persist); roi_wgs = env_int("EVAM_PP_ROI_WGS", roi_wgs);
-        roi_frames_xcd = env_int("EVAM_PP_ROI_FRAMES_XCD", roi_frames_xcd);
+        roi_tail = env_int("EVAM_PP_ROI_TAIL", roi_tail);
     }
 };
 
@@ -3415,11 +3031,11 @@ hipError_t launch_roi_px(const QParams& p, int grid, int lds, hipStream_t s) {
 // PX = 1 (adjacent lanes, adjacent pixels) by default. PX = 4 (one dwordx4 store per channel and
 // one row setup per 4 pixels; EVAM_PP_ROI_PX=4) measured 8 % slower on C3: lanes 4 pixels apart
 // spread their LDS tap reads over 4x more dwords, so the byte reads bank-conflict.
-// NB = 3 staging buffers (EVAM_PP_ROI_NBUF=3): two groups of DMA in flight, PX = 1 only.
+// (Three staging buffers, EVAM_PP_ROI_NBUF=3, measured neutral or slower for two rounds: retired in round 5.)
 template <int FMT, int OUT>
 hipError_t launch_roi_t(int px, int nb, const QParams& p, int grid, int lds, hipStream_t s) {
+    (void)nb;
     if (px == 4 && p.DW % 4 == 0) return launch_roi_px<FMT, OUT, 4, 2>(p, grid, lds, s);
-    if (nb == 3) return launch_roi_px<FMT, OUT, 1, 3>(p, grid, lds, s);
     return launch_roi_px<FMT, OUT, 1, 2>(p, grid, lds, s);
 }
 
@@ -3566,7 +3182,10 @@ bool plan_wave(int f, const Geom& g, int DW, int DH, int count, int out_dtype, i
 
 // Ring depth: D = 2 (D 1 / 3 / 4 measured slower on C2 and C5, rounds 2-3: profiles/r03f_bench_lines.txt, C2 D 3
 // +2.7 us; the other depths were retired in round 5).
-constexpr int kStripD = 2;
+#ifndef EVAM_PP_STRIP_DEPTH
+#define EVAM_PP_STRIP_DEPTH 2  // A/B builds only (tools/build_variant.sh -DEVAM_PP_STRIP_DEPTH=3)
+#endif
+constexpr int kStripD = EVAM_PP_STRIP_DEPTH;
 template <int FMT, int OUT, int PX>
 const void* strip_fn_p(int pr) {
     return pr ? (const void*)evam_pp_strip<FMT, OUT, kStripD, PX, 1> : (const void*)evam_pp_strip<FMT, OUT, kStripD, PX, 0>;
@@ -3819,8 +3438,8 @@ hipError_t launch_band(int f, int out, int px, const TParams& p, dim3 grid, int 
 
 template <int FMT, int OUT>
 const void* roi_fn_t(int px, int nb) {
-    return px == 4 ? (const void*)evam_pp_roi<FMT, OUT, 4, 2>
-                   : (nb == 3 ? (const void*)evam_pp_roi<FMT, OUT, 1, 3> : (const void*)evam_pp_roi<FMT, OUT, 1, 2>);
+    (void)nb;
+    return px == 4 ? (const void*)evam_pp_roi<FMT, OUT, 4, 2> : (const void*)evam_pp_roi<FMT, OUT, 1, 2>;
 }
 const void* roi_fn(int f, int out, int px, int nb) {
     switch (f * 2 + out) {
@@ -3833,72 +3452,6 @@ const void* roi_fn(int f, int out, int px, int nb) {
     case kBGR * 2 + 0: return roi_fn_t<kBGR, 0>(px, nb);
     default: return roi_fn_t<kBGR, 1>(px, nb);
     }
-}
-
-template <int FMT, int OUT>
-hipError_t launch_roip_t(const PParams& p, int grid, int lds, hipStream_t s) {
-    if (lds > 64 * 1024) {
-        hipError_t e = hipFuncSetAttribute((const void*)evam_pp_roip<FMT, OUT>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-        if (e != hipSuccess) return e;
-    }
-    hipLaunchKernelGGL((evam_pp_roip<FMT, OUT>), dim3(grid), dim3(kThreads), lds, s, p);
-    return hipGetLastError();
-}
-hipError_t launch_roip(int f, int out, const PParams& p, int grid, int lds, hipStream_t s) {
-    switch (f * 2 + out) {
-    case kNV12 * 2 + 0: return launch_roip_t<kNV12, 0>(p, grid, lds, s);
-    case kNV12 * 2 + 1: return launch_roip_t<kNV12, 1>(p, grid, lds, s);
-    case kI420 * 2 + 0: return launch_roip_t<kI420, 0>(p, grid, lds, s);
-    case kI420 * 2 + 1: return launch_roip_t<kI420, 1>(p, grid, lds, s);
-    case kBGRX * 2 + 0: return launch_roip_t<kBGRX, 0>(p, grid, lds, s);
-    case kBGRX * 2 + 1: return launch_roip_t<kBGRX, 1>(p, grid, lds, s);
-    case kBGR * 2 + 0: return launch_roip_t<kBGR, 0>(p, grid, lds, s);
-    default: return launch_roip_t<kBGR, 1>(p, grid, lds, s);
-    }
-}
-const void* roip_fn(int f, int out) {
-    switch (f * 2 + out) {
-    case kNV12 * 2 + 0: return (const void*)evam_pp_roip<kNV12, 0>;
-    case kNV12 * 2 + 1: return (const void*)evam_pp_roip<kNV12, 1>;
-    case kI420 * 2 + 0: return (const void*)evam_pp_roip<kI420, 0>;
-    case kI420 * 2 + 1: return (const void*)evam_pp_roip<kI420, 1>;
-    case kBGRX * 2 + 0: return (const void*)evam_pp_roip<kBGRX, 0>;
-    case kBGRX * 2 + 1: return (const void*)evam_pp_roip<kBGRX, 1>;
-    case kBGR * 2 + 0: return (const void*)evam_pp_roip<kBGR, 0>;
-    default: return (const void*)evam_pp_roip<kBGR, 1>;
-    }
-}
-
-// Persistent ROI-kernel plan (evam_pp_roip) for one format group: G = n_cu x W workgroups (W = EVAM_PP_ROI_WGS, all
-// resident), K ROI slots each (kalloc: room for the XCD deal's imbalance), and the LDS carve
-// [LUT][records x kalloc][XTab x DW x 2][YTab x DH x 2][two staging buffers], the buffers taking what W workgroups per CU
-// leave (at most 32 KB; at least the widest crop's output row). False: the group takes evam_pp_roi.
-constexpr int kRoipKcap = 16;  // records per workgroup: one LDS-DMA instruction of 64 x 16 B
-bool plan_roip(int f, int DW, int DH, int out_dtype, int max_row_bytes, int count, int n_cu, const Knobs& kn, PParams& q,
-               int& G, int& kalloc, int& lds) {
-    if (DW > kRoiK * kThreads || DH > 65535 || count <= 0) return false;
-    const int W = std::max(1, std::min(8, kn.roi_wgs));
-    G = std::min(count, n_cu * W);
-    int K = (count + G - 1) / G;
-    if (K > kRoipKcap) { K = kRoipKcap; G = (count + K - 1) / K; }
-    kalloc = std::min(kRoipKcap, K + (kn.roi_frames_xcd ? 1 : 0));
-    q.DW = DW; q.DH = DH;
-    q.offRec = out_dtype == EVAM_DTYPE_F32 ? kLutBytes : 0;
-    q.offXT = q.offRec + kalloc * (int)sizeof(RoiRec);
-    q.offYT = q.offXT + 2 * DW * (int)sizeof(XTab);
-    q.offBuf = q.offYT + 2 * DH * (int)sizeof(YTab);
-    const int budget = ((160 * 1024) / W) & ~1023;
-    int buf = std::min(32 * 1024, ((budget - q.offBuf) / 2) & ~15);
-    if (buf < max_row_bytes) buf = (max_row_bytes + 15) & ~15;
-    q.buf_bytes = buf;
-    lds = q.offBuf + 2 * buf;
-    if (lds > 160 * 1024) return false;
-    const void* fn = roip_fn(f, out_dtype);
-    while (resident_per_cu(fn, lds) < W && q.buf_bytes - 512 >= max_row_bytes) {
-        q.buf_bytes -= 512;
-        lds -= 2 * 512;
-    }
-    return true;
 }
 
 // ROI-kernel plan for one format group with per-item geometry: the tile height, the LDS carve and the
@@ -3927,7 +3480,7 @@ bool plan_roi(int f, int DW, int DH, int out_dtype, int px, int max_row_bytes, i
     const int64_t grid = (int64_t)count * base_tiles;
     const int per_cu = (int)std::max<int64_t>(1, std::min<int64_t>(kRoiWavesPerSimd, (grid + n_cu - 1) / n_cu));
     const int pxv = px == 4 && DW % 4 == 0 ? 4 : 1;
-    const int nb = pxv == 1 && kn.roi_nbuf == 3 ? 3 : 2;
+    const int nb = 2;
     int buf = kn.roi_buf;
     if (buf <= 0) buf = std::min(12 * 1024, ((((160 * 1024) / per_cu) & ~1023) - q.offBuf) / nb & ~15);
     q.buf_bytes = (std::max(buf, max_row_bytes) + 15) & ~15;
@@ -4032,11 +3585,8 @@ struct evam_pp {
     std::vector<int> sc_members;   // item indices grouped by source format
     std::vector<Geom> sc_geo;
     std::vector<int> sc_units;     // ROI work units: (item, row0, row1, cost)
-    std::vector<int> sc_frame_of, sc_pslot, sc_fx;  // persistent ROI plan: item -> frame, slots, frame -> XCD
-    std::vector<int64_t> sc_fcost;                  // persistent ROI plan: per frame cost
     std::vector<int> sc_start;     // ROI unit counting sort: bucket starts
     std::vector<int> sc_slot;      // ROI units in launch order
-    std::vector<int> sc_xq[8];     // ROI units per XCD (EVAM_PP_ROI_XCD)
     int memo_key[4] = {-1, -1, -1, -1};  // (format, staging buffer, row cap, DH) of memo_rg
     std::vector<uint32_t> memo_rg;       // per crop width: rows per group | groups of the whole height << 16
     TParams sc_tparams;            // strip-kernel arguments (3.5 KB: kept off the stack)
@@ -4340,11 +3890,9 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
     //   uniform geometry        -> staged / wave / row kernels: host-built tables, items in kernel arguments
     //   per-item geometry       -> ROI kernel: raw ROI rect + source (RoiRec), geometry resolved on the device
     //   ROI plan impossible     -> generic kernel, per-item ItemDesc in the descriptor block
-    enum { kPathNone, kPathUniform, kPathRoi, kPathGeneric, kPathRoiP };
+    enum { kPathNone, kPathUniform, kPathRoi, kPathGeneric };
     int path[4];
     QParams qp[4];
-    PParams pq[4];
-    int pG[4] = {0, 0, 0, 0}, pKa[4] = {0, 0, 0, 0}, pK[4] = {0, 0, 0, 0}, plds[4] = {0, 0, 0, 0};
     int qlds[4] = {0, 0, 0, 0}, qbase[4] = {1, 1, 1, 1}, qrec[4] = {0, 0, 0, 0};
     int64_t qslots[4] = {0, 0, 0, 0};
     bool any_generic = false, any_roi = false;
@@ -4352,20 +3900,18 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
         path[f] = kPathNone;
         if (!count[f]) continue;
         if (uniform[f] && kn.rows) path[f] = kPathUniform;
-        else if (kn.roi && kn.roi_persist && plan_roip(f, DW, DH, cfg->out_dtype, row_bytes_bound(f, max_cw[f]), count[f],
-                                                       h->n_cu, kn, pq[f], pG[f], pKa[f], plds[f])) path[f] = kPathRoiP;
         else if (kn.roi && plan_roi(f, DW, DH, cfg->out_dtype, kn.roi_px, row_bytes_bound(f, max_cw[f]), count[f], h->n_cu,
                                     kn, qp[f], qbase[f], qlds[f], qslots[f])) path[f] = kPathRoi;
         else path[f] = kPathGeneric;
         any_generic |= path[f] == kPathGeneric;
-        any_roi |= path[f] == kPathRoi || path[f] == kPathRoiP;
+        any_roi |= path[f] == kPathRoi;
     }
     // Full geometry on the host only where something consumes it.
     const bool all_geo = out_xform != nullptr || h->opt_stats;
     int64_t src_bytes = 0;
     for (int i = 0; i < n_items; i++) {
         const int f = fmt[i];
-        if (!all_geo && (path[f] == kPathRoi || path[f] == kPathRoiP)) continue;
+        if (!all_geo && path[f] == kPathRoi) continue;
         if (!all_geo && path[f] == kPathUniform && i != rep[f]) continue;  // same crop size: rep's geometry
         Geom& g = geo[i];
         const evam_roi* r = items ? &items[i] : nullptr;
@@ -4405,19 +3951,11 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
     size_t rec_off[4] = {0, 0, 0, 0}, dyn_bytes = 0;
     if (any_roi) {
         for (int f = 0; f < 4; f++) {
-            if (path[f] == kPathRoiP) {
-                rec_off[f] = dyn_bytes;
-                dyn_bytes += sizeof(RoiRec) * (size_t)pG[f] * (size_t)pKa[f];
-                continue;
-            }
             if (path[f] != kPathRoi) continue;
             rec_off[f] = dyn_bytes;
-            // at most ceil(groups / roi_unit) <= DH units per ROI when base tiles are split
-            const int64_t per = qbase[f] == 1 && kn.roi_unit > 0
-                                    ? std::min<int64_t>(DH, (DH + kn.roi_unit - 1) / kn.roi_unit) : qbase[f];
-            dyn_bytes += sizeof(RoiRec) * (size_t)count[f] * (size_t)per;
+            dyn_bytes += sizeof(RoiRec) * (size_t)count[f] * (size_t)qbase[f];
             // tail split: up to n_cu ROIs become kn.roi_tail row tiles each
-            if (qbase[f] == 1 && kn.roi_unit <= 0 && kn.roi_tail > 1)
+            if (qbase[f] == 1 && kn.roi_tail > 1)
                 dyn_bytes += sizeof(RoiRec) * (size_t)std::min(count[f], h->n_cu) * (size_t)(kn.roi_tail - 1);
         }
     }
@@ -4482,67 +4020,26 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
         // bytes, crop width x touched rows). Workgroups are dispatched in order as slots free, so
         // the long ROIs start first and the short ones fill the tail.
         const bool sort = kn.roi_sort != 0;
-        const bool xcd_group = kn.roi_xcd != 0;
         std::vector<int>& bucket = h->sc_bucket;
         bucket.resize(n_items);
         for (int f = 0; f < 4; f++) {
-            if (path[f] == kPathRoiP) {
-                // persistent ROI kernel: every workgroup's K records, workgroup-major (roi_persist_assign)
-                RoiRec* rr = reinterpret_cast<RoiRec*>(dyn + rec_off[f]);
-                std::vector<int>& fo = h->sc_frame_of;  // per item: its source frame
-                fo.resize(n_items);
-                for (int m = mfirst[f]; m < mfirst[f + 1]; m++) {
-                    const int i = members[m];
-                    fo[i] = items ? items[i].src_index : i;
-                }
-                int K = roi_persist_assign(members.data() + mfirst[f], count[f], geo.data(), fo.data(), n_srcs, DH, pG[f],
-                                           pKa[f], kn.roi_frames_xcd != 0, h->sc_pslot, h->sc_order, h->sc_fcost, h->sc_fx);
-                if (!K)  // the XCD deal needs more slots than planned: one pool (K = ceil(count / G) fits)
-                    K = roi_persist_assign(members.data() + mfirst[f], count[f], geo.data(), fo.data(), n_srcs, DH, pG[f],
-                                           pKa[f], false, h->sc_pslot, h->sc_order, h->sc_fcost, h->sc_fx);
-                if (!K) return fail(EVAM_PP_ERR_INVALID_ARG, "evam_pp_run: persistent ROI plan failed");
-                pK[f] = K;
-                const int* sl = h->sc_pslot.data();
-                const int total = pG[f] * K;
-                for (int pos = 0; pos < total; pos++) {
-                    const int i = sl[pos];
-                    RoiRec r;  // built in registers, then one 64-byte copy into the write-combined slot
-                    if (i < 0) {
-                        memset(&r, 0, sizeof(r));
-                        r.item = -1;
-                    } else {
-                        const evam_image& sim = srcs[items ? items[i].src_index : i];
-                        r.plane[0] = sim.planes[0]; r.plane[1] = sim.planes[1]; r.plane[2] = sim.planes[2];
-                        r.pitch[0] = sim.pitch[0]; r.pitch[1] = sim.pitch[1]; r.pitch[2] = sim.pitch[2];
-                        r.width = (uint16_t)sim.width; r.height = (uint16_t)sim.height;
-                        if (items) { r.x = items[i].x; r.y = items[i].y; r.w = items[i].w; r.h = items[i].h; }
-                        else { r.x = r.y = r.w = r.h = 0; }  // w <= 0: the full frame
-                        r.item = i;
-                        r.row0 = 0;
-                        r.row1 = (uint16_t)DH;
-                    }
-                    memcpy(&rr[pos], &r, sizeof(RoiRec));
-                }
-                continue;
-            }
             if (path[f] != kPathRoi) continue;
             RoiRec* rr = reinterpret_cast<RoiRec*>(dyn + rec_off[f]);
             std::vector<int>& ord = h->sc_order;
             roi_largest_first(members.data() + mfirst[f], count[f], geo.data(), DH, sort, bucket.data(), ord);
             HP(6);
-            // Work units (one workgroup each): row tiles of each ROI of about kn.roi_unit row groups (a
-            // group is one DMA round trip: the per-workgroup critical path), so the widest crops no
-            // longer bound the launch. Units launch largest first; beyond the resident workgroups the
-            // dispatcher starts each remaining unit as a slot frees up.
+            // Work units (one workgroup each): one per ROI, or per row tile of TH rows for outputs taller than one
+            // tile. Units launch largest first; beyond the resident workgroups the dispatcher starts each remaining
+            // unit as a slot frees up. (Row tiles of a few row groups per ROI, EVAM_PP_ROI_UNIT, measured slower for
+            // two rounds and were retired in round 5.)
             const QParams& q = qp[f];
             const int base = qbase[f];
             const int pxr = kn.roi_px == 4 && DW % 4 == 0 ? 4 : 1;
             const int rcap = std::max(1, ((kRoiK / pxr) * kThreads) / (DW / pxr));
-            const int gt = kn.roi_unit;
             std::vector<int>& un = h->sc_units;  // (item, row0, row1, cost) per unit
             un.clear();
             int maxcost = 1;
-            if (base == 1 && gt <= 0) {
+            if (base == 1) {
                 // one unit per ROI (the default): no row split, no 64-bit divisions (this loop runs per ROI
                 // on the host for every call: 1,600 ROIs in C3)
                 // Tail split: every ROI does the same pixel work (DW x DH), so when the ROIs do not divide
@@ -4592,11 +4089,9 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
             for (size_t p = 0; p < ord.size(); p++) {
                 const int i = ord[p];
                 const int R = std::max(1, std::min(std::min(q.buf_bytes / row_bytes_bound(f, geo[i].cw), rcap), DH));
-                int nt = base;
-                if (base == 1 && gt > 0) nt = std::max(1, std::min(DH, ((DH + R - 1) / R + gt - 1) / gt));
-                for (int t = 0; t < nt; t++) {
-                    const int y0 = base > 1 ? t * q.TH : (int)((int64_t)DH * t / nt);
-                    const int y1 = base > 1 ? std::min(DH, (t + 1) * q.TH) : (int)((int64_t)DH * (t + 1) / nt);
+                for (int t = 0; t < base; t++) {
+                    const int y0 = t * q.TH;
+                    const int y1 = std::min(DH, (t + 1) * q.TH);
                     const int cost = (y1 - y0 + R - 1) / R;
                     maxcost = std::max(maxcost, cost);
                     un.insert(un.end(), {i, y0, y1, cost});
@@ -4613,48 +4108,6 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
             std::vector<int>& order = h->sc_slot;
             order.resize(nu);
             for (int u = 0; u < nu; u++) order[start[maxcost - un[4 * u + 3]]++] = u;
-            if (xcd_group) {
-                // Record p runs on XCD p % 8 (blocks are dealt round-robin): deal the units of frame s to
-                // positions = s (mod 8), largest first within each XCD, so the overlapping crops of one frame
-                // share one L2; a position whose XCD has no units left takes the largest head of another.
-                std::vector<int>* q = h->sc_xq;
-                for (int x = 0; x < 8; x++) q[x].clear();
-                // frames onto XCDs largest total first, each onto the least loaded (a unit costs its row groups plus
-                // the fixed output work, ~4 groups' worth), so every XCD gets about the same work
-                std::vector<int64_t>& fc = h->sc_fcost;
-                std::vector<int>& fx = h->sc_fx;
-                fc.assign(n_srcs, 0);
-                for (int u = 0; u < nu; u++) {
-                    const int i = un[4 * u];
-                    fc[items ? items[i].src_index : i] += 4 + un[4 * u + 3];
-                }
-                std::vector<int>& fr = h->sc_frame_of;
-                fr.resize(n_srcs);
-                for (int k = 0; k < n_srcs; k++) fr[k] = k;
-                std::stable_sort(fr.begin(), fr.end(), [&](int a, int b) { return fc[a] > fc[b]; });
-                fx.assign(n_srcs, 0);
-                int64_t load[8] = {0};
-                for (int k : fr) {
-                    int x = 0;
-                    for (int y = 1; y < 8; y++)
-                        if (load[y] < load[x]) x = y;
-                    fx[k] = x;
-                    load[x] += fc[k];
-                }
-                for (int u : order) {
-                    const int i = un[4 * u];
-                    q[fx[items ? items[i].src_index : i]].push_back(u);
-                }
-                size_t head[8] = {0};
-                for (int p = 0; p < nu; p++) {
-                    int x = p & 7;
-                    if (head[x] == q[x].size())
-                        for (int y = 0, best = -1; y < 8; y++)
-                            if (head[y] < q[y].size() &&
-                                (best < 0 || un[4 * q[y][head[y]] + 3] > un[4 * q[best][head[best]] + 3])) x = best = y;
-                    order[p] = q[x][head[x]++];
-                }
-            }
             for (int pos = 0; pos < nu; pos++) {
                 const int u = order[pos];
                 const int i = un[4 * u];
@@ -4702,24 +4155,6 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
     };
     for (int f = 0; f < 4; f++) {
         if (path[f] == kPathNone) continue;
-        if (path[f] == kPathRoiP) {
-            PParams& q = pq[f];
-            q.recs = reinterpret_cast<const RoiRec*>(d_dyn + rec_off[f]);
-            q.lut = lut_d;
-            q.dst = dst->data;
-            q.K = pK[f];
-            q.mode = cfg->resize_mode;
-            q.placement = cfg->placement;
-            q.slot_offset = dst->slot_offset;
-            q.slot_stride = dst->slot_stride;
-            q.color_rgb = color_rgb;
-            q.fill = fill;
-            q.prio = kn.prio;
-            hipError_t e = launch_roip(f, cfg->out_dtype, q, pG[f], plds[f], h->stream);
-            if (e != hipSuccess) return fail(EVAM_PP_ERR_HIP, "kernel launch failed: %s", hipGetErrorString(e));
-            launches++; kmask |= EVAM_KERNEL_ROI;
-            continue;
-        }
         if (path[f] == kPathRoi) {
             QParams& q = qp[f];
             q.recs = reinterpret_cast<const RoiRec*>(d_dyn + rec_off[f]);
@@ -4734,7 +4169,7 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
             q.prio = kn.prio;
             const int64_t grid = qrec[f];
             if (grid > 0x7FFFFFFF) return fail(EVAM_PP_ERR_INVALID_ARG, "evam_pp_run: too many tiles");
-            hipError_t e = launch_roi(f, cfg->out_dtype, kn.roi_px, kn.roi_nbuf, q, (int)grid, qlds[f], h->stream);
+            hipError_t e = launch_roi(f, cfg->out_dtype, kn.roi_px, 2, q, (int)grid, qlds[f], h->stream);
             if (e != hipSuccess) return fail(EVAM_PP_ERR_HIP, "kernel launch failed: %s", hipGetErrorString(e));
             launches++; kmask |= EVAM_KERNEL_ROI;
             continue;

@@ -339,63 +339,8 @@ static void check_clip_simd() {
 }
 
 
-// Persistent ROI plan (roi_persist_assign): every ROI in exactly one slot, a workgroup's ROIs in slots 0.. without
-// gaps, K = ceil(n / G) in one pool and at most kcap with the XCD deal, every frame's ROIs on workgroups of one XCD
-// (b % 8), and the snake deal's per-workgroup cost spread bounded by the largest ROI per round.
-static void check_roi_persist() {
-    std::vector<int> slot, ord, fx;
-    std::vector<int64_t> fcost;
-    int xcd_used = 0;
-    for (int it = 0; it < 3000; it++) {
-        const int n = uni(1, 2500), G = uni(1, 1100), n_frames = uni(1, 64), DH = uni(1, 200);
-        const bool xcd = uni(0, 1);
-        std::vector<Geom> geo(n + 7);
-        std::vector<int> idx(n), frame(n + 7, -1);
-        for (int m = 0; m < n; m++) {
-            const int i = m + (it % 7);  // item indices need not start at 0
-            idx[m] = i;
-            geo[i] = Geom{0, 0, uni(2, 400), uni(2, 300), 0, 0, 0, 0};
-            frame[i] = uni(0, n_frames - 1);
-        }
-        const int kcap = 16;
-        int K = roi_persist_assign(idx.data(), n, geo.data(), frame.data(), n_frames, DH, G, kcap, xcd, slot, ord, fcost, fx);
-        const int K1 = (n + G - 1) / G;
-        const bool dealt = K != 0 && xcd && G >= 8 && n_frames > 1;  // the XCD deal ran
-        if (!K) {
-            CHECK(xcd || K1 > kcap, "persist it %d: no plan without the XCD deal", it);
-            if (K1 > kcap) continue;
-            K = roi_persist_assign(idx.data(), n, geo.data(), frame.data(), n_frames, DH, G, kcap, false, slot, ord, fcost, fx);
-        }
-        CHECK(K >= 1 && K <= kcap && (int64_t)slot.size() == (int64_t)G * K, "persist it %d: K %d", it, K);
-        std::vector<int> seen(n + 7, 0), wg_of(n + 7, -1);
-        for (int b = 0; b < G; b++) {
-            bool gap = false;
-            for (int k = 0; k < K; k++) {
-                const int i = slot[(size_t)b * K + k];
-                if (i < 0) { gap = true; continue; }
-                CHECK(!gap, "persist it %d: workgroup %d has a hole before slot %d", it, b, k);
-                CHECK(i >= it % 7 && i < n + it % 7, "persist it %d: item %d out of range", it, i);
-                seen[i]++;
-                wg_of[i] = b;
-            }
-        }
-        for (int m = 0; m < n; m++) CHECK(seen[idx[m]] == 1, "persist it %d: item %d placed %d times", it, idx[m], seen[idx[m]]);
-        if (!xcd || G < 8 || n_frames < 2) CHECK(K == K1, "persist it %d: K %d != %d", it, K, K1);
-        if (dealt) {  // every frame's ROIs on the workgroups of one XCD
-            std::vector<int> fxcd(n_frames, -1);
-            for (int m = 0; m < n; m++) {
-                const int i = idx[m], x = wg_of[i] % 8;
-                if (fxcd[frame[i]] < 0) fxcd[frame[i]] = x;
-                CHECK(fxcd[frame[i]] == x, "persist it %d: frame %d on XCDs %d and %d", it, frame[i], fxcd[frame[i]], x);
-            }
-            xcd_used++;
-        }
-    }
-    printf("roi_persist: 3000 plans checked, %d with every frame on one XCD\n", xcd_used);
-}
 
 int main() {
-    check_roi_persist();
     check_clip_simd();
     check_roi_tail();
     check_geometry();

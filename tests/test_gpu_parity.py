@@ -472,26 +472,6 @@ def test_roi_kernel_px4(evam, O, coracle, gpu, fmt, dst, dtype, monkeypatch):
 
 
 @pytest.mark.parametrize("fmt", FORMATS)
-def test_roi_kernel_xcd_order(evam, O, coracle, gpu, fmt, monkeypatch):
-    """ROI records dealt to XCDs by source frame (EVAM_PP_ROI_XCD=1), more frames than XCDs."""
-    import torch
-
-    monkeypatch.setenv("EVAM_PP_ROI_XCD", "1")
-    rng = np.random.default_rng(zlib.crc32(f"xcd{fmt}".encode()))
-    W, H = 192, 108
-    frames = [O.random_frame(rng, fc(O, fmt), W, H, pattern="gradient" if i % 2 else "uniform") for i in range(11)]
-    rois = [(int(rng.integers(0, 11)), int(rng.integers(0, W - 8)), int(rng.integers(0, H - 8)),
-             int(rng.integers(4, 120)), int(rng.integers(4, 90))) for _ in range(53)]
-    info = evam.PreProcInfo(resize="aspect-ratio", placement="center", fill=(1, 2, 3),
-                            range=(0.0, 1.0), mean=(0.1, 0.2, 0.3), std=(0.3, 0.2, 0.1))
-    shape = (len(rois), 3, 40, 40)
-    got, _ = run_hip(evam, torch, upload(evam, frames, gpu), shape, torch.float32, info,
-                     rois=[evam.Roi(*r) for r in rois])
-    ref, _ = run_oracle(O, coracle, frames, shape, "f32", info, rois=rois)
-    assert_same(got, ref, f"roi xcd order {fmt}")
-
-
-@pytest.mark.parametrize("fmt", FORMATS)
 @pytest.mark.parametrize("kind", ["inside", "mixed"])
 @pytest.mark.parametrize("simd", ["1", "0"])
 def test_roi_host_pass1_simd(evam, O, coracle, gpu, fmt, kind, simd, monkeypatch):
@@ -616,26 +596,6 @@ def test_staged_many_tile_columns(evam, O, coracle, gpu, fmt, monkeypatch):
     assert_same(got, ref, f"staged >16 tile columns {fmt}")
 
 
-@pytest.mark.parametrize("unit", ["2", "4"])
-def test_roi_work_units(evam, O, coracle, gpu, unit, monkeypatch):
-    """ROI batches with the crops split into row tiles of a few row groups each (EVAM_PP_ROI_UNIT): every
-    tile of a ROI lands in its own rows of the ROI's slot."""
-    import torch
-
-    monkeypatch.setenv("EVAM_PP_ROI_UNIT", unit)
-    rng = np.random.default_rng(zlib.crc32(f"unit{unit}".encode()))
-    W, H = 640, 360
-    frames = [O.random_frame(rng, O.NV12, W, H, pattern="gradient" if i else "uniform") for i in range(2)]
-    rois = [(int(rng.integers(0, 2)), int(rng.integers(0, W - 8)), int(rng.integers(0, H - 8)),
-             int(rng.integers(8, 400)), int(rng.integers(8, 300))) for _ in range(40)]
-    info = evam.PreProcInfo(range=(0.0, 1.0), mean=(0.1, 0.2, 0.3), std=(0.3, 0.2, 0.1))
-    shape = (len(rois), 3, 72, 72)
-    got, _ = run_hip(evam, torch, upload(evam, frames, gpu), shape, torch.float32, info,
-                     rois=[evam.Roi(*r) for r in rois])
-    ref, _ = run_oracle(O, coracle, frames, shape, "f32", info, rois=rois)
-    assert_same(got, ref, f"roi units {unit}")
-
-
 @pytest.mark.parametrize("tail", ["1", "2", "4", "7"])
 @pytest.mark.parametrize("dst", [(72, 72), (37, 29)])
 def test_roi_tail_split(evam, O, coracle, gpu, tail, dst, monkeypatch):
@@ -656,32 +616,6 @@ def test_roi_tail_split(evam, O, coracle, gpu, tail, dst, monkeypatch):
                      rois=[evam.Roi(*r) for r in rois])
     ref, _ = run_oracle(O, coracle, frames, shape, "f32", info, rois=rois)
     assert_same(got, ref, f"roi tail split {tail} {dst}")
-
-
-@pytest.mark.parametrize("fmt", FORMATS)
-@pytest.mark.parametrize("buf", ["0", "1024", "3072"])
-def test_roi_kernel_three_buffers(evam, O, coracle, gpu, fmt, buf, monkeypatch):
-    """ROI kernel with three staging buffers (EVAM_PP_ROI_NBUF=3: two groups of DMA in flight, counted
-    vmcnt waits). Small forced buffers (EVAM_PP_ROI_BUF) make every crop walk many row groups, so each
-    wait level of the pipeline (first group, second, steady state, last partial group) is exercised."""
-    import torch
-
-    monkeypatch.setenv("EVAM_PP_ROI_NBUF", "3")
-    if buf != "0":
-        monkeypatch.setenv("EVAM_PP_ROI_BUF", buf)
-    rng = np.random.default_rng(zlib.crc32(f"nb3{fmt}{buf}".encode()))
-    W, H = 400, 240
-    frames = [O.random_frame(rng, fc(O, fmt), W, H, pattern="gradient" if i else "uniform") for i in range(3)]
-    rois = [(int(rng.integers(0, 3)), int(rng.integers(-6, W - 8)), int(rng.integers(-6, H - 8)),
-             int(rng.integers(6, 390)), int(rng.integers(6, 230))) for _ in range(37)]
-    for dst, info in (((72, 72), evam.PreProcInfo(range=(0.0, 1.0), mean=(0.1, 0.2, 0.3), std=(0.3, 0.2, 0.1))),
-                      ((64, 40), evam.PreProcInfo(resize="aspect-ratio", placement="center", color_space="RGB",
-                                                  fill=(7, 8, 9), range=(0.0, 1.0)))):
-        shape = (len(rois), 3, dst[1], dst[0])
-        got, _ = run_hip(evam, torch, upload(evam, frames, gpu), shape, torch.float32, info,
-                         rois=[evam.Roi(*r) for r in rois])
-        ref, _ = run_oracle(O, coracle, frames, shape, "f32", info, rois=rois)
-        assert_same(got, ref, f"roi 3 buffers {fmt} buf={buf} dst={dst}")
 
 
 
