@@ -7,11 +7,13 @@
 # Steps:
 #   test              pytest -m gpu (one process)                      -> gpurun_out/pytest_gpu_TAG.log
 #   smoke             __graft_entry__.smoke()                          -> gpurun_out/smoke_TAG.txt
-#   driver            the driver's own bench command (C2, CPU baseline) -> gpurun_out/bench_TAG_driver.json
+#   driver[:N]        the driver's own bench command (C2, CPU baseline), N times -> gpurun_out/bench_TAG_driver[_k].json
+#   feed:c2,c4        bench.py --feed host (PCIe-inclusive) lines -> gpurun_out/bench_TAG_feed_<cfg>.json
 #   bench:c1,c2,...   one bench line per config (BENCH_STEPS, default 1000; CPU baseline unless CPU=0)
 #   prof:c1,c2,...    rocprofv3 --kernel-trace --stats per config (tools/prof_configs.sh, 200 steps)
 #   pmc:c2,c3,...     FETCH_SIZE / WRITE_SIZE passes per config (tools/pmc.sh) -> pmc_traffic_TAG_<cfg>.json
 #   valu:c1,...       SQ_INSTS_VALU pass per config (tools/pmc.sh)
+#   stall:c1,...      stall-attribution passes per config (tools/pmc.sh, two SQ groups)
 #   ab:CFG:SET1|SET2  same-box alternating env A/B (tools/gpu_env_ab.sh)
 #   dist              bench.py under torch.distributed.run, 2 ranks sharing the GPU over gloo
 #
@@ -40,9 +42,21 @@ for st in "$@"; do
         || { tail -20 "$OUT/smoke_$TAG.txt"; exit 1; }
       tail -1 "$OUT/smoke_$TAG.txt" ;;
     driver)
-      timeout -k 10 240 python3 bench.py --gpus 1 --steps 20 --warmup 5 > "$OUT/bench_${TAG}_driver.json" \
-        2> "$OUT/bench_${TAG}_driver.err" || { tail -20 "$OUT/bench_${TAG}_driver.err"; exit 1; }
-      tail -1 "$OUT/bench_${TAG}_driver.json" ;;
+      # driver[:N]: the driver's own command N times on this box (box variance next to the 780.7 k bar)
+      n=1; [ "$arg" != "$st" ] && n="$arg"
+      for k in $(seq 1 "$n"); do
+        sfx=""; [ "$n" -gt 1 ] && sfx="_$k"
+        timeout -k 10 240 python3 bench.py --gpus 1 --steps 20 --warmup 5 > "$OUT/bench_${TAG}_driver$sfx.json" \
+          2> "$OUT/bench_${TAG}_driver$sfx.err" || { tail -20 "$OUT/bench_${TAG}_driver$sfx.err"; exit 1; }
+        tail -1 "$OUT/bench_${TAG}_driver$sfx.json"
+      done ;;
+    feed)
+      # PCIe-inclusive lines: frames start in pinned host memory (f3 host feed, touched-rows plan)
+      for c in $cfgs; do
+        timeout -k 10 300 python3 bench.py --config "$c" --steps 300 --warmup 30 --feed host --no-cpu-baseline \
+          > "$OUT/bench_${TAG}_feed_$c.json" 2> "$OUT/bench_${TAG}_feed_$c.err" || { tail -20 "$OUT/bench_${TAG}_feed_$c.err"; exit 1; }
+        tail -1 "$OUT/bench_${TAG}_feed_$c.json"
+      done ;;
     bench)
       for c in $cfgs; do
         timeout -k 10 300 python3 bench.py --config "$c" --steps "${BENCH_STEPS:-1000}" --warmup 100 $CPUARG \
