@@ -2391,6 +2391,7 @@ struct QParams {
     int color_rgb;
     uint32_t fill;
     int prio;                 // progress-based priority (as the strip kernel's), over the quarters of the row groups
+    int rmax;                 // most output rows per row group (0: as many as the staging buffer and kRoiK allow)
 };
 
 
@@ -2541,6 +2542,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(96))) void
     const int QW = DW / PX;
     int R = rowb > 0 ? P.buf_bytes / rowb : rows;
     R = min(R, (KQ * kThreads) / QW);
+    if (P.rmax > 0) R = min(R, P.rmax);
     R = max(1, min(R, rows));
     const int offC = 2 * R * segY;
     const int nq = R * QW;                        // quads per full group
@@ -2837,6 +2839,8 @@ struct Knobs {
     int roi_sort = 0;  // 1: largest estimated bytes first before the stable sort by row groups (C3: equal or
                        // slower, profiles/r04k_ab_lines.txt; the units are ordered by row groups either way)
     int roi_tail = 4;                              // row tiles per ROI of the uneven tail over the CUs (1: no split)
+    int roi_rmax = 10;                             // ROI kernel: most output rows per row group (0: buffer / kRoiK bound);
+                                                   // C3 +1 % at 10 (profiles/r05j_c3_roi_rmax_ab.txt: 6 -4 %, 8 / 12 / 14 within noise)
     int strip = 1, strip_th = -1, strip_nw = -1, strip_px = 0;  // strip kernel: allowed (2: forced), rows per
                                                                 // tile, waves, px
     int strip_pair = 1;                            // strip kernel: paired-tap DMA where the footprints allow it
@@ -2865,7 +2869,7 @@ struct Knobs {
         reuse = env_int("EVAM_PP_REUSE", reuse); wave_lds = env_int("EVAM_PP_WAVE_LDS", wave_lds);
         roi_th = env_int("EVAM_PP_ROI_TH", roi_th); roi_buf = env_int("EVAM_PP_ROI_BUF", roi_buf);
         roi_px = env_int("EVAM_PP_ROI_PX", roi_px); roi_sort = env_int("EVAM_PP_ROI_SORT", roi_sort);
-        roi_tail = env_int("EVAM_PP_ROI_TAIL", roi_tail);
+        roi_tail = env_int("EVAM_PP_ROI_TAIL", roi_tail); roi_rmax = env_int("EVAM_PP_ROI_RMAX", roi_rmax);
     }
 };
 
@@ -4035,7 +4039,8 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
             const QParams& q = qp[f];
             const int base = qbase[f];
             const int pxr = kn.roi_px == 4 && DW % 4 == 0 ? 4 : 1;
-            const int rcap = std::max(1, ((kRoiK / pxr) * kThreads) / (DW / pxr));
+            int rcap = std::max(1, ((kRoiK / pxr) * kThreads) / (DW / pxr));
+            if (kn.roi_rmax > 0) rcap = std::min(rcap, kn.roi_rmax);
             std::vector<int>& un = h->sc_units;  // (item, row0, row1, cost) per unit
             un.clear();
             int maxcost = 1;
@@ -4167,6 +4172,7 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
             q.color_rgb = color_rgb;
             q.fill = fill;
             q.prio = kn.prio;
+            q.rmax = kn.roi_rmax;
             const int64_t grid = qrec[f];
             if (grid > 0x7FFFFFFF) return fail(EVAM_PP_ERR_INVALID_ARG, "evam_pp_run: too many tiles");
             hipError_t e = launch_roi(f, cfg->out_dtype, kn.roi_px, 2, q, (int)grid, qlds[f], h->stream);
