@@ -2087,6 +2087,7 @@ template <int FMT, int OUT, int PX>
 __global__ __launch_bounds__(256) void evam_pp_band(const TParams P) {
     __shared__ __attribute__((aligned(16))) float lut_s[OUT == 1 ? 768 : 4];
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    if (kAblate & 128) return;  // diagnostics: launch cost only
     static_assert(FMT == kNV12 || FMT == kI420, "4:2:0 sources");
     static_assert(PX == 1 || PX == 2 || PX == 4, "pixels per lane");
     constexpr int NPC = FMT == kI420 ? 2 : 1;  // chroma planes
@@ -2226,6 +2227,11 @@ __global__ __launch_bounds__(256) void evam_pp_band(const TParams P) {
         anyp |= xin && padc[j];
     }
     const bool anypad = __builtin_amdgcn_ballot_w64(anyp) != 0;
+    if (kAblate & 64) {  // diagnostics: prologue only (row / column coefficients, the first rows' DMA landed)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("" ::"v"(lY[0]), "v"(lC[0]), "v"(wp[0]), "v"(lb0), "v"(lb1), "v"((int)anypad));
+        return;
+    }
     const size_t esz = OUT == 1 ? 4 : 1;
     const uint32_t vo = (uint32_t)(xin ? X : 0) * (uint32_t)esz;
     const size_t plane = (size_t)p_DW * p_DH;
@@ -2320,6 +2326,14 @@ __global__ __launch_bounds__(256) void evam_pp_band(const TParams P) {
         }
 #endif
         const uint32_t wb0 = (uint32_t)__builtin_amdgcn_readlane(lb0, i), wb1 = (uint32_t)__builtin_amdgcn_readlane(lb1, i);
+        if (kAblate & 2) {  // diagnostics: no pixel math (no tap reads), stores and DMA kept
+            put_fill(vr0 + i);
+            pos += nst;
+            asm volatile("" ::: "memory");
+            if (i + 1 < n) issue_to(min(rhi, __builtin_amdgcn_readlane(lr1, i + 1) + ahead));
+            asm volatile("" ::: "memory");
+            continue;
+        }
         // HA <- row ra, HB <- row rb, reusing what the previous output row filtered (wave-uniform branches)
         if (ra != pa) {
             if (ra == pb) {

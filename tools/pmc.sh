@@ -1,6 +1,6 @@
 #!/bin/bash
 # PMC passes over the default bench (one counter group per rocprofv3 run, kernel-trace/stats only,
-# never combined with sys/runtime tracing). Output: gpurun_out/pmc_<tag>/<pass>/...counter_collection.csv
+# never combined with sys/runtime tracing). Per run at most 8 SQ_, 4 TCC_, 4 TCP_, 2 TA_, 2 TD_, 2 GRBM_ counters. Output: gpurun_out/pmc_<tag>/<pass>/...counter_collection.csv
 set -euo pipefail
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 OUT="$ROOT/gpurun_out/pmc_${1:-r01}"; mkdir -p "$OUT"
@@ -12,7 +12,8 @@ if [ -n "${PMC_GROUPS:-}" ]; then IFS=';' read -ra GROUPS_DEFAULT <<< "$PMC_GROU
 GROUPS_DEFAULT=("FETCH_SIZE" "WRITE_SIZE"
   "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM SQ_INSTS_VALU"
   "SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INST_LEVEL_VMEM SQ_INSTS_LDS SQ_INST_CYCLES_VMEM_RD SQ_INST_CYCLES_VMEM_WR SQ_VMEM_TA_ADDR_FIFO_FULL SQ_VMEM_TA_CMD_FIFO_FULL"
-  "TA_BUSY_avr TA_ADDR_STALLED_BY_TC_CYCLES_sum TA_DATA_STALLED_BY_TC_CYCLES_sum TA_TOTAL_WAVEFRONTS_sum"
+  "TA_BUSY_avr TA_ADDR_STALLED_BY_TC_CYCLES_sum"
+  "TA_DATA_STALLED_BY_TC_CYCLES_sum TA_TOTAL_WAVEFRONTS_sum"
   "TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCP_PENDING_STALL_CYCLES_sum TCP_TCC_READ_REQ_LATENCY_sum"
   "TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_TAG_STALL_sum"
   "GRBM_GUI_ACTIVE TCP_TCR_TCP_STALL_CYCLES_sum TCP_READ_TAGCONFLICT_STALL_CYCLES_sum TCP_TD_TCP_STALL_CYCLES_sum")
