@@ -328,7 +328,10 @@ def main():
     backend = os.environ.get("EVAM_BENCH_BACKEND", "nccl")
     if backend == "gloo":
         local = local % max(1, torch.cuda.device_count())
-    if world > 1:
+    # EVAM_BENCH_PG=1: a process group even for one rank, so a one-GPU box runs the RCCL reduction path
+    # (init, all_reduce MAX, all_gather on device tensors) that the driver's multi-GPU runs take
+    pg = world > 1 or os.environ.get("EVAM_BENCH_PG") == "1"
+    if pg:
         torch.cuda.set_device(local)
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
@@ -437,7 +440,7 @@ def main():
     stream = inflight_streams[0] if inflight else torch.cuda.current_stream(device)  # where pps[0] launches
     e0 = torch.cuda.Event(enable_timing=True)
     e1 = torch.cuda.Event(enable_timing=True)
-    if world > 1:
+    if pg:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -455,7 +458,7 @@ def main():
     t_submit = time.perf_counter() - t0  # host time to enqueue the K steps (≈ wall when host-bound)
     e1.record(stream)
     torch.cuda.synchronize()
-    if world > 1:
+    if pg:
         dist.barrier()
     wall = time.perf_counter() - t0
     kern_ms = e0.elapsed_time(e1) / (args.steps - ev_from)  # one launch per step
@@ -521,7 +524,7 @@ def main():
                     "mean_launch_ms": round(res_ms, 5), "steps": args.resident_steps,
                     "set_bytes": in_bytes + out_n * 3 * DH * DW * esz}
     tot = evam.streams.reduce_run(wall, n * args.steps, alg_bytes * args.steps,
-                                  device=device if world > 1 and backend == "nccl" else None,
+                                  device=device if pg and backend == "nccl" else None,
                                   device_key=evam.streams.device_key(local))
     wall_max = tot.elapsed_max_s
     value = tot.frames / wall_max
@@ -537,7 +540,7 @@ def main():
             "unit": "frames/s",
             # RCCL: one rank per GPU by construction (it refuses two ranks on one device); a gloo rehearsal may put
             # several ranks on one GPU, counted once by device_key
-            "n_gpus": world if (world > 1 and backend == "nccl") else tot.devices,
+            "n_gpus": world if (pg and backend == "nccl") else tot.devices,
             "ranks": world,
             "steps": args.steps,
             "warmup": args.warmup,
@@ -592,7 +595,7 @@ def main():
         print(json.dumps(res), flush=True)
     for h in pps:
         h.close()
-    if world > 1:
+    if pg:
         dist.destroy_process_group()
 
 

@@ -73,3 +73,19 @@ def test_two_ranks_match_single_process(gpu, tmp_path, config):
     if ring > 1:  # slots no step wrote keep their initial value; slots 0 and 1 were written
         r = by_stream[0]
         assert (r[5] == 7.0).all() and not (r[0] == 7.0).all() and not (r[1] == 7.0).all()
+
+
+def test_bench_rccl_reduction_path_one_rank(gpu, tmp_path):
+    """bench.py's multi-GPU reduction on RCCL (backend "nccl": init_process_group with the device, barrier, all_reduce MAX
+    of the elapsed time, all_gather of the per-rank totals on device tensors), run as one rank on this one-GPU box
+    (EVAM_BENCH_PG=1): the path the driver's 2/4/8-GPU runs take, short of the inter-GPU transport."""
+    port = _free_port()
+    env = dict(os.environ, RANK="0", LOCAL_RANK="0", WORLD_SIZE="1", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+               EVAM_BENCH_PG="1")
+    env.pop("EVAM_BENCH_BACKEND", None)
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--steps", "10", "--warmup", "3",
+                        "--no-cpu-baseline", "--resident-steps", "0"], env=env, capture_output=True, text=True,
+                       timeout=240)
+    assert p.returncode == 0, p.stderr[-2000:]
+    d = json.loads(p.stdout.strip().splitlines()[-1])
+    assert d["n_gpus"] == 1 and d["ranks"] == 1 and d["value"] > 0
