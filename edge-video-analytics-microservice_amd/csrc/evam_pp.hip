@@ -2405,7 +2405,6 @@ struct QParams {
     int color_rgb;
     uint32_t fill;
     int prio;                 // progress-based priority (as the strip kernel's), over the quarters of the row groups
-    int rmax;                 // most output rows per row group (0: as many as the staging buffer and kRoiK allow)
 };
 
 
@@ -2556,7 +2555,6 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(96))) void
     const int QW = DW / PX;
     int R = rowb > 0 ? P.buf_bytes / rowb : rows;
     R = min(R, (KQ * kThreads) / QW);
-    if (P.rmax > 0) R = min(R, P.rmax);
     R = max(1, min(R, rows));
     const int offC = 2 * R * segY;
     const int nq = R * QW;                        // quads per full group
@@ -2849,12 +2847,10 @@ struct Knobs {
     int nsegx = 0;                                 // staged tile width in 64-column segments (0: widest that fits)
     int stage_r = -1;                              // staged pipeline: rows per group
     int wth = -1, px = 0, reuse = 1, wave_lds = 40 * 1024;
-    int roi_th = -1, roi_buf = -1, roi_px = 1;     // roi_buf -1: sized for one round
+    int roi_th = -1, roi_buf = -1, roi_px = 2;     // roi_buf -1: sized for one round; pixels per lane (1 for odd DW)
     int roi_sort = 0;  // 1: largest estimated bytes first before the stable sort by row groups (C3: equal or
                        // slower, profiles/r04k_ab_lines.txt; the units are ordered by row groups either way)
     int roi_tail = 4;                              // row tiles per ROI of the uneven tail over the CUs (1: no split)
-    int roi_rmax = 10;                             // ROI kernel: most output rows per row group (0: buffer / kRoiK bound);
-                                                   // C3 +1 % at 10 (profiles/r05j_c3_roi_rmax_ab.txt: 6 -4 %, 8 / 12 / 14 within noise)
     int strip = 1, strip_th = -1, strip_nw = -1, strip_px = 0;  // strip kernel: allowed (2: forced), rows per
                                                                 // tile, waves, px
     int strip_pair = 1;                            // strip kernel: paired-tap DMA where the footprints allow it
@@ -2883,7 +2879,7 @@ struct Knobs {
         reuse = env_int("EVAM_PP_REUSE", reuse); wave_lds = env_int("EVAM_PP_WAVE_LDS", wave_lds);
         roi_th = env_int("EVAM_PP_ROI_TH", roi_th); roi_buf = env_int("EVAM_PP_ROI_BUF", roi_buf);
         roi_px = env_int("EVAM_PP_ROI_PX", roi_px); roi_sort = env_int("EVAM_PP_ROI_SORT", roi_sort);
-        roi_tail = env_int("EVAM_PP_ROI_TAIL", roi_tail); roi_rmax = env_int("EVAM_PP_ROI_RMAX", roi_rmax);
+        roi_tail = env_int("EVAM_PP_ROI_TAIL", roi_tail);
     }
 };
 
@@ -3046,14 +3042,15 @@ hipError_t launch_roi_px(const QParams& p, int grid, int lds, hipStream_t s) {
     return hipGetLastError();
 }
 
-// PX = 1 (adjacent lanes, adjacent pixels) by default. PX = 4 (one dwordx4 store per channel and
-// one row setup per 4 pixels; EVAM_PP_ROI_PX=4) measured 8 % slower on C3: lanes 4 pixels apart
-// spread their LDS tap reads over 4x more dwords, so the byte reads bank-conflict.
+// PX = 2 adjacent pixels per lane by default (round 5; 1 for odd output widths): one dwordx2 store per channel and
+// one row setup per 2 pixels, C3 +3.7 % over PX = 1 on one box (profiles/r05p_c3_roi_px_rmax_ab.txt; PX = 4 equals
+// PX = 1 there, round 2 measured it 8 % slower: lanes 4 pixels apart spread their LDS tap reads over more dwords).
 // (Three staging buffers, EVAM_PP_ROI_NBUF=3, measured neutral or slower for two rounds: retired in round 5.)
 template <int FMT, int OUT>
 hipError_t launch_roi_t(int px, int nb, const QParams& p, int grid, int lds, hipStream_t s) {
     (void)nb;
     if (px == 4 && p.DW % 4 == 0) return launch_roi_px<FMT, OUT, 4, 2>(p, grid, lds, s);
+    if (px == 2 && p.DW % 2 == 0) return launch_roi_px<FMT, OUT, 2, 2>(p, grid, lds, s);
     return launch_roi_px<FMT, OUT, 1, 2>(p, grid, lds, s);
 }
 
@@ -3457,7 +3454,8 @@ hipError_t launch_band(int f, int out, int px, const TParams& p, dim3 grid, int 
 template <int FMT, int OUT>
 const void* roi_fn_t(int px, int nb) {
     (void)nb;
-    return px == 4 ? (const void*)evam_pp_roi<FMT, OUT, 4, 2> : (const void*)evam_pp_roi<FMT, OUT, 1, 2>;
+    return px == 4 ? (const void*)evam_pp_roi<FMT, OUT, 4, 2>
+         : px == 2 ? (const void*)evam_pp_roi<FMT, OUT, 2, 2> : (const void*)evam_pp_roi<FMT, OUT, 1, 2>;
 }
 const void* roi_fn(int f, int out, int px, int nb) {
     switch (f * 2 + out) {
@@ -3497,7 +3495,7 @@ bool plan_roi(int f, int DW, int DH, int out_dtype, int px, int max_row_bytes, i
     q.offBuf = q.offYT + (int)sizeof(YTab) * q.TH;
     const int64_t grid = (int64_t)count * base_tiles;
     const int per_cu = (int)std::max<int64_t>(1, std::min<int64_t>(kRoiWavesPerSimd, (grid + n_cu - 1) / n_cu));
-    const int pxv = px == 4 && DW % 4 == 0 ? 4 : 1;
+    const int pxv = (px == 4 || px == 2) && DW % px == 0 ? px : 1;
     const int nb = 2;
     int buf = kn.roi_buf;
     if (buf <= 0) buf = std::min(12 * 1024, ((((160 * 1024) / per_cu) & ~1023) - q.offBuf) / nb & ~15);
@@ -4052,9 +4050,8 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
             // two rounds and were retired in round 5.)
             const QParams& q = qp[f];
             const int base = qbase[f];
-            const int pxr = kn.roi_px == 4 && DW % 4 == 0 ? 4 : 1;
-            int rcap = std::max(1, ((kRoiK / pxr) * kThreads) / (DW / pxr));
-            if (kn.roi_rmax > 0) rcap = std::min(rcap, kn.roi_rmax);
+            const int pxr = (kn.roi_px == 4 || kn.roi_px == 2) && DW % kn.roi_px == 0 ? kn.roi_px : 1;
+            const int rcap = std::max(1, ((kRoiK / pxr) * kThreads) / (DW / pxr));
             std::vector<int>& un = h->sc_units;  // (item, row0, row1, cost) per unit
             un.clear();
             int maxcost = 1;
@@ -4186,7 +4183,6 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
             q.color_rgb = color_rgb;
             q.fill = fill;
             q.prio = kn.prio;
-            q.rmax = kn.roi_rmax;
             const int64_t grid = qrec[f];
             if (grid > 0x7FFFFFFF) return fail(EVAM_PP_ERR_INVALID_ARG, "evam_pp_run: too many tiles");
             hipError_t e = launch_roi(f, cfg->out_dtype, kn.roi_px, 2, q, (int)grid, qlds[f], h->stream);

@@ -448,13 +448,15 @@ def test_stream_switch_and_descriptor_churn(evam, O, coracle, gpu):
     pp.close()
 
 
+@pytest.mark.parametrize("px", ["4", "2"])
 @pytest.mark.parametrize("fmt", FORMATS)
-@pytest.mark.parametrize("dst,dtype", [((72, 72), "f32"), ((64, 36), "u8")])
-def test_roi_kernel_px4(evam, O, coracle, gpu, fmt, dst, dtype, monkeypatch):
-    """The ROI kernel's 4-pixels-per-lane variant (EVAM_PP_ROI_PX=4) on a ROI batch."""
+@pytest.mark.parametrize("dst,dtype", [((72, 72), "f32"), ((64, 36), "u8"), ((45, 30), "f32")])
+def test_roi_kernel_px4(evam, O, coracle, gpu, fmt, dst, dtype, px, monkeypatch):
+    """The ROI kernel's 4- and 2-pixels-per-lane variants (EVAM_PP_ROI_PX) on a ROI batch (an odd output width falls
+    back to one pixel per lane)."""
     import torch
 
-    monkeypatch.setenv("EVAM_PP_ROI_PX", "4")
+    monkeypatch.setenv("EVAM_PP_ROI_PX", px)
     rng = np.random.default_rng(zlib.crc32(f"px4{fmt}{dst}".encode()))
     W, H = 320, 200
     frames = [O.random_frame(rng, fc(O, fmt), W, H, pattern="gradient" if i else "uniform") for i in range(2)]
@@ -468,7 +470,7 @@ def test_roi_kernel_px4(evam, O, coracle, gpu, fmt, dst, dtype, monkeypatch):
     got, _ = run_hip(evam, torch, upload(evam, frames, gpu), shape,
                      torch.float32 if dtype == "f32" else torch.uint8, info, rois=[evam.Roi(*r) for r in rois])
     ref, _ = run_oracle(O, coracle, frames, shape, dtype, info, rois=rois)
-    assert_same(got, ref, f"roi px4 {fmt} {dst} {dtype}")
+    assert_same(got, ref, f"roi px{px} {fmt} {dst} {dtype}")
 
 
 @pytest.mark.parametrize("fmt", FORMATS)
