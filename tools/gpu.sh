@@ -9,6 +9,7 @@
 #   smoke             __graft_entry__.smoke()                          -> gpurun_out/smoke_TAG.txt
 #   driver[:N]        the driver's own bench command (C2, CPU baseline), N times -> gpurun_out/bench_TAG_driver[_k].json
 #   feed:c2,c4        bench.py --feed host (PCIe-inclusive) lines -> gpurun_out/bench_TAG_feed_<cfg>.json
+#   pipe              bench.py --via pipeline (C2 through PipelineServer) + its own rocprof kernel stats
 #   bench:c1,c2,...   one bench line per config (BENCH_STEPS, default 1000; CPU baseline unless CPU=0)
 #   prof:c1,c2,...    rocprofv3 --kernel-trace --stats per config (tools/prof_configs.sh, 200 steps)
 #   pmc:c2,c3,...     FETCH_SIZE / WRITE_SIZE passes per config (tools/pmc.sh) -> pmc_traffic_TAG_<cfg>.json
@@ -57,6 +58,12 @@ for st in "$@"; do
           > "$OUT/bench_${TAG}_feed_$c.json" 2> "$OUT/bench_${TAG}_feed_$c.err" || { tail -20 "$OUT/bench_${TAG}_feed_$c.err"; exit 1; }
         tail -1 "$OUT/bench_${TAG}_feed_$c.json"
       done ;;
+    pipe)
+      # C2 frames through PipelineServer (device runner, 256-frame hub launches, null detector): a throughput line
+      timeout -k 10 300 python3 bench.py --via pipeline --steps 400 --warmup 40 --hub-batch 256 \
+        > "$OUT/bench_${TAG}_pipeline.json" 2> "$OUT/bench_${TAG}_pipeline.err" || { tail -20 "$OUT/bench_${TAG}_pipeline.err"; exit 1; }
+      tail -1 "$OUT/bench_${TAG}_pipeline.json"
+      PROF_ARGS="--via pipeline --hub-batch 256" STEPS=200 bash tools/prof_configs.sh "${TAG}_pipeline" c2 ;;
     bench)
       for c in $cfgs; do
         timeout -k 10 300 python3 bench.py --config "$c" --steps "${BENCH_STEPS:-1000}" --warmup 100 $CPUARG \

@@ -11,7 +11,7 @@ cd /tmp
 for c in $CFGS; do
   echo "[prof] $c"; date
   timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_${TAG}_$c" -o run -- \
-    python3 "$ROOT/bench.py" --config "$c" --steps ${STEPS:-200} --warmup 50 --no-cpu-baseline --resident-steps 0 \
+    python3 "$ROOT/bench.py" --config "$c" --steps ${STEPS:-200} --warmup 50 --no-cpu-baseline --resident-steps 0 ${PROF_ARGS:-} \
     > "$OUT/prof_${TAG}_$c.json" 2> "$OUT/prof_${TAG}_$c.err" || { tail -20 "$OUT/prof_${TAG}_$c.err"; exit 1; }
   python3 - "$OUT/prof_${TAG}_$c" "$OUT/prof_${TAG}_$c.json" "$c" <<'EOF' | tee -a "$OUT/prof_$TAG.txt"
 import csv, glob, json, sys
@@ -21,10 +21,11 @@ for f in glob.glob(d + "/**/*kernel_stats.csv", recursive=True):
     for r in csv.DictReader(open(f)):
         if "evam_pp" in r["Name"]:
             avg_us = float(r["AverageNs"]) / 1e3
-            ab = b["roofline"]["algorithmic_bytes_per_launch"]
-            print(f"{c}: kernel {r['Name'][:60]} calls {r['Calls']} avg {avg_us:.2f} us "
-                  f"({ab / avg_us / 1e3:.0f} GB/s alg) | bench step {b['ms_per_step'] * 1e3:.2f} us, "
-                  f"value {b['value']}, event-based {b['roofline']['achieved']} GB/s")
+            ab = b.get("roofline", {}).get("algorithmic_bytes_per_launch")
+            rate = f" ({ab / avg_us / 1e3:.0f} GB/s alg)" if ab else ""
+            tail = (f" | bench step {b['ms_per_step'] * 1e3:.2f} us, value {b['value']}, event-based "
+                    f"{b['roofline']['achieved']} GB/s" if "ms_per_step" in b else f" | value {b['value']}")
+            print(f"{c}: kernel {r['Name'][:60]} calls {r['Calls']} avg {avg_us:.2f} us{rate}{tail}")
 EOF
 done
 echo "[prof] done"; date
