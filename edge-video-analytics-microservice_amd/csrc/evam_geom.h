@@ -235,6 +235,30 @@ inline void build_tables_into(const Geom& g, int DW, int DH, XTab* x, YTab* y) {
     }
 }
 
+// Six-column lanes (band kernel, 4 pixels per lane): every lane with a visible pixel has four, and their taps read
+// six source columns c0..c5 as pixel 0 (c0, c1), 1 (c1, c2), 2 (c3, c4), 3 (c4, c5), with c0 / c1, c2 / c3 and
+// c4 / c5 in one chroma column each. A 3:2 horizontal scale (C1: 768 -> 512) has this shape on every lane, so a lane
+// converts 6 luma samples and 3 chroma samples per source row instead of 8 and 8. Crop origins are even for 4:2:0
+// (roi_clip), so the chroma column of crop-relative column s is x0 / 2 + s / 2 on every item.
+inline bool band_six_columns(const XTab* xt, int DW, uint32_t x0_mask) {
+    if (DW % 4 || (x0_mask & 0xAAAAAAAAu)) return false;
+    for (int X = 0; X < DW; X += 4) {
+        const XTab* e = xt + X;
+        bool vis[4], any = false, all = true;
+        for (int j = 0; j < 4; j++) {
+            vis[j] = (e[j].a0 | e[j].a1) != 0;
+            any |= vis[j];
+            all &= vis[j];
+        }
+        if (!any) continue;
+        if (!all) return false;
+        if (e[0].s1 != e[1].s0 || e[2].s1 != e[3].s0) return false;
+        if ((e[0].s0 >> 1) != (e[0].s1 >> 1) || (e[1].s1 >> 1) != (e[2].s0 >> 1) || (e[2].s1 >> 1) != (e[3].s1 >> 1))
+            return false;
+    }
+    return true;
+}
+
 // ROI launch order: largest estimated work first (counting sort on 64 buckets of crop width x touched
 // rows, stable within a bucket). idx: the group's item indices; bucket: scratch indexed by item index.
 inline void roi_largest_first(const int* idx, int n, const Geom* geo, int DH, bool sort, int* bucket,

@@ -485,13 +485,15 @@ __device__ __forceinline__ UVs uv_terms_sat(uint32_t U, uint32_t V) {
 __device__ __forceinline__ uint32_t luma_term(uint32_t Y) { return __umul24(max(Y, 16u), (uint32_t)kCY); }
 // One source row, one channel: taps' sums s0 (column x0) and s1 (column x1), packed weights w = a0 | a1 << 16
 // (plain 11-bit) -> 16 * (c0 * a0 + c1 * a1).
-__device__ __forceinline__ uint32_t hpass_sat(uint32_t y0, uint32_t t0, uint32_t y1, uint32_t t1, uint32_t w) {
-    const uint32_t s0 = __builtin_elementwise_add_sat(y0, t0);
-    const uint32_t s1 = __builtin_elementwise_add_sat(y1, t1);
+// hpass_sums: the same from the taps' saturated sums (pixels whose taps meet at one column share a sum).
+__device__ __forceinline__ uint32_t hpass_sums(uint32_t s0, uint32_t s1, uint32_t w) {
     const evam_u16x2 h = __builtin_bit_cast(evam_u16x2, __builtin_amdgcn_perm(s1, s0, 0x07060302u));
     const evam_u16x2 c = __builtin_elementwise_sub_sat(h, (evam_u16x2){61440, 61440});
     const uint32_t c16 = __builtin_bit_cast(uint32_t, c) & 0xFFF0FFF0u;
     return __builtin_amdgcn_udot2(__builtin_bit_cast(evam_u16x2, c16), __builtin_bit_cast(evam_u16x2, w), 0u, false);
+}
+__device__ __forceinline__ uint32_t hpass_sat(uint32_t y0, uint32_t t0, uint32_t y1, uint32_t t1, uint32_t w) {
+    return hpass_sums(__builtin_elementwise_add_sat(y0, t0), __builtin_elementwise_add_sat(y1, t1), w);
 }
 
 // Horizontal pass of one source row, three channels, from the two taps' luma bytes and chroma terms.
@@ -2080,16 +2082,20 @@ __device__ __forceinline__ void vmcnt_le(int n) {
 //    terms per chroma row, so a source row is converted and filtered once however many output rows read
 //    it (~0.84 source rows per output row at 432 -> 512);
 //  * coefficients of the strip's columns (per lane) and of the band's rows (one per lane, v_readlane)
-//    come from the kernels' shared linear_coef: no table loads;
+//    come from the kernels' shared linear_coef: no table loads (the host's column table loaded at entry instead
+//    was 1.5 % slower on C1: the per-pixel setup then waits for the load, profiles/r05t_c1_band_table_dd_ab.txt);
+//  * DD (six-column lanes, band_six_columns): a lane's 4 pixels read 6 source columns and 3 chroma columns, so a
+//    source row costs 6 luma and 18 saturating sums instead of 8 and 24, a chroma row 3 conversions instead of 8;
 //  * each channel of a row leaves as one PX-wide store per lane.
 // Workgroups of up to four waves: the strips of one band of one item.
-template <int FMT, int OUT, int PX>
+template <int FMT, int OUT, int PX, int DD>
 __global__ __launch_bounds__(256) void evam_pp_band(const TParams P) {
     __shared__ __attribute__((aligned(16))) float lut_s[OUT == 1 ? 768 : 4];
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     if (kAblate & 128) return;  // diagnostics: launch cost only
     static_assert(FMT == kNV12 || FMT == kI420, "4:2:0 sources");
     static_assert(PX == 1 || PX == 2 || PX == 4, "pixels per lane");
+    static_assert(!DD || PX == 4, "six-column lanes hold 4 pixels");
     constexpr int NPC = FMT == kI420 ? 2 : 1;  // chroma planes
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -2278,6 +2284,16 @@ __global__ __launch_bounds__(256) void evam_pp_band(const TParams P) {
     int cc = -1;
     auto chroma_row = [&](int c) {
         const uint8_t* cb = cbuf + (c - clo) * segC;
+        cc = c;
+        if constexpr (DD) {  // the chroma columns of (c0, c1), (c2, c3), (c4, c5) in tA[0..2]
+            const uint32_t o[3] = {lC[0] & 0xFFFF, lC[1] >> 16, lC[2] >> 16};
+#pragma unroll
+            for (int k = 0; k < 3; k++) {
+                const uint8_t* a = cb + o[k];
+                tA[k] = uvt(a[0], FMT == kNV12 ? a[1] : a[segC / 2]);
+            }
+            return;
+        }
 #pragma unroll
         for (int j = 0; j < PX; j++) {
             const uint8_t* a0 = cb + (lC[j] & 0xFFFF);
@@ -2290,13 +2306,30 @@ __global__ __launch_bounds__(256) void evam_pp_band(const TParams P) {
                 tB[j] = uvt(a1[0], a1[segC / 2]);
             }
         }
-        cc = c;
     };
     // horizontal pass of source row r (crop-relative) into H
     auto hrow = [&](int r, uint32_t (&H)[PX][3]) {
         const int c = (y0 + r) >> 1;
         if (c != cc) chroma_row(c);
         const uint8_t* yb = wbuf + (r - rlo) * segY;
+        if constexpr (DD) {  // columns c0..c5: pixel 0 (c0, c1), 1 (c1, c2), 2 (c3, c4), 3 (c4, c5)
+            const uint32_t yl[6] = {luma_term(yb[lY[0] & 0xFFFF]), luma_term(yb[lY[0] >> 16]), luma_term(yb[lY[1] >> 16]),
+                                    luma_term(yb[lY[2] & 0xFFFF]), luma_term(yb[lY[2] >> 16]), luma_term(yb[lY[3] >> 16])};
+#pragma unroll
+            for (int ch3 = 0; ch3 < 3; ch3++) {
+                uint32_t sm[6];
+#pragma unroll
+                for (int k = 0; k < 6; k++) {
+                    const UVs& t = tA[k >> 1];
+                    sm[k] = __builtin_elementwise_add_sat(yl[k], ch3 == 0 ? t.b : (ch3 == 1 ? t.g : t.r));
+                }
+                H[0][ch3] = hpass_sums(sm[0], sm[1], wp[0]) & kVMask;
+                H[1][ch3] = hpass_sums(sm[1], sm[2], wp[1]) & kVMask;
+                H[2][ch3] = hpass_sums(sm[3], sm[4], wp[2]) & kVMask;
+                H[3][ch3] = hpass_sums(sm[4], sm[5], wp[3]) & kVMask;
+            }
+            return;
+        }
 #pragma unroll
         for (int j = 0; j < PX; j++) {
             const uint32_t yA = luma_term(yb[lY[j] & 0xFFFF]), yB = luma_term(yb[lY[j] >> 16]);
@@ -2856,6 +2889,7 @@ struct Knobs {
     int strip_pair = 1;                            // strip kernel: paired-tap DMA where the footprints allow it
     int strip_waves = 16;                          // strip / band kernels: resident waves per CU the tiles are sized for
     int band = 1, band_px = 0;                     // band kernel: allowed (2: forced), pixels per lane
+    int band_dd = 1;                               // band kernel: six-column lanes where the column table allows
     int prio = 1;                                  // progress-based wave priority (strip, band, ROI kernels): C2 +3 %,
                                                    // C4 +3 %, C5 +3-5 %, C1 +9 % (profiles/r04k_ab_lines.txt)
     int band_ahead = 2;                            // band kernel: source rows issued ahead of the current output row's
@@ -2866,6 +2900,7 @@ struct Knobs {
         prio = env_int("EVAM_PP_PRIO", prio);
         band_ahead = env_int("EVAM_PP_BAND_AHEAD", band_ahead);
         band = env_int("EVAM_PP_BAND", band); band_px = env_int("EVAM_PP_BAND_PX", band_px);
+        band_dd = env_int("EVAM_PP_BAND_DD", band_dd);
         strip = env_int("EVAM_PP_STRIP", strip); strip_th = env_int("EVAM_PP_STRIP_TH", strip_th);
         strip_waves = env_int("EVAM_PP_STRIP_WAVES", strip_waves);
         strip_pair = env_int("EVAM_PP_STRIP_PAIR", strip_pair); strip_nw = env_int("EVAM_PP_STRIP_NW", strip_nw);
@@ -3335,20 +3370,6 @@ hipError_t launch_strip(int f, int out, int pr, int px, const TParams& p, dim3 g
     }
 }
 
-template <int FMT, int OUT>
-const void* band_fn_t(int px) {
-    return px == 4 ? (const void*)evam_pp_band<FMT, OUT, 4>
-         : px == 2 ? (const void*)evam_pp_band<FMT, OUT, 2> : (const void*)evam_pp_band<FMT, OUT, 1>;
-}
-const void* band_fn(int f, int out, int px) {
-    switch (f * 2 + out) {
-    case kNV12 * 2 + 0: return band_fn_t<kNV12, 0>(px);
-    case kNV12 * 2 + 1: return band_fn_t<kNV12, 1>(px);
-    case kI420 * 2 + 0: return band_fn_t<kI420, 0>(px);
-    default: return band_fn_t<kI420, 1>(px);
-    }
-}
-
 // Band-kernel plan for a uniform 4:2:0 group whose consecutive output rows share source rows (vertical
 // upscales, C1). Fills the geometry, strips, bands and LDS fields of TParams (not items, LUT, output,
 // colour).
@@ -3361,7 +3382,7 @@ const void* band_fn(int f, int out, int px) {
 // Returns false for geometries it does not suit (fewer than 1 in 8 rows sharing source rows, footprints
 // over 1 KB, outputs wider than kMaxStrips strips).
 bool plan_band(int f, const Geom& g, int DW, int DH, int count, int out_dtype, int n_cu, const XTab* xt,
-               const YTab* yt, uint32_t x0_mask, const Knobs& kn, TParams& p, int& px, int& nw, int& lds) {
+               const YTab* yt, uint32_t x0_mask, const Knobs& kn, TParams& p, int& px, bool& dd, int& nw, int& lds) {
     if (f != kNV12 && f != kI420) return false;
     int shared = 0, vis = 0;
     for (int Y = 0; Y + 1 < DH; Y++) {
@@ -3431,23 +3452,25 @@ bool plan_band(int f, const Geom& g, int DW, int DH, int count, int out_dtype, i
         const int Xv0 = std::max(s * sw, g.ox), Xv1 = std::min(std::min(s * sw + sw, DW), g.ox + g.rw) - 1;
         p.sfoot[k] = w < nw && s < nstrips && Xv0 <= Xv1 ? int2{xt[Xv0].s0, xt[Xv1].s1} : int2{-1, -1};
     }
+    dd = px == 4 && kn.band_dd && band_six_columns(xt, DW, x0_mask);
     return (int64_t)per_launch * p.tiles_per_item <= 0x7FFFFFFF;
 }
 
 template <int FMT, int OUT>
-hipError_t launch_band_t(int px, const TParams& p, dim3 grid, int nw, int lds, hipStream_t s) {
+hipError_t launch_band_t(int px, bool dd, const TParams& p, dim3 grid, int nw, int lds, hipStream_t s) {
     const dim3 blk(64 * nw);
-    if (px == 4) hipLaunchKernelGGL((evam_pp_band<FMT, OUT, 4>), grid, blk, lds, s, p);
-    else if (px == 2) hipLaunchKernelGGL((evam_pp_band<FMT, OUT, 2>), grid, blk, lds, s, p);
-    else hipLaunchKernelGGL((evam_pp_band<FMT, OUT, 1>), grid, blk, lds, s, p);
+    if (px == 4 && dd) hipLaunchKernelGGL((evam_pp_band<FMT, OUT, 4, 1>), grid, blk, lds, s, p);
+    else if (px == 4) hipLaunchKernelGGL((evam_pp_band<FMT, OUT, 4, 0>), grid, blk, lds, s, p);
+    else if (px == 2) hipLaunchKernelGGL((evam_pp_band<FMT, OUT, 2, 0>), grid, blk, lds, s, p);
+    else hipLaunchKernelGGL((evam_pp_band<FMT, OUT, 1, 0>), grid, blk, lds, s, p);
     return hipGetLastError();
 }
-hipError_t launch_band(int f, int out, int px, const TParams& p, dim3 grid, int nw, int lds, hipStream_t s) {
+hipError_t launch_band(int f, int out, int px, bool dd, const TParams& p, dim3 grid, int nw, int lds, hipStream_t s) {
     switch (f * 2 + out) {
-    case kNV12 * 2 + 0: return launch_band_t<kNV12, 0>(px, p, grid, nw, lds, s);
-    case kNV12 * 2 + 1: return launch_band_t<kNV12, 1>(px, p, grid, nw, lds, s);
-    case kI420 * 2 + 0: return launch_band_t<kI420, 0>(px, p, grid, nw, lds, s);
-    default: return launch_band_t<kI420, 1>(px, p, grid, nw, lds, s);
+    case kNV12 * 2 + 0: return launch_band_t<kNV12, 0>(px, dd, p, grid, nw, lds, s);
+    case kNV12 * 2 + 1: return launch_band_t<kNV12, 1>(px, dd, p, grid, nw, lds, s);
+    case kI420 * 2 + 0: return launch_band_t<kI420, 0>(px, dd, p, grid, nw, lds, s);
+    default: return launch_band_t<kI420, 1>(px, dd, p, grid, nw, lds, s);
     }
 }
 
@@ -4236,9 +4259,10 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
             if (kn.band && kn.wave != 2 && kn.strip != 2) {
                 TParams* tp = &h->sc_tparams;
                 int bpx = 0, nw = 0, lds = 0;
+                bool dd = false;
                 const XTab* hx = reinterpret_cast<const XTab*>(h->h_block.data() + tab_off[f]);
                 if (plan_band(f, g0, DW, DH, count[f], cfg->out_dtype, h->n_cu, hx, reinterpret_cast<const YTab*>(hx + DW),
-                              x0_mask[f], kn, *tp, bpx, nw, lds)) {
+                              x0_mask[f], kn, *tp, bpx, dd, nw, lds)) {
                     tp->lut = lut_d;
                     tp->dst = dst->data;
                     tp->slot_offset = dst->slot_offset;
@@ -4252,7 +4276,7 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
                         fill_args(tp->items, m0, nm);
                         tp->units = nm * tp->tiles_per_item;
                         const dim3 gr((unsigned)tp->tiles_x, (unsigned)((DH + tp->TH - 1) / tp->TH), (unsigned)nm);
-                        hipError_t e = launch_band(f, cfg->out_dtype, bpx, *tp, gr, nw, lds, h->stream);
+                        hipError_t e = launch_band(f, cfg->out_dtype, bpx, dd, *tp, gr, nw, lds, h->stream);
                         if (e != hipSuccess) return fail(EVAM_PP_ERR_HIP, "kernel launch failed: %s", hipGetErrorString(e));
                         launches++; kmask |= EVAM_KERNEL_BAND;
                     }

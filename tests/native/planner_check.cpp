@@ -340,7 +340,54 @@ static void check_clip_simd() {
 
 
 
+// band_six_columns admits a column table only if the band kernel's six-column lanes (DD) read, for every visible
+// pixel, the luma and chroma columns the per-pixel taps name: px 0 (c0, c1), 1 (c1, c2), 2 (c3, c4), 3 (c4, c5),
+// chroma of c0 / c1 from c0, of c2 / c3 from c2, of c4 / c5 from c4, for every even crop origin.
+static void check_six_columns() {
+    int admitted = 0, c1_ok = 0;
+    for (int it = 0; it < 4000; it++) {
+        Geom g{};
+        const int DW = it == 0 ? 512 : 4 * uni(1, 200);
+        g.cw = it == 0 ? 768 : (it % 3 == 0 ? 3 * uni(1, 300) : uni(2, 2000));
+        g.rw = it == 0 ? DW : (it % 3 == 0 ? std::min(DW, 2 * (g.cw / 3)) : uni(1, DW));
+        if (g.rw < 1) g.rw = 1;
+        g.ox = it % 5 == 0 ? 4 * uni(0, (DW - g.rw) / 4) : uni(0, DW - g.rw);
+        g.ch = g.rh = 8;
+        std::vector<XTab> xt(DW);
+        std::vector<YTab> yt(8);
+        build_tables_into(g, DW, 8, xt.data(), yt.data());
+        const uint32_t x0_mask = it % 7 == 1 ? 0x6u : 0x1u;  // origins 1, 2 (odd: never admitted) or 0
+        const bool ok = band_six_columns(xt.data(), DW, x0_mask);
+        if (x0_mask & 0xAAAAAAAAu) CHECK(!ok, "odd crop origin admitted");
+        if (it == 0) c1_ok = ok;
+        if (!ok) continue;
+        admitted++;
+        for (int X = 0; X < DW; X += 4) {
+            const XTab* e = &xt[X];
+            if (!((e[0].a0 | e[0].a1) || (e[1].a0 | e[1].a1) || (e[2].a0 | e[2].a1) || (e[3].a0 | e[3].a1))) continue;
+            const int c[6] = {e[0].s0, e[0].s1, e[1].s1, e[2].s0, e[2].s1, e[3].s1};
+            const int tap[4][2] = {{0, 1}, {1, 2}, {3, 4}, {4, 5}};
+            for (int x0 : {0, 2, 6, 30}) {
+                auto chroma = [&](int s) { return (x0 + s) >> 1; };
+                for (int j = 0; j < 4; j++) {
+                    CHECK((e[j].a0 | e[j].a1) != 0, "partly visible lane admitted (X=%d)", X + j);
+                    CHECK(c[tap[j][0]] == e[j].s0 && c[tap[j][1]] == e[j].s1, "cw %d rw %d ox %d DW %d X %d: luma taps",
+                          g.cw, g.rw, g.ox, DW, X + j);
+                    for (int t = 0; t < 2; t++) {
+                        const int k = tap[j][t];
+                        CHECK(chroma(c[k & ~1]) == chroma(t ? e[j].s1 : e[j].s0), "cw %d rw %d X %d: chroma tap",
+                              g.cw, g.rw, X + j);
+                    }
+                }
+            }
+        }
+    }
+    CHECK(c1_ok, "C1 (768 -> 512) not admitted");
+    printf("six-column lanes: %d of 4000 tables admitted, every admitted lane exact\n", admitted);
+}
+
 int main() {
+    check_six_columns();
     check_clip_simd();
     check_roi_tail();
     check_geometry();

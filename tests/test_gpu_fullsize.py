@@ -33,13 +33,14 @@ def oracle_items(O, coracle, frames, items, out_shape, dtype, info, slot=lambda 
     return ref
 
 
-@pytest.mark.parametrize("shape", ["default", "band_px2", "band_th16", "ahead64", "noprio", "wave"])
+@pytest.mark.parametrize("shape", ["default", "band_nodd", "band_px2", "band_th16", "ahead64", "noprio", "wave"])
 def test_c1_bench_batch(evam, O, coracle, gpu, shape, monkeypatch):
-    """C1: 32 x 768x432 NV12 -> 32x3x512x512 u8, bench frames: the band kernel (default; 2 pixels per lane;
-    16-row bands) and the wave kernel's REUSE path (EVAM_PP_WAVE=2)."""
+    """C1: 32 x 768x432 NV12 -> 32x3x512x512 u8, bench frames: the band kernel (default: six-column lanes;
+    per-pixel taps; 2 pixels per lane; 16-row bands) and the wave kernel's REUSE path (EVAM_PP_WAVE=2)."""
     import torch
 
-    for k, v in {"default": {}, "band_px2": {"EVAM_PP_BAND_PX": "2"}, "band_th16": {"EVAM_PP_STRIP_TH": "16"},
+    for k, v in {"default": {}, "band_nodd": {"EVAM_PP_BAND_DD": "0"}, "band_px2": {"EVAM_PP_BAND_PX": "2"},
+                 "band_th16": {"EVAM_PP_STRIP_TH": "16"},
                  "ahead64": {"EVAM_PP_BAND_AHEAD": "64"}, "noprio": {"EVAM_PP_PRIO": "0"},
                  "wave": {"EVAM_PP_WAVE": "2"}}[shape].items():
         monkeypatch.setenv(k, v)

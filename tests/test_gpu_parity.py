@@ -413,6 +413,37 @@ def test_wave_kernel_variants(evam, O, coracle, gpu, fmt, src, dst, resize, vari
         assert_same(got, ref, f"wave {fmt} {src}->{dst} {resize} {variant} {dtype}")
 
 
+@pytest.mark.parametrize("fmt", ["NV12", "I420"])
+@pytest.mark.parametrize("src,dst,resize", [
+    ((768, 432), (512, 512), "no-aspect-ratio"),   # C1: every lane reads 6 source columns
+    ((432, 768), (512, 512), "aspect-ratio"),      # 3:2 with letterbox columns (whole padding lanes)
+    ((600, 338), (400, 400), "no-aspect-ratio"),   # 3:2 horizontal, 338 -> 400 vertical
+    ((630, 300), (420, 420), "aspect-ratio"),      # 3:2 with letterbox rows
+    ((700, 400), (500, 500), "no-aspect-ratio"),   # 7:5: per-pixel taps (not admitted)
+])
+@pytest.mark.parametrize("dd", ["1", "0"])
+def test_band_six_column_lanes(evam, O, coracle, gpu, fmt, src, dst, resize, dd, monkeypatch):
+    """The band kernel's six-column lanes (4 pixels per lane reading 6 luma and 3 chroma columns, admitted by
+    band_six_columns on the host) against the oracle, next to the per-pixel taps (EVAM_PP_BAND_DD=0), on 3:2
+    horizontal scales with and without letterbox columns and rows, and one geometry the check refuses."""
+    import torch
+
+    monkeypatch.setenv("EVAM_PP_BAND", "2")
+    monkeypatch.setenv("EVAM_PP_STRIP", "0")
+    monkeypatch.setenv("EVAM_PP_BAND_DD", dd)
+    rng = np.random.default_rng(zlib.crc32(repr(("dd", fmt, src, dst, resize)).encode()))
+    frames = [O.random_frame(rng, fc(O, fmt), src[0], src[1], pattern=p) for p in ("uniform", "gradient", "uniform")]
+    for dtype in ("u8", "f32"):
+        info = evam.PreProcInfo(color_space="BGR" if dtype == "u8" else "RGB", fill=(5, 50, 250), placement="center",
+                                resize=resize, **({"range": (0.0, 1.0), "mean": (0.1, 0.2, 0.3), "std": (0.3, 0.2, 0.1)}
+                                                  if dtype == "f32" else {}))
+        shape = (3, 3, dst[1], dst[0])
+        got, _ = run_hip(evam, torch, upload(evam, frames, gpu), shape,
+                         torch.float32 if dtype == "f32" else torch.uint8, info)
+        ref, _ = run_oracle(O, coracle, frames, shape, dtype, info)
+        assert_same(got, ref, f"band dd={dd} {fmt} {src}->{dst} {resize} {dtype}")
+
+
 def test_stream_switch_and_descriptor_churn(evam, O, coracle, gpu):
     """Descriptor slots stay valid across torch stream switches and many changing ROI sets / geometries
     (the upload ring and the pinned ROI ring wrap; slot fences, one per run of ROI slots, follow the stream)."""

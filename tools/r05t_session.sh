@@ -1,0 +1,7 @@
+set -euo pipefail
+cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fullsize.py -m gpu -x -q --timeout 120 --timeout-method thread -k "band or c1 or wave_kernel" > gpurun_out/pytest_r05t.log 2>&1 || { tail -40 gpurun_out/pytest_r05t.log; exit 1; }
+tail -2 gpurun_out/pytest_r05t.log
+B="EVAM_PP_LIB=$GRAFT_REPO_ROOT/ab/libevam_pp_base.so"
+bash tools/gpu_env_ab.sh r05t c1 "$B|EVAM_PP_DEFAULT=1|EVAM_PP_BAND_DD=0"
+bash tools/gpu_env_ab.sh r05t c1_i420 "$B|EVAM_PP_DEFAULT=1|EVAM_PP_BAND_DD=0"
