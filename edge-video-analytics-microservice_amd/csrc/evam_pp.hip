@@ -478,9 +478,11 @@ constexpr uint32_t kSatBias = 0xF0000000u;  // 2^32 - 2^28
 constexpr uint32_t kKBs = (uint32_t)kKB + kSatBias, kKGs = (uint32_t)kKG + kSatBias, kKRs = (uint32_t)kKR + kSatBias;
 struct UVs { uint32_t b, g, r; };
 __device__ __forceinline__ UVs uv_terms_sat(uint32_t U, uint32_t V) {
-    return UVs{__umul24(U, (uint32_t)kCUB) + kKBs,
-               (uint32_t)(__mul24((int)V, kCVG) + __mul24((int)U, kCUG)) + kKGs,
-               __umul24(V, (uint32_t)kCVR) + kKRs};
+    // G as two chained v_mad_i32_i24 (the opaque middle value keeps the compiler from re-forming two products and
+    // an add3): 4 VALU per chroma sample instead of 5
+    int gu = __mul24((int)U, kCUG) + (int)kKGs;
+    asm("" : "+v"(gu));
+    return UVs{__umul24(U, (uint32_t)kCUB) + kKBs, (uint32_t)(__mul24((int)V, kCVG) + gu), __umul24(V, (uint32_t)kCVR) + kKRs};
 }
 __device__ __forceinline__ uint32_t luma_term(uint32_t Y) { return __umul24(max(Y, 16u), (uint32_t)kCY); }
 // One source row, one channel: taps' sums s0 (column x0) and s1 (column x1), packed weights w = a0 | a1 << 16
@@ -2438,6 +2440,7 @@ struct QParams {
     int color_rgb;
     uint32_t fill;
     int prio;                 // progress-based priority (as the strip kernel's), over the quarters of the row groups
+    uint32_t mqw;             // q / QW as mulhi(q, mqw) for the lane quads (QW = DW / PX > 1): ceil(2^32 / QW)
 };
 
 
@@ -2549,8 +2552,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(96))) void
 
     // Prologue order: the row table is built first; group 0's DMA (it needs only the row table and the
     // analytic footprint) goes out before the column table and the per-lane setup are built, so its
-    // latency overlaps them.
-    XTab* xt = reinterpret_cast<XTab*>(smem + P.offXT);
+    // latency overlaps them. The column table holds each column's packed tap offsets into the staged rows and
+    // weights (lY, lC, wa: what every lane reading the column needs), so the per-lane setup is table reads.
+    uint4* ct = reinterpret_cast<uint4*>(smem + P.offXT);
     YTab* yt = reinterpret_cast<YTab*>(smem + P.offYT);
     const int DW = P.DW;
     const int Y0 = __builtin_amdgcn_readfirstlane(rr01 & 0xFFFF), Y1 = __builtin_amdgcn_readfirstlane(rr01 >> 16);
@@ -2641,19 +2645,22 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(96))) void
     uint8_t* const buf0 = smem + P.offBuf;
     uint8_t* const buf1 = buf0 + P.buf_bytes;
     issue(0, buf0);
+    static_assert(sizeof(uint4) == sizeof(XTab), "column entries take the host's XTab carve");
     for (int X = tid; X < DW; X += kThreads) {
-        XTab e;
-        e.s0 = 0; e.s1 = 0; e.a0 = 0; e.a1 = 0; e.pad = 0;
+        uint4 e = {0u, 0u, 0u, 0u};  // (lY, lC, wa, 0); all 0: padding column
         const int dx = X - ox;
         if (dx >= 0 && dx < rw) {
             int sx, a0, a1;
             linear_coef(dx, scx, cw, true, sx, a0, a1);
-            e.s0 = sx;
-            e.s1 = min(sx + 1, cw - 1);
-            e.a0 = (uint16_t)(a0 << 4);
-            e.a1 = (uint16_t)(a1 << 4);
+            const int ca = x0 + sx, cb = x0 + min(sx + 1, cw - 1);
+            e.x = (uint32_t)(ca * T::bpp - fsY) | ((uint32_t)(cb * T::bpp - fsY) << 16);
+            if constexpr (FMT == kNV12)
+                e.y = (uint32_t)(2 * (ca >> 1) - fsC) | ((uint32_t)(2 * (cb >> 1) - fsC) << 16);
+            else if constexpr (FMT == kI420)
+                e.y = (uint32_t)((ca >> 1) - fsC) | ((uint32_t)((cb >> 1) - fsC) << 16);
+            e.z = ((uint32_t)a0 << 4) | ((uint32_t)a1 << 20);
         }
-        xt[X] = e;
+        ct[X] = e;
     }
     lds_barrier();  // column table visible to the per-lane setup; group 0's DMA stays in flight
     EVAM_STAMP(9);
@@ -2667,24 +2674,17 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(96))) void
     int rr[KQ];
 #pragma unroll
     for (int k = 0; k < KQ; k++) {
-        const int q = tid + k * kThreads;
-        const bool v = k < K && q < nq;
-        const int r = v ? q / QW : 0;
-        const int c0 = v ? (q - r * QW) * PX : 0;
+        const uint32_t q = (uint32_t)(tid + k * kThreads);  // < 2^16: mulhi by ceil(2^32 / QW) is q / QW exactly
+        const bool v = k < K && (int)q < nq;
+        const int r = v ? (QW > 1 ? (int)__umulhi(q, P.mqw) : (int)q) : 0;
+        const int c0 = v ? ((int)q - r * QW) * PX : 0;
         rr[k] = v ? r : -1;
 #pragma unroll
         for (int j = 0; j < PX; j++) {
-            const XTab e = xt[c0 + j];
-            wa[k][j] = (uint32_t)e.a0 | ((uint32_t)e.a1 << 16);
-            lY[k][j] = lC[k][j] = 0;
-            if (v && wa[k][j] != 0) {
-                const int ca = x0 + e.s0, cb = x0 + e.s1;
-                lY[k][j] = (uint32_t)(ca * T::bpp - fsY) | ((uint32_t)(cb * T::bpp - fsY) << 16);
-                if constexpr (FMT == kNV12)
-                    lC[k][j] = (uint32_t)(2 * (ca >> 1) - fsC) | ((uint32_t)(2 * (cb >> 1) - fsC) << 16);
-                else if constexpr (FMT == kI420)
-                    lC[k][j] = (uint32_t)((ca >> 1) - fsC) | ((uint32_t)((cb >> 1) - fsC) << 16);
-            }
+            const uint4 e = ct[c0 + j];
+            lY[k][j] = e.x;
+            lC[k][j] = e.y;
+            wa[k][j] = e.z;
         }
     }
     const int ngroups = (rows + R - 1) / R;
@@ -3519,6 +3519,8 @@ bool plan_roi(int f, int DW, int DH, int out_dtype, int px, int max_row_bytes, i
     const int64_t grid = (int64_t)count * base_tiles;
     const int per_cu = (int)std::max<int64_t>(1, std::min<int64_t>(kRoiWavesPerSimd, (grid + n_cu - 1) / n_cu));
     const int pxv = (px == 4 || px == 2) && DW % px == 0 ? px : 1;
+    const uint32_t qw = (uint32_t)(DW / pxv);
+    q.mqw = qw > 1 ? (uint32_t)((0x100000000ull + qw - 1) / qw) : 0u;
     const int nb = 2;
     int buf = kn.roi_buf;
     if (buf <= 0) buf = std::min(12 * 1024, ((((160 * 1024) / per_cu) & ~1023) - q.offBuf) / nb & ~15);
