@@ -2309,8 +2309,25 @@ __global__ __launch_bounds__(256) void evam_pp_band(const TParams P) {
             }
         }
     };
-    // horizontal pass of source row r (crop-relative) into H
-    auto hrow = [&](int r, uint32_t (&H)[PX][3]) {
+    // A source row's 3 PX filtered values travel as 64-bit register pairs (value k of pixel j at flat index
+    // 3 j + k), so the HA <- HB copy of a one-row step is one v_pk_mov_b32 per two values.
+    constexpr int NH = (3 * PX + 1) / 2;
+    struct HRow { uint64_t p[NH]; };
+    auto hget = [](const HRow& h, int j, int k) -> uint32_t {
+        const int f = 3 * j + k;
+        return (uint32_t)(h.p[f >> 1] >> (32 * (f & 1)));
+    };
+    auto hpack = [](HRow& h, const uint32_t (&H)[PX][3]) {
+#pragma unroll
+        for (int i = 0; i < NH; i++) {
+            const int f0 = 2 * i, f1 = 2 * i + 1;
+            const uint32_t lo = H[f0 / 3][f0 % 3], hi = f1 < 3 * PX ? H[f1 / 3][f1 % 3] : 0u;
+            h.p[i] = (uint64_t)lo | ((uint64_t)hi << 32);
+        }
+    };
+    // horizontal pass of source row r (crop-relative) into HR
+    auto hrow = [&](int r, HRow& HR) {
+        uint32_t H[PX][3];
         const int c = (y0 + r) >> 1;
         if (c != cc) chroma_row(c);
         const uint8_t* yb = wbuf + (r - rlo) * segY;
@@ -2330,6 +2347,7 @@ __global__ __launch_bounds__(256) void evam_pp_band(const TParams P) {
                 H[2][ch3] = hpass_sums(sm[3], sm[4], wp[2]) & kVMask;
                 H[3][ch3] = hpass_sums(sm[4], sm[5], wp[3]) & kVMask;
             }
+            hpack(HR, H);
             return;
         }
 #pragma unroll
@@ -2340,8 +2358,9 @@ __global__ __launch_bounds__(256) void evam_pp_band(const TParams P) {
             H[j][1] = hpass_sat(yA, tA[j].g, yB, tB[j].g, wp[j]) & kVMask;
             H[j][2] = hpass_sat(yA, tA[j].r, yB, tB[j].r, wp[j]) & kVMask;
         }
+        hpack(HR, H);
     };
-    uint32_t HA[PX][3], HB[PX][3];
+    HRow HA, HB;
     int pa = -1, pb = -1;
     const int nst = 3;  // stores per output row (one PX-wide store per channel)
     // progress-based priority (EVAM_PP_PRIO), as in the strip kernel
@@ -2372,19 +2391,13 @@ __global__ __launch_bounds__(256) void evam_pp_band(const TParams P) {
         // HA <- row ra, HB <- row rb, reusing what the previous output row filtered (wave-uniform branches)
         if (ra != pa) {
             if (ra == pb) {
-#pragma unroll
-                for (int j = 0; j < PX; j++)
-#pragma unroll
-                    for (int c = 0; c < 3; c++) HA[j][c] = HB[j][c];
+                HA = HB;
             } else {
                 hrow(ra, HA);
             }
         }
         if (rb == ra) {
-#pragma unroll
-            for (int j = 0; j < PX; j++)
-#pragma unroll
-                for (int c = 0; c < 3; c++) HB[j][c] = HA[j][c];
+            HB = HA;
         } else if (rb != pb || ra == pb) {  // HB was overwritten into HA above, or holds another row
             hrow(rb, HB);
         }
@@ -2394,7 +2407,7 @@ __global__ __launch_bounds__(256) void evam_pp_band(const TParams P) {
 #pragma unroll
         for (int j = 0; j < PX; j++)
 #pragma unroll
-            for (int c = 0; c < 3; c++) v[c][j] = vfinal_masked<OUT>(HA[j][c], HB[j][c], wb0, wb1);
+            for (int c = 0; c < 3; c++) v[c][j] = vfinal_masked<OUT>(hget(HA, j, c), hget(HB, j, c), wb0, wb1);
         if (anypad) {
 #pragma unroll
             for (int j = 0; j < PX; j++) {
@@ -2492,9 +2505,10 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(96))) void
                  "s"(P.DW), "s"(P.DH));
     if (kAblate & 128) return;  // diagnostics: launch cost only
     EVAM_STAMP(0);
-    // The whole 64-byte record in one scalar load, issued first: it is a PCIe read from pinned host
-    // memory (~1-2 us under load), and field-by-field loads became up to three dependent round trips
-    // per wave. Its latency overlaps the LUT load below.
+    // The whole 64-byte record in one scalar load, issued first (field-by-field loads became up to three
+    // dependent round trips per wave). The record slot is device memory the host wrote through its BAR
+    // mapping (PinRing, HipRings::pinned_alloc), or pinned host memory read over PCIe where the platform does
+    // not map device memory (~1-2 us more under load). Its latency overlaps the LUT load below.
     typedef unsigned int u32x16 __attribute__((ext_vector_type(16)));
     const u32x16 rec = *((const __attribute__((address_space(4))) u32x16*)(P.recs) + blockIdx.x);
     // The LUT by LDS-DMA, issued first: no VGPR waits on it, and group 0's wait (everything older than its
@@ -2890,6 +2904,7 @@ struct Knobs {
     int strip_waves = 16;                          // strip / band kernels: resident waves per CU the tiles are sized for
     int band = 1, band_px = 0;                     // band kernel: allowed (2: forced), pixels per lane
     int band_dd = 1;                               // band kernel: six-column lanes where the column table allows
+    int rec_device = 1;                            // ROI records in host-written device memory where mapped (0: pinned host)
     int prio = 1;                                  // progress-based wave priority (strip, band, ROI kernels): C2 +3 %,
                                                    // C4 +3 %, C5 +3-5 %, C1 +9 % (profiles/r04k_ab_lines.txt)
     int band_ahead = 2;                            // band kernel: source rows issued ahead of the current output row's
@@ -2901,6 +2916,7 @@ struct Knobs {
         band_ahead = env_int("EVAM_PP_BAND_AHEAD", band_ahead);
         band = env_int("EVAM_PP_BAND", band); band_px = env_int("EVAM_PP_BAND_PX", band_px);
         band_dd = env_int("EVAM_PP_BAND_DD", band_dd);
+        rec_device = env_int("EVAM_PP_REC_DEVICE", rec_device);
         strip = env_int("EVAM_PP_STRIP", strip); strip_th = env_int("EVAM_PP_STRIP_TH", strip_th);
         strip_waves = env_int("EVAM_PP_STRIP_WAVES", strip_waves);
         strip_pair = env_int("EVAM_PP_STRIP_PAIR", strip_pair); strip_nw = env_int("EVAM_PP_STRIP_NW", strip_nw);
@@ -3554,7 +3570,41 @@ struct HipRings {
     int stream_destroy(Stream s) { return err(hipStreamDestroy(s), "hipStreamDestroy"); }
     int stream_wait(Stream s, Event e) { return err(hipStreamWaitEvent(s, e, 0), "hipStreamWaitEvent"); }
     int stream_sync(Stream s) { return err(hipStreamSynchronize(s), "hipStreamSynchronize"); }
-    int pinned_alloc(uint8_t** h, const uint8_t** d, size_t n) {
+    // ROI record slots: fine-grained device memory that the host writes through the platform's BAR mapping of it
+    // (one 64-byte scalar load per workgroup from device memory instead of a PCIe read from host memory: ~4.5 us
+    // less per 1,600-workgroup launch, tools/microbench/rec_hostwrite.hip), where the allocation is mapped
+    // read-write into this process; else pinned, coherent host memory (EVAM_PP_REC_DEVICE=0 forces that).
+    bool rec_device = true;
+    static bool host_mapped_rw(const void* p, size_t n) {
+        FILE* f = fopen("/proc/self/maps", "r");
+        if (!f) return false;
+        const uintptr_t a = reinterpret_cast<uintptr_t>(p), e = a + n;
+        char line[512];
+        bool ok = false;
+        while (!ok && fgets(line, sizeof(line), f)) {
+            unsigned long lo = 0, hi = 0;
+            char perm[8] = {};
+            if (sscanf(line, "%lx-%lx %7s", &lo, &hi, perm) == 3 && lo <= a && e <= hi) ok = perm[0] == 'r' && perm[1] == 'w';
+        }
+        fclose(f);
+        return ok;
+    }
+    int pinned_alloc(uint8_t** h, const uint8_t** d, size_t n, bool* wc) {
+        *wc = false;
+        if (rec_device) {
+            void* p = nullptr;
+            if (hipExtMallocWithFlags(&p, n, hipDeviceMallocFinegrained) == hipSuccess) {
+                if (host_mapped_rw(p, n)) {
+                    *h = static_cast<uint8_t*>(p);
+                    *d = static_cast<const uint8_t*>(p);
+                    *wc = true;
+                    return 0;
+                }
+                (void)hipFree(p);
+            } else {
+                (void)hipGetLastError();
+            }
+        }
         if (hipHostMalloc((void**)h, n, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
             *h = nullptr;
             return fail(EVAM_PP_ERR_OOM, "evam_pp_run: hipHostMalloc(%zu) failed", n);
@@ -3564,7 +3614,7 @@ struct HipRings {
         *d = reinterpret_cast<const uint8_t*>(dp);
         return 0;
     }
-    int pinned_free(uint8_t* h) { return err(hipHostFree(h), "hipHostFree"); }
+    int pinned_free(uint8_t* h, bool wc) { return wc ? err(hipFree(h), "hipFree") : err(hipHostFree(h), "hipHostFree"); }
     int host_alloc(uint8_t** h, size_t n) {
         if (hipHostMalloc((void**)h, n, hipHostMallocDefault) != hipSuccess) {
             *h = nullptr;
@@ -4052,9 +4102,11 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
     uint8_t* dyn = nullptr;
     const uint8_t* d_dyn = nullptr;
     PinGuard pin_guard{h};
+    bool dyn_wc = false;
     if (any_roi) {
         HipRings b;
-        if (int rc = h->pin.acquire(b, dyn_bytes, &dyn, &d_dyn)) return rc;
+        b.rec_device = kn.rec_device != 0;
+        if (int rc = h->pin.acquire(b, dyn_bytes, &dyn, &d_dyn, &dyn_wc)) return rc;
         pin_guard.armed = true;
         HP(5);
         // Launch order: largest estimated work first (counting sort on 64 buckets of the staged
@@ -4162,8 +4214,15 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
                 r.item = i;
                 r.row0 = (uint16_t)un[4 * u + 1];
                 r.row1 = (uint16_t)un[4 * u + 2];
-                memcpy(&rr[pos], &r, sizeof(RoiRec));
+                if (dyn_wc) {  // write-combined device memory: the 64-byte line as four streaming stores
+                    const __m128i* src = reinterpret_cast<const __m128i*>(&r);
+                    __m128i* dst = reinterpret_cast<__m128i*>(&rr[pos]);
+                    for (int k = 0; k < 4; k++) _mm_stream_si128(dst + k, _mm_load_si128(src + k));
+                } else {
+                    memcpy(&rr[pos], &r, sizeof(RoiRec));
+                }
             }
+            if (dyn_wc) _mm_sfence();  // the records reach device memory before the launch's doorbell
             const int nrec = nu;
             qrec[f] = nrec;
         }

@@ -8,8 +8,9 @@
 //   typename B::Event, typename B::Stream       (value types; a default-constructed Event is "none")
 //   event_create(Event*), event_destroy(Event), event_record(Event, Stream), event_sync(Event)
 //   stream_create(Stream*), stream_destroy(Stream), stream_wait(Stream, Event), stream_sync(Stream)
-//   pinned_alloc(uint8_t** host, const uint8_t** dev, size_t)   (mapped, coherent: kernels read it in place)
-//   pinned_free(uint8_t*), host_alloc(uint8_t**, size_t), host_free(uint8_t*)
+//   pinned_alloc(uint8_t** host, const uint8_t** dev, size_t, bool* wc)   (kernels read it in place; wc: the host
+//       writes it through a write-combined mapping of device memory: stream whole lines, fence after)
+//   pinned_free(uint8_t*, bool wc), host_alloc(uint8_t**, size_t), host_free(uint8_t*)
 //   dev_alloc(uint8_t**, size_t), dev_free(uint8_t*), copy_h2d(uint8_t* dst, const uint8_t* src, size_t, Stream)
 #ifndef EVAM_RINGS_H
 #define EVAM_RINGS_H
@@ -24,8 +25,9 @@
 namespace evam {
 
 // Per-call ROI records ([RoiRec x n], launch order) change with every detection result. They are written
-// into a slot of pinned, coherent (fine-grained) host memory that the ROI kernel reads in place over PCIe:
-// one memcpy per call and no copy command. Slots are used in order and fenced in runs of kFence: one
+// into a slot that the ROI kernel reads in place — fine-grained device memory the host writes through its
+// BAR mapping where the platform maps it, else pinned, coherent host memory read over PCIe: one pass of
+// host stores per call and no copy command. Slots are used in order and fenced in runs of kFence: one
 // event, recorded after the call that used the run's last slot, covers the run (an event record per call
 // adds a packet the command processor serves between every two ROI launches).
 template <class B>
@@ -35,13 +37,14 @@ struct PinRingT {
     uint8_t* host[N] = {};
     const uint8_t* dev[N] = {};  // device address of host[k]
     size_t cap[N] = {};
+    bool wc[N] = {};             // host[k] is a write-combined mapping of device memory
     typename B::Event used[N] = {};
     bool used_rec[N] = {};
     int cur = -1;
 
     // Next slot with at least n bytes. Blocks only while a kernel of up to N calls ago may still read it:
     // the fence of the slot's run was recorded after the run's last call of the previous lap.
-    int acquire(B& b, size_t n, uint8_t** h, const uint8_t** d) {
+    int acquire(B& b, size_t n, uint8_t** h, const uint8_t** d, bool* is_wc = nullptr) {
         const int k = (cur + 1) % N;
         const int fk = k | (kFence - 1);
         if (!used[fk]) {
@@ -52,18 +55,20 @@ struct PinRingT {
         }
         if (cap[k] < n) {
             if (host[k]) {
-                if (int rc = b.pinned_free(host[k])) return rc;
+                if (int rc = b.pinned_free(host[k], wc[k])) return rc;
             }
             host[k] = nullptr;
             dev[k] = nullptr;
             cap[k] = 0;
+            wc[k] = false;
             const size_t c = std::max<size_t>(n * 2, 64 * 1024);
-            if (int rc = b.pinned_alloc(&host[k], &dev[k], c)) return rc;
+            if (int rc = b.pinned_alloc(&host[k], &dev[k], c, &wc[k])) return rc;
             cap[k] = c;
         }
         cur = k;
         *h = host[k];
         *d = dev[k];
+        if (is_wc) *is_wc = wc[k];
         return 0;
     }
 
@@ -81,10 +86,11 @@ struct PinRingT {
 
     void release(B& b) {
         for (int k = 0; k < N; k++) {
-            if (host[k]) (void)b.pinned_free(host[k]);
+            if (host[k]) (void)b.pinned_free(host[k], wc[k]);
             if (used[k]) (void)b.event_destroy(used[k]);
             host[k] = nullptr;
             dev[k] = nullptr;
+            wc[k] = false;
             used[k] = typename B::Event{};
             used_rec[k] = false;
             cap[k] = 0;

@@ -70,8 +70,14 @@ struct Sim {
         free(p);
         return 0;
     }
-    int pinned_alloc(uint8_t** h, const uint8_t** d, size_t n) { int rc = alloc(h, n); *d = *h; return rc; }
-    int pinned_free(uint8_t* h) { return release(h, host_t, "pinned slot freed"); }
+    int pinned_alloc(uint8_t** h, const uint8_t** d, size_t n, bool* wc) {
+        int rc = alloc(h, n);
+        *d = *h;
+        *wc = (++pinned_allocs & 1) != 0;  // both slot kinds, alternating
+        return rc;
+    }
+    int pinned_free(uint8_t* h, bool) { return release(h, host_t, "pinned slot freed"); }
+    int pinned_allocs = 0;
     int host_alloc(uint8_t** h, size_t n) { return alloc(h, n); }
     int host_free(uint8_t* h) { return release(h, host_t, "host staging slot freed"); }
     int dev_alloc(uint8_t** d, size_t n) { return alloc(d, n); }

@@ -444,10 +444,14 @@ def test_band_six_column_lanes(evam, O, coracle, gpu, fmt, src, dst, resize, dd,
         assert_same(got, ref, f"band dd={dd} {fmt} {src}->{dst} {resize} {dtype}")
 
 
-def test_stream_switch_and_descriptor_churn(evam, O, coracle, gpu):
+@pytest.mark.parametrize("rec_device", ["1", "0"])
+def test_stream_switch_and_descriptor_churn(evam, O, coracle, gpu, rec_device, monkeypatch):
     """Descriptor slots stay valid across torch stream switches and many changing ROI sets / geometries
-    (the upload ring and the pinned ROI ring wrap; slot fences, one per run of ROI slots, follow the stream)."""
+    (the upload ring and the ROI record ring wrap; slot fences, one per run of ROI slots, follow the stream), with
+    the record slots in host-written device memory (default) and in pinned host memory (EVAM_PP_REC_DEVICE=0)."""
     import torch
+
+    monkeypatch.setenv("EVAM_PP_REC_DEVICE", rec_device)
 
     rng = np.random.default_rng(11)
     frames = [O.random_frame(rng, O.NV12, 320, 180) for _ in range(2)]

@@ -11,8 +11,10 @@ export TMPDIR=/tmp
 cd /tmp
 for a in $ABL; do
   d="$OUT/profabl_${TAG}_${CFG}_$a"
-  lib="$ROOT/ab/libevam_pp_abl$a.so"; [ "$a" = 0 ] && lib="$ROOT/edge-video-analytics-microservice_amd/libevam_pp.so"
-  EVAM_PP_LIB="$lib" EVAM_PP_DIAGNOSTIC_BUILD_OK=1 timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d "$d" -o run -- \
+  # 0: the in-tree product library (or the caller's EVAM_PP_LIB variant)
+  lib="$ROOT/ab/libevam_pp_abl$a.so"; [ "$a" = 0 ] && lib="${EVAM_PP_LIB:-}"
+  if [ -n "$lib" ]; then export EVAM_PP_LIB="$lib"; else unset EVAM_PP_LIB; fi
+  EVAM_PP_DIAGNOSTIC_BUILD_OK=1 timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d "$d" -o run -- \
     python3 "$ROOT/bench.py" --config "$CFG" --steps 200 --warmup 30 --no-cpu-baseline --resident-steps 0 "$@" \
     > "$d.json" 2> "$d.err" || { tail -5 "$d.err"; exit 1; }
   python3 - "$d" "$a" "$CFG" <<'PY' | tee -a "$OUT/profabl_$TAG.txt"
