@@ -497,6 +497,13 @@ __device__ __forceinline__ uint32_t hpass_sums(uint32_t s0, uint32_t s1, uint32_
 __device__ __forceinline__ uint32_t hpass_sat(uint32_t y0, uint32_t t0, uint32_t y1, uint32_t t1, uint32_t w) {
     return hpass_sums(__builtin_elementwise_add_sat(y0, t0), __builtin_elementwise_add_sat(y1, t1), w);
 }
+// u8 bytes (x >> 2) of four vertical-pass sums x = mulhi + mulhi + 2 < 2^16 (each result <= 255), packed little-endian: two u16 pairs, one packed
+// shift each, one byte permute (5 VALU for 4 pixels instead of 4 shifts and 4 shift / or steps)
+__device__ __forceinline__ uint32_t pack4_u8_sums(uint32_t x0, uint32_t x1, uint32_t x2, uint32_t x3) {
+    const evam_u16x2 p01 = __builtin_bit_cast(evam_u16x2, x0 | (x1 << 16)) >> (evam_u16x2){2, 2};
+    const evam_u16x2 p23 = __builtin_bit_cast(evam_u16x2, x2 | (x3 << 16)) >> (evam_u16x2){2, 2};
+    return __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, p23), __builtin_bit_cast(uint32_t, p01), 0x06040200u);
+}
 
 // Horizontal pass of one source row, three channels, from the two taps' luma bytes and chroma terms.
 __device__ __forceinline__ void hrow_sat(uint32_t Y0, uint32_t Y1, const UVs& tA, const UVs& tB, uint32_t w,
@@ -2408,6 +2415,35 @@ __global__ __launch_bounds__(256) void evam_pp_band(const TParams P) {
         for (int j = 0; j < PX; j++)
 #pragma unroll
             for (int c = 0; c < 3; c++) v[c][j] = vfinal_masked<OUT>(hget(HA, j, c), hget(HB, j, c), wb0, wb1);
+        if constexpr (OUT == 0 && PX == 4) {  // u8, 4 pixels per lane: the sums packed by pack4_u8_sums
+            uint32_t x[3][4];
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+#pragma unroll
+                for (int c = 0; c < 3; c++) x[c][j] = mulhi_u24(wb0, hget(HA, j, c)) + mulhi_u24(wb1, hget(HB, j, c)) + 2u;
+            if (anypad) {  // padding columns: the fill byte as a sum (x >> 2 == fill)
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    x[0][j] = padc[j] ? fill0 << 2 : x[0][j];
+                    x[1][j] = padc[j] ? fill1 << 2 : x[1][j];
+                    x[2][j] = padc[j] ? fill2 << 2 : x[2][j];
+                }
+            }
+            if (xin) {
+                const uint32_t off = vo + (uint32_t)((vr0 + i) * p_DW);
+                __builtin_amdgcn_raw_buffer_store_b32(pack4_u8_sums(x[0][0], x[0][1], x[0][2], x[0][3]), rsO0, off, 0,
+                                                      EVAM_PP_STORE_AUX);
+                __builtin_amdgcn_raw_buffer_store_b32(pack4_u8_sums(x[1][0], x[1][1], x[1][2], x[1][3]), rsO1, off, 0,
+                                                      EVAM_PP_STORE_AUX);
+                __builtin_amdgcn_raw_buffer_store_b32(pack4_u8_sums(x[2][0], x[2][1], x[2][2], x[2][3]), rsO2, off, 0,
+                                                      EVAM_PP_STORE_AUX);
+            }
+            pos += nst;
+            asm volatile("" ::: "memory");  // issue order is what the counted waits assume
+            if (i + 1 < n) issue_to(min(rhi, __builtin_amdgcn_readlane(lr1, i + 1) + ahead));
+            asm volatile("" ::: "memory");
+            continue;
+        }
         if (anypad) {
 #pragma unroll
             for (int j = 0; j < PX; j++) {
