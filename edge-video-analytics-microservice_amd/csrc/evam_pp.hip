@@ -2931,9 +2931,11 @@ struct Knobs {
     int stage_r = -1;                              // staged pipeline: rows per group
     int wth = -1, px = 0, reuse = 1, wave_lds = 40 * 1024;
     int roi_th = -1, roi_buf = -1, roi_px = 2;     // roi_buf -1: sized for one round; pixels per lane (1 for odd DW)
-    int roi_sort = 0;  // 1: largest estimated bytes first before the stable sort by row groups (C3: equal or
-                       // slower, profiles/r04k_ab_lines.txt; the units are ordered by row groups either way)
+    int roi_sort = 1;  // 1: largest estimated bytes first before the stable sort by row groups (alone: equal or
+                       // slower, profiles/r04k_ab_lines.txt; with the snake deal below C3 +1.5-2 %,
+                       // profiles/r05zf_c3_snake_ab.txt)
     int roi_tail = 4;                              // row tiles per ROI of the uneven tail over the CUs (1: no split)
+    int roi_snake = 1;                             // snake deal of the sorted units over the CUs (0: bands in one direction)
     int strip = 1, strip_th = -1, strip_nw = -1, strip_px = 0;  // strip kernel: allowed (2: forced), rows per
                                                                 // tile, waves, px
     int strip_pair = 1;                            // strip kernel: paired-tap DMA where the footprints allow it
@@ -2966,7 +2968,7 @@ struct Knobs {
         reuse = env_int("EVAM_PP_REUSE", reuse); wave_lds = env_int("EVAM_PP_WAVE_LDS", wave_lds);
         roi_th = env_int("EVAM_PP_ROI_TH", roi_th); roi_buf = env_int("EVAM_PP_ROI_BUF", roi_buf);
         roi_px = env_int("EVAM_PP_ROI_PX", roi_px); roi_sort = env_int("EVAM_PP_ROI_SORT", roi_sort);
-        roi_tail = env_int("EVAM_PP_ROI_TAIL", roi_tail);
+        roi_tail = env_int("EVAM_PP_ROI_TAIL", roi_tail); roi_snake = env_int("EVAM_PP_ROI_SNAKE", roi_snake);
     }
 };
 
@@ -4237,6 +4239,14 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
             std::vector<int>& order = h->sc_slot;
             order.resize(nu);
             for (int u = 0; u < nu; u++) order[start[maxcost - un[4 * u + 3]]++] = u;
+            // Snake deal: workgroup p starts on XCD p % 8 and within it on CU (p / 8) % 32, so each band of n_cu
+            // consecutive positions puts one unit on every CU; reversing every other band gives each CU one large and
+            // one small unit per two bands instead of always the k-th largest of every band (per-CU work balance is
+            // what bounds a one-round launch: profiles/r05ze_c3_head_split_ab.txt, r05zd_c3_xcd_frames_devrec_ab.txt)
+            if (kn.roi_snake) {
+                const int band = std::max(1, h->n_cu);
+                for (int b0 = band; b0 < nu; b0 += 2 * band) std::reverse(order.begin() + b0, order.begin() + std::min(nu, b0 + band));
+            }
             for (int pos = 0; pos < nu; pos++) {
                 const int u = order[pos];
                 const int i = un[4 * u];

@@ -113,14 +113,14 @@ def test_c2_bench_batch(evam, O, coracle, gpu, shape, monkeypatch):
     pp.close()
 
 
-@pytest.mark.parametrize("kernel", ["roi_tail1", "roi", "roi_noprio", "roi_sorted", "roi_pinned"])
+@pytest.mark.parametrize("kernel", ["roi_tail1", "roi", "roi_noprio", "roi_unsorted", "roi_pinned"])
 @pytest.mark.parametrize("seed", [0, 3])
 def test_c3_bench_roi_set(evam, O, coracle, gpu, seed, kernel, monkeypatch):
     """C3: bench.py's seeded ROI set (50 per frame, w 24..400, h 24..300) on 32 bench 1080p NV12 frames ->
     1600x3x72x72 fp32 through the ROI kernel, with and without its tail split (EVAM_PP_ROI_TAIL: the 64 ROIs beyond 6
-    per CU as row tiles), without progress-based priority (EVAM_PP_PRIO=0), with the largest-bytes pre-order
-    (EVAM_PP_ROI_SORT=1) and with the records in pinned host memory instead of host-written device memory
-    (EVAM_PP_REC_DEVICE=0)."""
+    per CU as row tiles), without progress-based priority (EVAM_PP_PRIO=0), without the largest-bytes pre-order and
+    the snake deal over the CUs (EVAM_PP_ROI_SORT=0 EVAM_PP_ROI_SNAKE=0) and with the records in pinned host memory
+    instead of host-written device memory (EVAM_PP_REC_DEVICE=0)."""
     import torch
 
     if kernel == "roi_pinned":
@@ -129,8 +129,9 @@ def test_c3_bench_roi_set(evam, O, coracle, gpu, seed, kernel, monkeypatch):
     if kernel.endswith("_noprio"):
         monkeypatch.setenv("EVAM_PP_PRIO", "0")
         kernel = kernel[:-7]
-    if kernel == "roi_sorted":  # largest estimated bytes first before the sort by row groups
-        monkeypatch.setenv("EVAM_PP_ROI_SORT", "1")
+    if kernel == "roi_unsorted":  # call order before the sort by row groups, bands dealt in one direction
+        monkeypatch.setenv("EVAM_PP_ROI_SORT", "0")
+        monkeypatch.setenv("EVAM_PP_ROI_SNAKE", "0")
     monkeypatch.setenv("EVAM_PP_ROI_TAIL", "1" if kernel == "roi_tail1" else "4")
 
     wl = bench.WORKLOADS["c3"]
