@@ -3,14 +3,18 @@
 
 Default workload (BASELINE.json configs[1], "C2"): a batch of 32 synthetic 1920x1080 NV12 frames,
 device-resident, -> 32x3x512x512 fp32 NCHW normalised (range [0,1], ImageNet mean/std in BGR order),
-one fused kernel launch per step. Other configs (--config c1|c3|c4|c5) are the remaining BASELINE
-workloads; the driver's headline line is c2.
+one fused kernel launch per step, two steps in flight on two handles / HIP streams (the shape
+PipelineServer's device runner runs by default; `--inflight 1` times one launch at a time, and every
+line carries that one-at-a-time kernel figure as roofline.single_launch). Other configs (--config
+c1|c3|c4|c5) are the remaining BASELINE workloads; the driver's headline line is c2.
 
     python bench.py [--gpus N --steps K --warmup W] [--config c2] [--no-cpu-baseline]
 
-Multi-GPU: one process per GPU (torchrun); camera streams are partitioned s mod G, every rank runs its
-own batch (weak scaling), no collective touches the hot loop; after the timed region one all_reduce(MAX)
-of the elapsed time and one all_gather of per-rank stats run over RCCL.
+Multi-GPU: one process per GPU; camera streams are partitioned s mod G, every rank runs its own batch
+(weak scaling), no collective touches the hot loop; after the timed region one all_reduce(MAX) of the
+elapsed time and one all_gather of per-rank stats run over RCCL. `bench.py --gpus N` started without a
+launcher starts the N ranks itself (the environment torch.distributed.run would set); under torchrun
+(`--nproc-per-node N ... bench.py --gpus N`) each rank runs directly.
 
 HBM-honest by default: every step reads a different set of frames and writes a different output
 tensor, from a pool whose footprint is >= 3x the 256 MiB Infinity Cache (MI355X_MICROARCH.md: a buffer
@@ -267,6 +271,58 @@ def via_pipeline(args, evam, torch, wl, device_index):
             "mean_frames_per_launch": round(float(np.mean(sizes)), 2) if sizes else 0.0}
 
 
+def rank_envs(n: int, base: dict, port: int) -> list[dict]:
+    """The environment torch.distributed.run gives each of n ranks on one node (one process per GPU,
+    streams s mod n), for `bench.py --gpus n` started without a launcher."""
+    envs = []
+    for r in range(n):
+        e = dict(base)
+        e.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0",
+                 ROLE_RANK=str(r), ROLE_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                 TORCHELASTIC_RUN_ID="evam-bench")
+        envs.append(e)
+    return envs
+
+
+def launch_ranks(n: int, backend: str) -> int:
+    """Start n rank processes of this script (one per GPU) and wait for them; rank 0 prints the aggregated line.
+    Returns the exit status: non-zero if any rank failed (the others are then terminated). With RCCL ("nccl") each
+    rank needs its own device, so fewer visible devices than n is an error, never a silent one-rank run. Runs before
+    this process touches the GPU (torch.cuda.device_count() does not initialise it on this image)."""
+    import socket
+    import subprocess
+
+    import torch
+
+    if backend == "nccl":
+        have = torch.cuda.device_count()
+        if have < n:
+            print(f"bench.py --gpus {n}: only {have} visible GPU(s); one rank per GPU needs {n} "
+                  "(EVAM_BENCH_BACKEND=gloo rehearses several ranks on one GPU)", file=sys.stderr)
+            return 2
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, os.path.abspath(__file__), *sys.argv[1:]]
+    procs = [subprocess.Popen(cmd, env=e) for e in rank_envs(n, os.environ, port)]
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 1
+                print(f"bench.py --gpus {n}: rank {procs.index(p)} exited with {code}; stopping the others",
+                      file=sys.stderr)
+                for q in live:
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
 def load_pmc_valu(config_name: str, n_frames_per_launch: int, pool: int):
     """Wave-level VALU instructions per launch from the committed rocprofv3 PMC summary, if any."""
     path = os.path.join(ROOT, "profiles", "pmc_valu.json")
@@ -306,14 +362,22 @@ def main():
     ap.add_argument("--frames-per-stream", type=int, default=16384, help="--via pipeline: frames per stream")
     ap.add_argument("--stream-batch", type=int, default=16, help="--via pipeline: gvadetect batch-size per stream")
     ap.add_argument("--hub-batch", type=int, default=256, help="--via pipeline: max frames per hub launch")
-    ap.add_argument("--inflight", type=int, default=1,
+    ap.add_argument("--inflight", type=int, default=2,
                     help="launches in flight: step t runs on handle/stream t mod N (independent outputs), so launch "
-                         "t+1's ramp overlaps launch t's tail; reported as its own line, timed by wall clock")
+                         "t+1's ramp overlaps launch t's tail, timed by wall clock. The default 2 is the shape the "
+                         "product runs (PipelineServer's device runner, server option inflight=2); the one-launch-at-"
+                         "a-time kernel figure is reported next to it as roofline.single_launch either way")
     ap.add_argument("--runner-inflight", type=int, default=2,
                     help="--via pipeline: ticks the device runner keeps in flight (server option inflight)")
     ap.add_argument("--runner", choices=["device", "threads"], default="device",
                     help="--via pipeline: one runner thread per device (default) or one thread per pipeline")
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # `bench.py --gpus N` without a launcher: start the N ranks here (before anything touches the GPU)
+        sys.exit(launch_ranks(args.gpus, os.environ.get("EVAM_BENCH_BACKEND", "nccl")))
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
 
     import torch
     import torch.distributed as dist
@@ -321,6 +385,9 @@ def main():
 
     evam = g.import_package()
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch one rank per GPU with --nproc-per-node "
+                         f"{args.gpus} (or run bench.py --gpus {args.gpus} without a launcher)")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # EVAM_BENCH_BACKEND=gloo: rehearse the multi-process path with more ranks than GPUs (ranks share
@@ -409,10 +476,11 @@ def main():
         inflight: on handle t mod --inflight (its own stream)."""
         k = t % P if k is None else k
         out = outs[k % n_out]
-        pp = pps[t % len(pps)] if inflight else pps[0]
+        slot = t % len(pps) if inflight else 0
+        pp = pps[slot]
         if feed is not None:
             # the copy wait and the consumed mark go on the stream the handle launches on (ADVICE r4)
-            st = inflight_streams[t % len(pps)] if inflight else None
+            st = inflight_streams[slot] if len(pps) > 1 else None
             j = feed.acquire()
             feed.submit(j)
             pp.convert(feed.batch(j, stream=st), out, info)
@@ -437,7 +505,7 @@ def main():
     inflight = len(pps) > 1
     for t in range(args.warmup):
         step(t, inflight=inflight)
-    stream = inflight_streams[0] if inflight else torch.cuda.current_stream(device)  # where pps[0] launches
+    stream = inflight_streams[0] if len(pps) > 1 else torch.cuda.current_stream(device)  # where pps[0] launches
     e0 = torch.cuda.Event(enable_timing=True)
     e1 = torch.cuda.Event(enable_timing=True)
     if pg:
@@ -464,6 +532,25 @@ def main():
     kern_ms = e0.elapsed_time(e1) / (args.steps - ev_from)  # one launch per step
     if inflight:  # launches overlap on several streams: the launch rate is the wall-clock step
         kern_ms = wall / args.steps * 1e3
+    # One launch at a time (the kernel-quality figure, comparable with a rocprof kernel average): back-to-back launches
+    # of the same pooled workload on ONE handle and stream, HIP events on that stream from the end of the first launch
+    # to the end of the last. Without launches in flight this is the timed loop's own event figure.
+    if inflight:
+        n_single = max(args.steps, 100)
+        for t in range(10):
+            step(t)
+        s0 = torch.cuda.Event(enable_timing=True)
+        s1 = torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        for t in range(n_single):
+            step(t)
+            if t == 0:
+                s0.record(stream)
+        s1.record(stream)
+        torch.cuda.synchronize()
+        single_ms, single_n = s0.elapsed_time(s1) / (n_single - 1), n_single - 1
+    else:
+        single_ms, single_n = kern_ms, args.steps - ev_from
     # Per-launch spread (median, p10 / p90), measured after the timed region: one event
     # pair around each of up to 200 extra steps, so the timed loop above carries no per-step events.
     n_dist = min(args.steps, 200)
@@ -534,8 +621,7 @@ def main():
     if rank == 0:
         res = {
             "metric": (METRIC if args.config == "c2" else f"{METRIC} [{args.config}]")
-                      + (" [host feed, PCIe-inclusive]" if feed is not None else "")
-                      + (f" [inflight {len(pps)}]" if inflight else ""),
+                      + (" [host feed, PCIe-inclusive]" if feed is not None else ""),
             "value": round(value, 1),
             "unit": "frames/s",
             # RCCL: one rank per GPU by construction (it refuses two ranks on one device); a gloo rehearsal may put
@@ -557,13 +643,25 @@ def main():
                        "pool_sets": P, "pool_bytes": pool_bytes,
                        "pool": "each step reads a different frame set and writes a different output tensor; "
                                "pool >= 3x the 256 MiB Infinity Cache" if P > 1 else "one resident set",
+                       "launches_in_flight": len(pps),
+                       "launch": (f"step t on handle t mod {len(pps)}, each bound to its own HIP stream (PipelineServer's "
+                                  f"device runner, inflight={len(pps)}): launch t+1's ramp overlaps launch t's tail"
+                                  if inflight else "one handle, one HIP stream, launches back to back"),
                        "parallelism": f"streams s mod {world}, one process per GPU, no hot-loop collective"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "algorithmic_bytes_per_launch": alg_bytes, "mean_launch_ms": round(kern_ms, 5),
                          "event_launches": args.steps - ev_from,
-                         "timing": ("wall clock over the timed steps (launches in flight on several streams)"
+                         "timing": (f"algorithmic bytes of one step / wall-clock step time, {len(pps)} launches in "
+                                    "flight on separate streams (kernels overlap: a rocprof kernel average is longer "
+                                    "than the step; the one-at-a-time kernel figure is single_launch)"
                                     if inflight else "HIP events on the launch stream"),
+                         "single_launch": {
+                             "achieved": round(alg_bytes / (single_ms * 1e-3) / 1e9, 1),
+                             "frac": round(alg_bytes / (single_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                             "mean_launch_ms": round(single_ms, 5), "launches": single_n,
+                             "timing": "HIP events on one handle's stream, launches back to back, one at a time "
+                                       "(compare with the rocprof kernel average of a one-stream run)"},
                          "launch_ms_p10_p50_p90": [pct[10], pct[50], pct[90]], "resident": resident},
             "latency": latency,
         }
@@ -574,11 +672,15 @@ def main():
             r = res["roofline"]
             hbm = {k: r[k] for k in ("achieved", "peak", "unit", "frac", "traffic")}
             g = valu / (kern_ms * 1e-3) / 1e9
+            g1 = valu / (single_ms * 1e-3) / 1e9
             res["roofline"] = {"bound": "valu", "achieved": round(g, 1), "peak": VALU_PEAK_GINST,
                                "unit": "G wave64-VALU-inst/s", "frac": round(g / VALU_PEAK_GINST, 4),
                                "traffic": r["traffic"], "valu_insts_per_launch": valu, "hbm": hbm,
                                **{k: r[k] for k in ("algorithmic_bytes_per_launch", "mean_launch_ms", "event_launches",
-                                                    "launch_ms_p10_p50_p90", "resident")}}
+                                                    "timing", "launch_ms_p10_p50_p90", "resident")},
+                               "single_launch": dict(r["single_launch"], achieved=round(g1, 1),
+                                                     frac=round(g1 / VALU_PEAK_GINST, 4),
+                                                     hbm_frac=r["single_launch"]["frac"])}
         if feed is not None:
             res["h2d"] = {"bytes_per_step": feed.bytes_per_batch, "frame_bytes": feed.frame_bytes,
                           "rows": args.feed_rows,

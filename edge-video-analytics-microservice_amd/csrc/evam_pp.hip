@@ -1723,8 +1723,9 @@ __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
     constexpr int SV = PR ? 512 : 2 * SLOT;
     constexpr int GRP = PR ? (PK ? 1024 : 2048) : 2 * SLOT + 2 * NPC * SLOT;
     constexpr int segY = SY;
-    // I420 with PR: one buffer resource over both chroma planes, based at the lower one (the host checks that
-    // both lie within 2 GiB of it)
+    // I420 with PR: one buffer resource over both chroma planes, based at the lower one. Every byte read lies below
+    // (offset of the upper plane) + (its extent), which must stay under num_records 0x7FFFFFFF: the host admits the
+    // pairing only when that holds for every item of the launch, else the group runs unpaired
     const uint8_t* const pcl = NPC == 2 && PR ? (p1 < p2 ? p1 : p2) : p1;
     const uint32_t dU = (uint32_t)(p1 - pcl), dV = (uint32_t)(p2 - pcl);
     const __amdgpu_buffer_rsrc_t rsC2 = __builtin_amdgcn_make_buffer_rsrc((void*)pcl, (short)0, 0x7FFFFFFF, 0x00020000);
@@ -4268,7 +4269,17 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
                     memcpy(&rr[pos], &r, sizeof(RoiRec));
                 }
             }
-            if (dyn_wc) _mm_sfence();  // the records reach device memory before the launch's doorbell
+            if (dyn_wc && nu > 0) {
+                // The records reach device memory before the launch's doorbell. The fence only drains this core's
+                // write-combining buffers into the PCIe posted-write stream; a read of the last written line cannot
+                // complete ahead of those posted writes, so once it returns every record is in device memory (the
+                // HIP runtime publishes host-written device kernel arguments the same way: a read-back of the last
+                // byte after the fence).
+                _mm_sfence();
+                _mm_mfence();
+                (void)*reinterpret_cast<const volatile uint32_t*>(reinterpret_cast<const uint8_t*>(&rr[nu - 1]) +
+                                                                  sizeof(RoiRec) - 4);
+            }
             const int nrec = nu;
             qrec[f] = nrec;
         }
@@ -4330,14 +4341,16 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
                 int pr = 0, spx = 0, lds = 0, grid = 0;
                 const XTab* hx = reinterpret_cast<const XTab*>(h->h_block.data() + tab_off[f]);
                 // I420 paired chroma addresses both chroma planes from one buffer resource based at the lower one:
-                // every item's U and V planes must lie within 1 GiB of each other (else no pairing for the group)
+                // for every item, the upper plane's offset from the lower plus its extent must fit the resource's
+                // 0x7FFFFFFF bytes (else no pairing for the group)
                 bool pair_ok = true;
                 if (f == kI420 && kn.strip_pair)
                     for (int m = mfirst[f]; m < mfirst[f + 1] && pair_ok; m++) {
                         const int i = members[m];
                         const evam_image& sr = srcs[items ? items[i].src_index : i];
                         const int64_t d = (int64_t)((intptr_t)sr.planes[2] - (intptr_t)sr.planes[1]);
-                        pair_ok = d > -(int64_t(1) << 30) && d < (int64_t(1) << 30);
+                        const int64_t ext = (int64_t)sr.pitch[d >= 0 ? 2 : 1] * (sr.height / 2);
+                        pair_ok = (d >= 0 ? d : -d) + ext <= (int64_t)0x7FFFFFFF;
                     }
                 if (plan_strip(f, g0, DW, DH, count[f], cfg->out_dtype, h->n_cu, hx, reinterpret_cast<const YTab*>(hx + DW),
                                x0_mask[f], kn, pair_ok, *tp, pr, spx, lds, grid)) {

@@ -70,3 +70,28 @@ def test_reduce_run_gloo_world2():
         assert el == 2.0                 # max over ranks
         assert frames == 64 and nbytes == 6400
         assert per == [32, 32]
+
+
+def test_bench_rank_envs():
+    """bench.py --gpus N without a launcher: the environment of each rank is torchrun's (RANK = LOCAL_RANK = r,
+    WORLD_SIZE = N, one rendezvous on 127.0.0.1)."""
+    import bench
+
+    envs = bench.rank_envs(4, {"PATH": "/bin", "RANK": "9"}, 29999)
+    assert [e["RANK"] for e in envs] == ["0", "1", "2", "3"]
+    assert [e["LOCAL_RANK"] for e in envs] == ["0", "1", "2", "3"]
+    assert {e["WORLD_SIZE"] for e in envs} == {"4"} and {e["LOCAL_WORLD_SIZE"] for e in envs} == {"4"}
+    assert {(e["MASTER_ADDR"], e["MASTER_PORT"]) for e in envs} == {("127.0.0.1", "29999")}
+    assert all(e["PATH"] == "/bin" for e in envs)
+
+
+def test_bench_gpus_without_devices_exits_nonzero():
+    """--gpus 2 under RCCL with fewer visible GPUs than ranks (none here) exits non-zero before any rank starts."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "EVAM_BENCH_BACKEND")}
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2"], env=env, capture_output=True,
+                       text=True, timeout=120)
+    assert p.returncode == 2 and "visible GPU" in p.stderr and not p.stdout.strip()

@@ -89,3 +89,36 @@ def test_bench_rccl_reduction_path_one_rank(gpu, tmp_path):
     assert p.returncode == 0, p.stderr[-2000:]
     d = json.loads(p.stdout.strip().splitlines()[-1])
     assert d["n_gpus"] == 1 and d["ranks"] == 1 and d["value"] > 0
+
+
+def _bench_env(**kw):
+    env = dict(os.environ, **kw)
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT", "EVAM_BENCH_PG"):
+        env.pop(k, None)
+    return env
+
+
+def test_bench_gpus2_launches_two_ranks(gpu):
+    """`bench.py --gpus 2` with no launcher starts two ranks itself. On this one-GPU box the gloo
+    rehearsal shares the device: rank 0's line reports both ranks and the frames of both."""
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "10", "--warmup", "3",
+                        "--no-cpu-baseline", "--resident-steps", "0"], env=_bench_env(EVAM_BENCH_BACKEND="gloo"),
+                       capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [ln for ln in p.stdout.strip().splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]  # rank 0 prints the one line
+    d = json.loads(lines[0])
+    assert d["ranks"] == 2 and d["n_gpus"] == 1 and d["value"] > 0
+    assert d["config"]["frames_per_gpu_per_step"] == 32
+
+
+def test_bench_gpus2_rccl_refuses_one_gpu(gpu):
+    """Under RCCL each rank needs its own GPU: --gpus 2 on a one-GPU box exits non-zero, never times one rank."""
+    import torch
+
+    if torch.cuda.device_count() >= 2:
+        pytest.skip("more than one GPU visible")
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "10", "--warmup", "3",
+                        "--no-cpu-baseline"], env=_bench_env(), capture_output=True, text=True, timeout=120)
+    assert p.returncode != 0
+    assert "visible GPU" in p.stderr and not p.stdout.strip()

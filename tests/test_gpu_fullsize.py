@@ -260,3 +260,36 @@ def test_inflight_two_streams_bit_equal(evam, gpu, config):
         assert torch.equal(a.view(torch.int32), b.view(torch.int32))
     for p in pps:
         p.close()
+
+
+@pytest.mark.parametrize("rec_device", ["1", "0"])
+def test_c3_roi_ring_full_queue(evam, gpu, rec_device, monkeypatch):
+    """The ROI record ring under a full queue: 48 back-to-back C3-size calls (1,600 ROIs
+    each, a different seeded ROI set every call, a different output tensor every call) with no host work or sync
+    between them, so the 16 record slots wrap three times while the GPU still runs earlier calls and every slot is
+    rewritten behind its fence. Records in host-written device memory (default) and in pinned host memory. Every
+    output equals the same call run alone and synchronised, bit for bit (that single-call result is pinned against the
+    oracle by test_c3_bench_roi_set)."""
+    import torch
+
+    monkeypatch.setenv("EVAM_PP_REC_DEVICE", rec_device)
+    wl = bench.WORKLOADS["c3"]
+    batch = evam.ImageBatch(bench.device_frames(evam, torch, wl, 32, gpu, seed=1234))
+    info = bench.make_info(evam, wl)
+    n_calls = 48
+    sets = [evam.RoiBatch(np.array(bench.seed_rois(wl["rois"], 32, *wl["src"], seed=500 + k), dtype=np.int32))
+            for k in range(n_calls)]
+    assert all(len(s) == 1600 for s in sets)
+    pp = evam.HipPreProcessor(device=0)
+    outs = [torch.full((1600, 3, 72, 72), 7.0, device=gpu) for _ in range(n_calls)]
+    torch.cuda.synchronize()
+    for k in range(n_calls):
+        pp.convert(batch, outs[k], info, rois=sets[k])
+    torch.cuda.synchronize()
+    assert pp.stats().kernels == evam.native.KERNEL_ROI
+    ref = torch.full((1600, 3, 72, 72), 7.0, device=gpu)
+    for k in range(n_calls):
+        pp.convert(batch, ref, info, rois=sets[k])
+        torch.cuda.synchronize()
+        assert torch.equal(outs[k].view(torch.int32), ref.view(torch.int32)), f"call {k} (rec_device={rec_device})"
+    pp.close()

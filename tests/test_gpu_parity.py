@@ -657,11 +657,12 @@ def test_roi_tail_split(evam, O, coracle, gpu, tail, dst, monkeypatch):
 
 
 
-@pytest.mark.parametrize("layout", ["v_first", "u_first", "far_apart"])
+@pytest.mark.parametrize("layout", ["v_first", "u_first", "far_apart", "beyond_2g"])
 def test_i420_paired_chroma_plane_layouts(evam, O, coracle, gpu, layout):
     """Strip kernel with paired taps on I420: both chroma planes are read through one buffer resource based at the
-    lower plane (U and V segments of both source rows in one LDS-DMA instruction). V below U, U below V, and planes
-    more than 1 GiB apart (no pairing for that group: one row per instruction) all equal the oracle."""
+    lower plane (U and V segments of both source rows in one LDS-DMA instruction). V below U, U below V, planes 1 GiB
+    apart (still paired: the upper plane ends inside the resource's 0x7FFFFFFF bytes) and planes 2 GiB apart (no
+    pairing for that group: one row per instruction) all equal the oracle."""
     import torch
 
     rng = np.random.default_rng(2024)
@@ -670,7 +671,7 @@ def test_i420_paired_chroma_plane_layouts(evam, O, coracle, gpu, layout):
     imgs = []
     for f in frames:
         y, u, v = (np.ascontiguousarray(p) for p in f.planes)
-        gap = (1 << 30) + 4096 if layout == "far_apart" else 4096
+        gap = {"far_apart": (1 << 30) + 4096, "beyond_2g": (2 << 30) + 4096}.get(layout, 4096)
         total = y.nbytes + u.nbytes + v.nbytes + gap + 3 * 256
         buf = torch.zeros(total, dtype=torch.uint8, device=gpu)
 
@@ -685,7 +686,7 @@ def test_i420_paired_chroma_plane_layouts(evam, O, coracle, gpu, layout):
             ut, o = put(o, u)
         else:
             ut, o = put(o, u)
-            o = (o + gap) // 256 * 256 if layout == "far_apart" else o
+            o = (o + gap) // 256 * 256 if layout in ("far_apart", "beyond_2g") else o
             vt, o = put(o, v)
         yt, o = put(o, y)
         imgs.append(evam.Image(O.I420, W, H, [yt, ut, vt]))

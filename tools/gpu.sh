@@ -11,7 +11,9 @@
 #   feed:c2,c4        bench.py --feed host (PCIe-inclusive) lines -> gpurun_out/bench_TAG_feed_<cfg>.json
 #   pipe              bench.py --via pipeline (C2 through PipelineServer) + its own rocprof kernel stats
 #   bench:c1,c2,...   one bench line per config (BENCH_STEPS, default 1000; CPU baseline unless CPU=0)
-#   prof:c1,c2,...    rocprofv3 --kernel-trace --stats per config (tools/prof_configs.sh, 200 steps)
+#   prof:c1,c2,...    rocprofv3 --kernel-trace --stats per config (tools/prof_configs.sh, 200 steps, bench default:
+#                     two launches in flight)
+#   prof1:c1,c2,...   the same, one launch at a time (--inflight 1: the kernel-quality average) -> prof_TAG_single_*
 #   pmc:c2,c3,...     FETCH_SIZE / WRITE_SIZE passes per config (tools/pmc.sh) -> pmc_traffic_TAG_<cfg>.json
 #   valu:c1,...       SQ_INSTS_VALU pass per config (tools/pmc.sh)
 #   stall:c1,...      stall-attribution passes per config (tools/pmc.sh, two SQ groups)
@@ -77,6 +79,8 @@ PY
       done ;;
     prof)
       STEPS=200 bash tools/prof_configs.sh "$TAG" "$cfgs" ;;
+    prof1)
+      PROF_ARGS="--inflight 1" STEPS=200 bash tools/prof_configs.sh "${TAG}_single" "$cfgs" ;;
     pmc)
       for c in $cfgs; do
         PMC_GROUPS="FETCH_SIZE;WRITE_SIZE" bash tools/pmc.sh "${TAG}_$c" "$c"

@@ -1,6 +1,7 @@
 #!/bin/bash
 # Plain bench.py lines (no profiler) of one config under several EVAM_PP_* settings, alternating, two passes.
-# Usage: tools/gpu_env_ab.sh TAG CFG "SET1|SET2|..."   (a SET is space-separated VAR=VALUE pairs)
+# Usage: tools/gpu_env_ab.sh TAG CFG "SET1|SET2|..."   (a SET is space-separated VAR=VALUE pairs and/or bench.py
+# options such as --inflight=1)
 set -euo pipefail
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$ROOT"; mkdir -p gpurun_out
@@ -9,7 +10,10 @@ for pass in 1 2; do
   k=0
   for s in "${LIST[@]}"; do
     f=gpurun_out/envab_${TAG}_${CFG}_${k}_$pass.json; k=$((k + 1))
-    env $s timeout -k 10 120 python bench.py --config $CFG --steps 1000 --warmup 100 --no-cpu-baseline --resident-steps 0 > $f 2>/dev/null
+    envs=(); opts=()
+    for w in $s; do case "$w" in --*) opts+=("$w") ;; *) envs+=("$w") ;; esac; done
+    env "${envs[@]}" timeout -k 10 120 python bench.py --config $CFG --steps ${AB_STEPS:-1000} --warmup 100 --no-cpu-baseline \
+      --resident-steps 0 "${opts[@]}" > $f 2>/dev/null
     python -c "import json; d=json.load(open('$f')); print('$CFG [$s]', d['value'], d['ms_per_step'], d['roofline']['frac'])" | tee -a gpurun_out/envab_$TAG.txt
   done
 done

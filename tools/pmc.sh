@@ -1,5 +1,5 @@
 #!/bin/bash
-# PMC passes over the default bench (one counter group per rocprofv3 run, kernel-trace/stats only,
+# PMC passes over the default bench, one launch at a time (--inflight 1: per-dispatch counters of one kernel; one counter group per rocprofv3 run, kernel-trace/stats only,
 # never combined with sys/runtime tracing). Per run at most 8 SQ_, 4 TCC_, 4 TCP_, 2 TA_, 2 TD_, 2 GRBM_ counters. Output: gpurun_out/pmc_<tag>/<pass>/...counter_collection.csv
 set -euo pipefail
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
@@ -21,7 +21,7 @@ fi
 for grp in "${GROUPS_DEFAULT[@]}"; do
   i=$((i+1))
   timeout -k 10 240 rocprofv3 --pmc $grp --output-format csv -d "$OUT/p$i" -o run -- \
-    python3 "$ROOT/bench.py" --config "$CFG" --steps 20 --warmup 5 --no-cpu-baseline --resident-steps 0 ${PMC_BENCH_ARGS:-} > "$OUT/p$i.json" 2> "$OUT/p$i.err" \
+    python3 "$ROOT/bench.py" --config "$CFG" --steps 20 --warmup 5 --no-cpu-baseline --resident-steps 0 --inflight 1 ${PMC_BENCH_ARGS:-} > "$OUT/p$i.json" 2> "$OUT/p$i.err" \
     || { echo "pass $i ($grp) failed"; tail -5 "$OUT/p$i.err"; exit 1; }
 done
 FR=$(python3 -c "import json;print(json.load(open('$OUT/p1.json'))['config']['frames_per_gpu_per_step'])")
