@@ -47,11 +47,11 @@ DTYPE_U8, DTYPE_F32 = 0, 1
 NORM_RANGE, NORM_MEAN_STD = 1, 2
 OPT_STATS, OPT_TIMING = 1, 2
 
-ABI_VERSION = 1
+ABI_VERSION = 2  # 2: evam_pp_run_slots
 
 # Every symbol include/evam_pp.h declares.
 EXPORTED_SYMBOLS = (
-    "evam_pp_create", "evam_pp_run", "evam_pp_sync", "evam_pp_set_stream", "evam_pp_set_option",
+    "evam_pp_create", "evam_pp_run", "evam_pp_run_slots", "evam_pp_sync", "evam_pp_set_stream", "evam_pp_set_option",
     "evam_pp_get_stats", "evam_pp_destroy", "evam_pp_last_error", "evam_pp_abi_version",
     "evam_pp_linear_table",
 )
@@ -108,6 +108,9 @@ def _declare(lib: ctypes.CDLL) -> ctypes.CDLL:
     lib.evam_pp_run.argtypes = [vp, P(EvamImage), ctypes.c_int, P(EvamRoi), ctypes.c_int, P(EvamPreproc),
                                 P(EvamTensor), P(EvamTransform)]
     lib.evam_pp_run.restype = ctypes.c_int
+    lib.evam_pp_run_slots.argtypes = [vp, P(EvamImage), ctypes.c_int, P(EvamRoi), ctypes.c_int, P(EvamPreproc),
+                                      P(EvamTensor), P(c_i32), P(EvamTransform)]
+    lib.evam_pp_run_slots.restype = ctypes.c_int
     lib.evam_pp_sync.argtypes = [vp]
     lib.evam_pp_sync.restype = ctypes.c_int
     lib.evam_pp_set_stream.argtypes = [vp, vp]

@@ -3717,6 +3717,7 @@ struct evam_pp {
     std::vector<int> sc_units;     // ROI work units: (item, row0, row1, cost)
     std::vector<int> sc_start;     // ROI unit counting sort: bucket starts
     std::vector<int> sc_slot;      // ROI units in launch order
+    std::vector<uint8_t> sc_seen;  // evam_pp_run_slots: output slots taken
     int memo_key[4] = {-1, -1, -1, -1};  // (format, staging buffer, row cap, DH) of memo_rg
     std::vector<uint32_t> memo_rg;       // per crop width: rows per group | groups of the whole height << 16
     TParams sc_tparams;            // strip-kernel arguments (3.5 KB: kept off the stack)
@@ -3875,8 +3876,15 @@ int evam_pp_linear_table(int src_size, int dst_size, int is_x, int32_t* ofs, int
     return EVAM_PP_OK;
 }
 
-int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* items, int n_items,
-                const evam_preproc* cfg, const evam_tensor* dst, evam_transform* out_xform) {
+}  // extern "C"
+
+namespace {
+
+// evam_pp_run and evam_pp_run_slots. slots == NULL: item i -> slot dst->slot_offset + i * dst->slot_stride; else item i
+// -> slot slots[i]. The kernels read one output index per item (ItemArg / ItemDesc .index, RoiRec .item) and compute
+// slot = slot_offset + index * slot_stride, so an explicit table travels as index = slots[i], offset 0, stride 1.
+int run_impl(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* items, int n_items, const evam_preproc* cfg,
+             const evam_tensor* dst, const int32_t* slots, evam_transform* out_xform) {
     HP_START;
     if (!h || !srcs || !cfg || !dst) return fail(EVAM_PP_ERR_INVALID_ARG, "evam_pp_run: NULL argument");
     if (n_srcs <= 0) return fail(EVAM_PP_ERR_INVALID_ARG, "evam_pp_run: n_srcs must be > 0");
@@ -3937,13 +3945,28 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
     int max_cw[4] = {0, 0, 0, 0}, max_ch[4] = {0, 0, 0, 0};
     uint32_t x0_mask[4] = {0, 0, 0, 0};  // crop origins x0 mod 32 present (wave-kernel staging bound)
     bool uniform[4] = {true, true, true, true};
-    // output slots are linear in the item index: the first and the last bound them all
-    for (int i : {0, n_items - 1}) {
-        const int64_t slot = (int64_t)dst->slot_offset + (int64_t)i * dst->slot_stride;
-        if (slot < 0 || slot >= dst->n)
-            return fail(EVAM_PP_ERR_INVALID_ARG, "evam_pp_run: item %d -> slot %lld outside tensor batch %d", i,
-                        (long long)slot, dst->n);
+    if (slots) {
+        // an explicit slot per item: each inside the batch, no two items into one slot
+        std::vector<uint8_t>& seen = h->sc_seen;
+        seen.assign((size_t)dst->n, 0);
+        for (int i = 0; i < n_items; i++) {
+            const int32_t sl = slots[i];
+            if (sl < 0 || sl >= dst->n)
+                return fail(EVAM_PP_ERR_INVALID_ARG, "evam_pp_run_slots: slots[%d] = %d outside tensor batch %d", i, sl,
+                            dst->n);
+            if (seen[sl]++)
+                return fail(EVAM_PP_ERR_INVALID_ARG, "evam_pp_run_slots: slot %d given to two items (slots[%d])", sl, i);
+        }
+    } else {
+        // output slots are linear in the item index: the first and the last bound them all
+        for (int i : {0, n_items - 1}) {
+            const int64_t slot = (int64_t)dst->slot_offset + (int64_t)i * dst->slot_stride;
+            if (slot < 0 || slot >= dst->n)
+                return fail(EVAM_PP_ERR_INVALID_ARG, "evam_pp_run: item %d -> slot %lld outside tensor batch %d", i,
+                            (long long)slot, dst->n);
+        }
     }
+    const int slot_offset = slots ? 0 : dst->slot_offset, slot_stride = slots ? 1 : dst->slot_stride;
     std::vector<int>& sfmt = h->sc_sfmt;  // per source: format id (looked up once, not per ROI)
     sfmt.resize(n_srcs);
     bool one_fmt = true, one_size = true;
@@ -4123,7 +4146,7 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
                     const Geom& g = geo[i];
                     d.x0 = g.x0; d.y0 = g.y0; d.cw = g.cw; d.ch = g.ch;
                     d.rw = g.rw; d.rh = g.rh; d.ox = g.ox; d.oy = g.oy;
-                    d.index = i;  // the slot offset / stride are launch parameters: the block survives clip-ring steps
+                    d.index = slots ? slots[i] : i;  // the slot offset / stride are launch parameters: the block survives clip-ring steps
                     d.pad_ = 0;
                     d.scale_x = 1. / ((double)g.rw / g.cw);
                     d.scale_y = 1. / ((double)g.rh / g.ch);
@@ -4258,7 +4281,7 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
                 r.width = (uint16_t)sim.width; r.height = (uint16_t)sim.height;
                 if (items) { r.x = items[i].x; r.y = items[i].y; r.w = items[i].w; r.h = items[i].h; }
                 else { r.x = r.y = r.w = r.h = 0; }  // w <= 0: the full frame
-                r.item = i;
+                r.item = slots ? slots[i] : i;
                 r.row0 = (uint16_t)un[4 * u + 1];
                 r.row1 = (uint16_t)un[4 * u + 2];
                 if (dyn_wc) {  // write-combined device memory: the 64-byte line as four streaming stores
@@ -4307,7 +4330,7 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
             for (int p = 0; p < 3; p++) { a[k].plane[p] = s.planes[p]; a[k].pitch[p] = s.pitch[p]; }
             a[k].x0 = geo[i].x0;
             a[k].y0 = geo[i].y0;
-            a[k].index = i;
+            a[k].index = slots ? slots[i] : i;
         }
     };
     for (int f = 0; f < 4; f++) {
@@ -4319,8 +4342,8 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
             q.dst = dst->data;
             q.mode = cfg->resize_mode;
             q.placement = cfg->placement;
-            q.slot_offset = dst->slot_offset;
-            q.slot_stride = dst->slot_stride;
+            q.slot_offset = slot_offset;
+            q.slot_stride = slot_stride;
             q.color_rgb = color_rgb;
             q.fill = fill;
             q.prio = kn.prio;
@@ -4356,8 +4379,8 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
                                x0_mask[f], kn, pair_ok, *tp, pr, spx, lds, grid)) {
                     tp->lut = lut_d;
                     tp->dst = dst->data;
-                    tp->slot_offset = dst->slot_offset;
-                    tp->slot_stride = dst->slot_stride;
+                    tp->slot_offset = slot_offset;
+                    tp->slot_stride = slot_stride;
                     tp->color_rgb = color_rgb;
                     tp->fill = fill;
                     tp->prio = kn.prio;
@@ -4385,8 +4408,8 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
                               x0_mask[f], kn, *tp, bpx, dd, nw, lds)) {
                     tp->lut = lut_d;
                     tp->dst = dst->data;
-                    tp->slot_offset = dst->slot_offset;
-                    tp->slot_stride = dst->slot_stride;
+                    tp->slot_offset = slot_offset;
+                    tp->slot_stride = slot_stride;
                     tp->color_rgb = color_rgb;
                     tp->fill = fill;
                     tp->prio = kn.prio;
@@ -4419,8 +4442,8 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
                     w.xtab = xt_d;
                     w.ytab = yt_d;
                     w.dst = dst->data;
-                    w.slot_offset = dst->slot_offset;
-                    w.slot_stride = dst->slot_stride;
+                    w.slot_offset = slot_offset;
+                    w.slot_stride = slot_stride;
                     w.color_rgb = color_rgb;
                     w.fill = fill;
                     for (int m0 = mfirst[f]; m0 < mfirst[f + 1]; m0 += kArgItems) {
@@ -4461,8 +4484,8 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
                 sp.xtab = xt_d;
                 sp.ytab = yt_d;
                 sp.dst = dst->data;
-                sp.slot_offset = dst->slot_offset;
-                sp.slot_stride = dst->slot_stride;
+                sp.slot_offset = slot_offset;
+                sp.slot_stride = slot_stride;
                 sp.DW = DW; sp.DH = DH;
                 const int tw = 64 * nsegx;
                 sp.tiles_x = (DW + tw - 1) / tw;
@@ -4510,8 +4533,8 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
             r.xtab = xt_d;
             r.ytab = yt_d;
             r.dst = dst->data;
-            r.slot_offset = dst->slot_offset;
-            r.slot_stride = dst->slot_stride;
+            r.slot_offset = slot_offset;
+            r.slot_stride = slot_stride;
             r.DW = DW; r.DH = DH;
             r.TW = rc.TW; r.TH = rc.TH;
             r.tiles_x = (DW + rc.TW - 1) / rc.TW;
@@ -4537,8 +4560,8 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
         p.items = items_d;
         p.lut = lut_d;
         p.dst = dst->data;
-        p.slot_offset = dst->slot_offset;
-        p.slot_stride = dst->slot_stride;
+        p.slot_offset = slot_offset;
+        p.slot_stride = slot_stride;
         p.DW = DW; p.DH = DH;
         p.TW = t.TW; p.TH = t.TH;
         p.tiles_x = (DW + t.TW - 1) / t.TW;
@@ -4588,6 +4611,21 @@ int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* 
     h->stats.src_bytes = h->opt_stats ? src_bytes : 0;
     h->stats.dst_bytes = (int64_t)n_items * plane * 3 * esz;
     return EVAM_PP_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* items, int n_items,
+                const evam_preproc* cfg, const evam_tensor* dst, evam_transform* out_xform) {
+    return run_impl(h, srcs, n_srcs, items, n_items, cfg, dst, nullptr, out_xform);
+}
+
+int evam_pp_run_slots(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* items, int n_items,
+                      const evam_preproc* cfg, const evam_tensor* dst, const int32_t* slots, evam_transform* out_xform) {
+    if (!slots) return fail(EVAM_PP_ERR_INVALID_ARG, "evam_pp_run_slots: slots is NULL");
+    return run_impl(h, srcs, n_srcs, items, n_items, cfg, dst, slots, out_xform);
 }
 
 }  // extern "C"

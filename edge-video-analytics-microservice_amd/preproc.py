@@ -368,11 +368,13 @@ class HipPreProcessor:
 
     # -- the hot path ------------------------------------------------------------------------------
     def convert(self, srcs, out, info: PreProcInfo | None = None, rois: Iterable | None = None,
-                slot_offset: int = 0, slot_stride: int = 1, want_transform: bool = False):
+                slot_offset: int = 0, slot_stride: int = 1, want_transform: bool = False, slots=None):
         """Pre-process ``srcs`` (or ``rois`` of them) into ``out`` ([N,3,H,W] uint8/float32, device).
 
         ``srcs``: an :class:`ImageBatch` (marshalled once) or a sequence of :class:`Image`.
         ``rois``: a :class:`RoiBatch`, an ``int32 [n, 5]`` array or a sequence of :class:`Roi`.
+        Item i goes to slot ``slot_offset + i * slot_stride`` of ``out``, or to ``slots[i]`` when ``slots`` (one
+        distinct slot per item, ``evam_pp_run_slots``) is given.
         Returns a list of :class:`Transform` when ``want_transform`` (``"lazy"``: a :class:`Transforms`
         sequence that builds each on access). Asynchronous on the current
         torch stream of ``self.device`` (or the stream given at construction).
@@ -400,7 +402,16 @@ class HipPreProcessor:
             items_p = None
         xf = (N.EvamTransform * n_items)() if want_transform else None
         self._bind_stream()
-        rc = self._run(self._h, batch.c_array, len(batch), items_p, n_items, cached, ctypes.byref(t), xf)
+        if slots is not None:
+            import numpy as np
+
+            sl = np.ascontiguousarray(slots, dtype=np.int32)
+            if sl.shape != (n_items,):
+                raise PreProcError(N.ERR_INVALID_ARG, f"slots must hold one slot per item ({n_items}), got {sl.shape}")
+            rc = self._lib.evam_pp_run_slots(self._h, batch.c_array, len(batch), items_p, n_items, cached,
+                                             ctypes.byref(t), sl.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), xf)
+        else:
+            rc = self._run(self._h, batch.c_array, len(batch), items_p, n_items, cached, ctypes.byref(t), xf)
         if rc:
             N.check(self._lib, rc)
         if not want_transform:

@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define EVAM_PP_ABI_VERSION 1
+#define EVAM_PP_ABI_VERSION 2 /* 2: evam_pp_run_slots */
 
 /* DL Streamer FourCC values: fourcc(a,b,c,d) = a | b<<8 | c<<16 | d<<24. */
 enum evam_fourcc {
@@ -156,6 +156,16 @@ int evam_pp_create(int hip_device, void* hip_stream, evam_pp** out);
  * into dst. out_xform: NULL or an array of n_items. Asynchronous on the handle's stream. */
 int evam_pp_run(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* items, int n_items,
                 const evam_preproc* cfg, const evam_tensor* dst, evam_transform* out_xform);
+
+/* evam_pp_run with an explicit output slot per item: item i is written to slot slots[i] of dst (dst->slot_offset
+ * and dst->slot_stride are ignored). slots is a HOST array of n_items distinct values in [0, dst->n); a value
+ * outside it or a slot given twice is EVAM_PP_ERR_INVALID_ARG. One launch can then write the new frames of many
+ * camera streams into a shared [S,16,3,H,W] clip ring, each at its own stream's slot s*16 + t_s % 16, where the
+ * reference's gvaactionrecognitionbin (pipelines/action_recognition/general/pipeline.json:3-4) pre-processes one
+ * stream's frame per encoder call. */
+int evam_pp_run_slots(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* items, int n_items,
+                      const evam_preproc* cfg, const evam_tensor* dst, const int32_t* slots,
+                      evam_transform* out_xform);
 
 int evam_pp_sync(evam_pp* h);
 int evam_pp_set_stream(evam_pp* h, void* hip_stream);

@@ -47,6 +47,8 @@ def test_null_arguments_rejected(evam):
     lib = evam.load_library()
     assert lib.evam_pp_run(None, None, 0, None, 0, None, None, None) == evam.native.ERR_INVALID_ARG
     assert b"NULL" in lib.evam_pp_last_error()
+    assert lib.evam_pp_run_slots(None, None, 0, None, 0, None, None, None, None) == evam.native.ERR_INVALID_ARG
+    assert b"slots is NULL" in lib.evam_pp_last_error()
     assert lib.evam_pp_sync(None) == evam.native.ERR_INVALID_ARG
     assert lib.evam_pp_create(0, None, None) == evam.native.ERR_INVALID_ARG
     lib.evam_pp_destroy(None)  # no-op

@@ -697,3 +697,46 @@ def test_i420_paired_chroma_plane_layouts(evam, O, coracle, gpu, layout):
     pp.close()
     ref, _ = run_oracle(O, coracle, frames, (2, 3, 256, 256), "f32", info)
     assert_same(got, ref, f"I420 paired chroma, {layout}")
+
+
+@pytest.mark.parametrize("kind", ["strip", "band", "wave", "staged", "roi", "generic"])
+def test_run_slots_explicit_output_slots(evam, O, coracle, gpu, kind, monkeypatch):
+    """evam_pp_run_slots: item i lands in slot slots[i] (a permutation with gaps over a larger tensor, as a shared
+    clip ring indexed s*16 + t_s % 16 gets), on every kernel family; untouched slots keep their value. Out-of-range
+    and repeated slots are refused before anything launches."""
+    import torch
+
+    env = {"strip": {}, "band": {"EVAM_PP_BAND": "2", "EVAM_PP_STRIP": "0"}, "wave": {"EVAM_PP_WAVE": "2"},
+           "staged": {"EVAM_PP_STRIP": "0", "EVAM_PP_WAVE": "0"}, "roi": {}, "generic": {"EVAM_PP_ROI": "0"}}[kind]
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    rng = np.random.default_rng(zlib.crc32(f"slots{kind}".encode()))
+    up = kind in ("band", "wave")
+    W, H = (120, 64) if up else (640, 360)
+    frames = [O.random_frame(rng, O.NV12, W, H, pattern="gradient" if i % 2 else "uniform") for i in range(6)]
+    imgs = upload(evam, frames, gpu)
+    info = evam.PreProcInfo(resize="aspect-ratio", crop="central", range=(0.0, 1.0), mean=(0.1, 0.2, 0.3),
+                            std=(0.3, 0.2, 0.1))
+    rois = None
+    if kind in ("roi", "generic"):
+        rois = [(i % 6, int(rng.integers(0, W // 2)), int(rng.integers(0, H // 2)), int(rng.integers(16, W // 2)),
+                 int(rng.integers(16, H // 2))) for i in range(9)]
+    n = len(rois) if rois else 6
+    dst = (96, 96) if not up else (200, 160)
+    slots = [5 * 16 + 3, 0, 17, 2 * 16 + 15, 31, 3 * 16 + 8, 4 * 16, 1, 70][:n]
+    out = torch.full((96, 3, dst[1], dst[0]), 7.0, device=gpu)
+    pp = evam.HipPreProcessor(device=0)
+    pp.convert(imgs, out, info, rois=[evam.Roi(*r) for r in rois] if rois else None, slots=slots)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy()
+    ref, _ = run_oracle(O, coracle, frames, (n, 3, dst[1], dst[0]), "f32", info, rois=rois)
+    for i, s in enumerate(slots):
+        assert_same(got[s], ref[i], f"run_slots {kind} item {i} -> slot {s}")
+    rest = np.setdiff1d(np.arange(96), slots)
+    assert (got[rest] == 7.0).all()
+    for bad in ([0] * n, [96] + slots[1:], [-1] + slots[1:]):
+        with pytest.raises(evam.PreProcError):
+            pp.convert(imgs, out, info, rois=[evam.Roi(*r) for r in rois] if rois else None, slots=bad)
+    with pytest.raises(evam.PreProcError):
+        pp.convert(imgs, out, info, rois=[evam.Roi(*r) for r in rois] if rois else None, slots=slots[:-1])
+    pp.close()
