@@ -198,6 +198,17 @@ PIPE_TEMPLATE = {
     "parameters": {"type": "object", "properties": {
         "detection-properties": {"element": {"name": "detection", "format": "element-properties"}}}},
 }
+ACTION_TEMPLATE = {
+    "type": "GStreamer",
+    "template": ["{auto_source} ! decodebin",
+                 " ! gvaactionrecognitionbin enc-model={models[bench_action][1][network]} "
+                 "model-proc={models[bench_action][1][proc]} name=action",
+                 " ! gvametaconvert name=metaconvert ! appsink name=appsink"],
+    "description": "bench: action-recognition encoder pre-processing (clip ring, no decoder) through the "
+                   "pipeline-server counterpart",
+    "parameters": {"type": "object", "properties": {
+        "action-properties": {"element": {"name": "action", "format": "element-properties"}}}},
+}
 IR_STUB = ('<?xml version="1.0"?><net name="bench_detector" version="11"><layers><layer id="0" name="data" '
            'type="Parameter" version="opset1"><data shape="1,3,{h},{w}" element_type="f32"/></layer></layers></net>')
 
@@ -211,17 +222,23 @@ def via_pipeline(args, evam, torch, wl, device_index):
     import tempfile
 
     ps = evam.pipeline_server
+    action = bool(wl.get("ring"))
     tmp = tempfile.mkdtemp(prefix="evam_bench_")
-    pdir = os.path.join(tmp, "pipelines", "object_detection", "bench")
+    kind, net = ("action_recognition", "bench_action") if action else ("object_detection", "bench_detector")
+    pdir = os.path.join(tmp, "pipelines", kind, "bench")
     os.makedirs(pdir)
-    json.dump(PIPE_TEMPLATE, open(os.path.join(pdir, "pipeline.json"), "w"))
+    json.dump(ACTION_TEMPLATE if action else PIPE_TEMPLATE, open(os.path.join(pdir, "pipeline.json"), "w"))
     DW, DH = wl["dst"]
-    mdir = os.path.join(tmp, "models", "bench_detector", "1")
+    mdir = os.path.join(tmp, "models", net, "1")
     os.makedirs(os.path.join(mdir, "FP32"))
-    open(os.path.join(mdir, "FP32", "bench_detector.xml"), "w").write(IR_STUB.format(w=DW, h=DH))
-    proc = {"input_preproc": [{"format": "image", "params": {"range": [0.0, 1.0], "mean": list(BGR_MEAN),
-                                                             "std": list(BGR_STD)}}] if wl["norm"] else []}
-    json.dump(proc, open(os.path.join(mdir, "bench_detector.json"), "w"))
+    open(os.path.join(mdir, "FP32", f"{net}.xml"), "w").write(IR_STUB.format(w=DW, h=DH))
+    params = {}
+    if wl["norm"]:
+        params.update(range=[0.0, 1.0], mean=list(BGR_MEAN), std=list(BGR_STD))
+    if wl["mode"] == "aspect-ratio":
+        params.update(resize="aspect-ratio", **({"crop": wl["crop"]} if wl.get("crop") else {}))
+    proc = {"input_preproc": [{"format": "image", "params": params}] if params else []}
+    json.dump(proc, open(os.path.join(mdir, f"{net}.json"), "w"))
     empty = torch.full((1, 1, 7), -1.0)
 
     def detector(t):
@@ -232,7 +249,8 @@ def via_pipeline(args, evam, torch, wl, device_index):
                              "device": device_index, "batch_max": args.hub_batch, "batch_wait_ms": 1.0,
                              "batch_target": args.hub_batch, "runner": args.runner,
                              "inflight": args.runner_inflight})
-    ps.PipelineServer.register_model("bench_detector/1", ps.InferenceModel(detector, (DW, DH), name="bench"))
+    # C5: the encoder is never called (no dec-model: the stage only fills the clip ring, as bench.py's direct line)
+    ps.PipelineServer.register_model(f"{net}/1", ps.InferenceModel(detector, (DW, DH), name="bench"))
     # distinct frames: at least 2 per stream and >= 3x the Infinity Cache, as the direct leg's pool
     W, H = wl["src"]
     n_pool = max(2 * S, -(-3 * MALL_BYTES // (W * H * 3 // 2)))
@@ -248,9 +266,10 @@ def via_pipeline(args, evam, torch, wl, device_index):
             qs.append(q)
         t0 = time.perf_counter()
         for k in range(S):
-            p = ps.PipelineServer.pipeline("object_detection", "bench")
+            p = ps.PipelineServer.pipeline(kind, "bench")
             p.start(source={"type": "application", "input": qs[k]}, destination={},
-                    parameters={"detection-properties": {"batch-size": args.stream_batch}})
+                    parameters={("action-properties" if action else "detection-properties"):
+                                {"batch-size": args.stream_batch}})
             pipes.append(p)
         for p in pipes:
             st = p.wait(600)
@@ -409,15 +428,19 @@ def main():
 
     wl = WORKLOADS[args.config]
     if args.via == "pipeline":
-        if world > 1 or wl.get("rois") or wl.get("ring"):
-            raise SystemExit("--via pipeline is wired for one process and full-frame detection configs (c1, c2, c4)")
+        if world > 1 or wl.get("rois"):
+            raise SystemExit("--via pipeline is wired for one process and the full-frame configs (c1, c2, c4, c5)")
         r = via_pipeline(args, evam, torch, wl, local)
         print(json.dumps({
             "metric": f"{METRIC} [{args.config}, via PipelineServer]", "value": r["value"], "unit": "frames/s",
             "n_gpus": 1, "higher_is_better": True, "dtype": "u8" if wl["dtype"] == "u8" else "u8->f32",
             "data": "synthetic device-resident frames through application sources; null detector",
             "config": {"workload": wl["desc"], **r,
-                       "path": ("one runner thread per device: bulk ingest of every stream's queue -> gvadetect "
+                       "path": (("one runner thread per device: bulk ingest of every stream's queue -> "
+                                 "gvaactionrecognitionbin stage -> one evam_pp_run_slots per tick over all streams' "
+                                 "new frames into the shared [32,16,3,H,W] clip ring (no decoder) -> per-frame results")
+                                if args.runner == "device" and wl.get("ring") else
+                                "one runner thread per device: bulk ingest of every stream's queue -> gvadetect "
                                 "stage -> one evam_pp_run per tick over all streams -> model -> per-frame results"
                                 if args.runner == "device" else
                                 "Pipeline thread per stream -> gvadetect stage -> per-device BatchHub -> one "

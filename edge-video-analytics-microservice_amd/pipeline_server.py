@@ -372,6 +372,7 @@ class BatchHub:
         self._cv = threading.Condition()
         self._stop = False
         self._pps: dict = {}            # slot -> pre-processing handle (bound to the slot's stream)
+        self._rings: dict = {}          # action stage hub key -> ClipRing shared by the device's action streams
         self._streams: list | None = None
         self.batches: list = []        # (key, units, requests) per executed batch (inspection / tests)
         self._thread = threading.Thread(target=self._loop, name=f"evam-hub-{device}", daemon=True)
@@ -408,6 +409,13 @@ class BatchHub:
             h = self._pps[slot] = HipPreProcessor(device=self.device) if s is None else \
                 HipPreProcessor(device=self.device, stream=s)
         return h
+
+    def clip_ring(self, key, size, device: int):
+        """The ClipRing of action streams whose stages share ``key`` (one model and pre-processing) on this device."""
+        r = self._rings.get(key)
+        if r is None:
+            r = self._rings[key] = ClipRing(device, size)
+        return r
 
     def submit(self, stage, items, units: int):
         """Queue ``items`` of ``stage`` and block until the batch holding them ran (re-raises its error)."""
@@ -486,6 +494,7 @@ class BatchHub:
         for h in self._pps.values():
             h.close()
         self._pps = {}
+        self._rings = {}
 
 
 class DeviceRunner:
@@ -999,20 +1008,64 @@ class ClassifyStage(_InferenceStage):
                 r.tensors.append(t)
 
 
-class ActionRecognitionStage(_InferenceStage):
-    """gvaactionrecognitionbin encoder input: aspect+central-crop into a 16-slot per-stream clip ring.
+class ClipRing:
+    """The clip ring of one action model on one device, shared by every action stream the device serves
+    (BASELINE configs[4]: 16-frame 224x224 clip stacking, batched across streams).
 
-    Runs on the pipeline's own handle, not through the hub: each stream owns its ring and writes slot
-    ``t % 16`` of it, so frames of different streams land in different tensors at different slots.
+    Pages of ``[ROWS * 16, 3, H, W]`` fp32 (``ROWS`` streams of 16 slots: the ``[S, 16, 3, H, W]`` layout of
+    bench.py's C5 line); a stream owns one row and writes its frame ``t`` at slot ``row * 16 + t % 16``, so the row
+    always holds its 16 most recent pre-processed frames. ``event`` marks the last launch that used the ring: ticks
+    run on alternating streams (``inflight``), and the next tick's launch waits for it before it overwrites slots.
+    """
+
+    ROWS = 32
+
+    def __init__(self, device: int, size):
+        self.device = int(device)
+        self.W, self.H = size
+        self.pages: list = []
+        self.free: list = []
+        self.event = None
+
+    def acquire(self):
+        """A free (page, row); a new page when every row is taken."""
+        if not self.free:
+            import torch
+
+            p = len(self.pages)
+            self.pages.append(torch.zeros((self.ROWS * ActionRecognitionStage.CLIP, 3, self.H, self.W),
+                                          dtype=torch.float32, device=f"cuda:{self.device}"))
+            self.free = [(p, r) for r in range(self.ROWS - 1, -1, -1)]
+        return self.free.pop()
+
+    def release(self, pr):
+        self.free.append(pr)
+
+
+class ActionRecognitionStage(_InferenceStage):
+    """gvaactionrecognitionbin (``pipelines/action_recognition/general/pipeline.json:3-4``): the encoder's
+    pre-processing (model-proc ``resize: aspect-ratio`` + ``crop: central``,
+    ``models_list/action-recognition-0001.json:3-13``) into a 16-slot clip ring per stream, batched across streams.
+
+    Every stream of the device owns a row of the model's shared :class:`ClipRing`; one ``evam_pp_run_slots`` per
+    tick writes the new frames of ALL action streams, each at its own slot ``row * 16 + t % 16`` (streams need not be
+    in step). A launch covers up to 16 consecutive frames of every stream; with a decoder it ends at the first frame
+    whose window is due, so no slot a due window reads is overwritten before the window is taken.
+
+    Inference follows the reference element: the encoder runs once per frame (on the frames each launch wrote, batched
+    across streams) and the decoder on the window of the stream's last 16 embeddings, oldest first, on every
+    ``inference-interval``-th frame once 16 frames have arrived. Without a decoder (``dec-model`` unset) the stage
+    only fills the ring.
     """
 
     CLIP = 16
-    batchable = False
 
     def __init__(self, el, server, device, slot=0):
         super().__init__(el, server, device, slot)
-        self.ring = None
-        self.t = 0
+        self.t = 0           # frames of this stream written so far
+        self._row = None     # (page, row) in the device's ClipRing
+        self.last_row = None
+        self._emb = collections.deque(maxlen=self.CLIP)  # the stream's last 16 encoder outputs (device rows)
         dec = el.properties.get("dec-model")
         self.decoder = server.model_for(dec, device) if dec else None
         mp = el.properties.get("model-proc")
@@ -1020,23 +1073,111 @@ class ActionRecognitionStage(_InferenceStage):
         if self.dec_proc:  # the decoder's model-proc carries the encoder's input_preproc too
             self.info = InferenceModel(None, self.model.input_size, self.dec_proc).preproc_info()
 
-    def process(self, items):
+    def _make_hub_key(self):
+        return super()._make_hub_key() + ("clip", id(self.decoder) if self.decoder is not None else None)
+
+    def out_dtype(self) -> int:
+        return N.DTYPE_F32
+
+    def ring(self) -> ClipRing:
+        return self.server.hub(self.slot).clip_ring(self.hub_key(), self.model.input_size, self.device)
+
+    def ring_row(self):
+        """This stream's 16 ring slots ``[16, 3, H, W]`` (slot k holds frame t with t % 16 == k), or None."""
+        pr = self._row if self._row is not None else self.last_row
+        if pr is None:
+            return None
+        p, r = pr
+        return self.ring().pages[p][r * self.CLIP:(r + 1) * self.CLIP]
+
+    def prepare(self, items):
+        return items, len(items)
+
+    def close(self):
+        if self._row is not None:
+            self.last_row = self._row  # inspection (tests): the row keeps its frames until another stream takes it
+            self.ring().release(self._row)
+            self._row = None
+        super().close()
+
+    def _due(self, req, j) -> bool:
+        return (self.decoder is not None and self.t + j + 1 >= self.CLIP
+                and req.items[j][0] % self.interval == 0)
+
+    def launch_batch(self, reqs, pp):
+        """Enqueue the launches over every request's frames (and, with a decoder, the encoder / decoder calls);
+        returns the completion that attaches the decoded actions to the frames."""
+        import numpy as np
         import torch
 
-        W, H = self.model.input_size
-        for fi, img, fr in items:
-            if self.ring is None:
-                self.ring = torch.zeros((self.CLIP, 3, H, W), dtype=torch.float32, device=f"cuda:{self.device}")
-            self.pp().convert([img], self.ring, self.info, slot_offset=self.t % self.CLIP, slot_stride=1)
-            self.t += 1
-            if self.t >= self.CLIP and self.decoder is not None and fi % self.interval == 0:
-                order = [(self.t + k) % self.CLIP for k in range(self.CLIP)]   # oldest first
-                logits = self.decoder.fn(self.model.fn(self.ring[order]))
-                logits = logits.detach().float().cpu().numpy() if hasattr(logits, "detach") else logits
-                post = (self.dec_proc or {}).get("output_postproc", [{}])[0]
-                t = P.classify(logits.reshape(1, -1), post.get("labels"), post.get("method", "softmax"),
-                               post.get("attribute_name", "action"), model=self.decoder.name)[0]
+        C = self.CLIP
+        ring = self.ring()
+        for r in reqs:
+            if r.stage._row is None:
+                r.stage._row = ring.acquire()
+        stream = torch.cuda.current_stream(self.device)
+        if ring.event is not None:
+            stream.wait_event(ring.event)
+        dec = self.decoder
+        lens = [len(r.items) for r in reqs]
+        kmax = max(lens)
+        windows = []  # (FrameResult, logits) of due frames
+        pos = 0
+        while pos < kmax:
+            end = min(kmax, pos + C)
+            if dec is not None:
+                for j in range(pos, end):  # the launch ends with the first frame whose window is due
+                    if any(j < n and r.stage._due(r, j) for r, n in zip(reqs, lens)):
+                        end = j + 1
+                        break
+            by_page: dict = {}
+            for r, n in zip(reqs, lens):
+                j1 = min(end, n)
+                if j1 <= pos:
+                    continue
+                st = r.stage
+                p, row = st._row
+                imgs, sl, owners = by_page.setdefault(p, ([], [], []))
+                imgs.extend(it[1] for it in r.items[pos:j1])
+                sl.append(row * C + (st.t + np.arange(pos, j1)) % C)
+                owners.append((r, pos, j1))
+            for p, (imgs, sl, owners) in by_page.items():
+                slots = np.concatenate(sl).astype(np.int32)
+                page = ring.pages[p]
+                pp.convert(imgs, page, self.info, slots=slots)
+                if dec is None:
+                    continue
+                emb = self.model.fn(page.index_select(0, torch.from_numpy(slots).to(page.device, torch.int64)))
+                k = 0
+                for r, j0, j1 in owners:
+                    st = r.stage
+                    for j in range(j0, j1):
+                        st._emb.append(emb[k])
+                        k += 1
+                        if st._due(r, j):
+                            windows.append((r.items[j][2], dec.fn(torch.stack(tuple(st._emb)))))
+            pos = end
+        for r, n in zip(reqs, lens):
+            r.stage.t += n
+        ev = torch.cuda.Event()
+        ev.record(stream)
+        ring.event = ev
+
+        def complete():
+            if not windows:
+                return
+            logits = torch.cat([lg.reshape(1, -1) if hasattr(lg, "reshape") else torch.as_tensor(lg).reshape(1, -1)
+                                for _, lg in windows]).detach().float().cpu().numpy()
+            post = (self.dec_proc or {}).get("output_postproc", [{}])[0]
+            tens = P.classify(logits, post.get("labels"), post.get("method", "softmax"),
+                              post.get("attribute_name", "action"), model=dec.name)
+            for (fr, _), t in zip(windows, tens):
                 fr.tensors.append(t)
+
+        return complete
+
+    def run_batch(self, reqs, pp):
+        self.launch_batch(reqs, pp)()
 
 
 STAGES = {"gvadetect": DetectStage, "gvaclassify": ClassifyStage, "gvainference": DetectStage,

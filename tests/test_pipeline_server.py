@@ -273,16 +273,22 @@ def test_end_to_end_detect_classify(ps, evam, model_dir, gpu, O):
 
 @pytest.mark.gpu
 def test_end_to_end_action_ring(ps, evam, model_dir, gpu, O):
+    """gvaactionrecognitionbin: each frame is pre-processed into the stream's clip-ring slot t % 16, the encoder runs
+    once per frame (on the frames of each launch) and the decoder on the window of the last 16 embeddings, oldest
+    first, from the 16th frame on (the reference element's encoder / decoder split)."""
     import torch
 
-    seen = []
+    enc_in, enc_out, dec_in = [], [], []
 
-    def encoder(clip):
-        seen.append(clip.clone())
-        return clip.mean(dim=(2, 3))            # [16, 3]
+    def encoder(x):                             # [n, 3, 32, 32] -> [n, 3]
+        enc_in.append(x.clone())
+        e = x.mean(dim=(2, 3))
+        enc_out.append(e.clone())
+        return e
 
-    def decoder(emb):
-        return emb.mean(0, keepdim=True)        # [1, 3]
+    def decoder(window):                        # [16, 3] -> [1, 3]
+        dec_in.append(window.clone())
+        return window.mean(0, keepdim=True)
 
     ps.PipelineServer.start({"pipeline_dir": PIPES, "model_dir": model_dir})
     ps.PipelineServer.register_model("ar/enc", ps.InferenceModel(encoder, (32, 32)))
@@ -300,13 +306,105 @@ def test_end_to_end_action_ring(ps, evam, model_dir, gpu, O):
         out.append(json.loads(x))
     assert len(out) == 18
     assert all("tensors" not in d for d in out[:15]) and all("tensors" in d for d in out[15:])
-    assert len(seen) == 3
-    # the first full clip is frames 0..15 in order, each aspect+central-cropped 96x54 -> 57x32 -> 32x32
-    ref = np.zeros((16, 3, 32, 32), np.float32)
+    # every frame reached the encoder once, in order, aspect+central-cropped 96x54 -> 57x32 -> 32x32, bit-exact
+    ref = np.zeros((18, 3, 32, 32), np.float32)
     c = O.COracle()
-    for i in range(16):
+    for i in range(18):
         c.preprocess_item(frames[i], None, ref, i, mode=2, lut=O.np_norm_lut(0))
-    assert np.array_equal(seen[0].cpu().numpy(), ref)
+    got = torch.cat(enc_in).cpu().numpy()
+    assert got.shape == ref.shape and np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+    # the decoder saw frames 0..15, 1..16, 2..17 (oldest first)
+    emb = torch.cat(enc_out)
+    assert len(dec_in) == 3
+    for k, w in enumerate(dec_in):
+        assert torch.equal(w, emb[k:k + 16])
+    # the ring row holds the last 16 frames at slot t % 16
+    row = p.stages[0].ring_row().cpu().numpy()
+    for t in range(2, 18):
+        assert np.array_equal(row[t % 16], ref[t])
+    ps.PipelineServer.stop()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("runner", ["device", "threads"])
+def test_action_streams_batched_staggered(ps, evam, model_dir, gpu, O, runner):
+    """32 action pipelines on one device, at different batch sizes and lengths so their frame counters are out of
+    step: every frame of every stream lands bit-exact in its stream's ring slot (checked as the
+    encoder reads it, and in the rows' final contents), launches are shared across streams, and every decoder window
+    is one stream's last 16 frames in order."""
+    import torch
+
+    S = 32
+    enc_in, enc_out, dec_in = [], [], []
+
+    def encoder(x):
+        enc_in.append(x.clone())
+        e = x.flatten(1).double().sum(1, keepdim=True).float()  # [n, 1] per-frame signature
+        e = torch.cat([e, x[:, :, 0, :4].flatten(1)], 1)          # plus raw pixels: unique per frame
+        enc_out.append(e.clone())
+        return e
+
+    def decoder(window):
+        dec_in.append(window.clone())
+        return torch.zeros((1, 3), device=window.device)
+
+    ps.PipelineServer.start({"pipeline_dir": PIPES, "model_dir": model_dir, "runner": runner, "batch_max": 256})
+    ps.PipelineServer.register_model("ar/enc", ps.InferenceModel(encoder, (32, 32)))
+    ps.PipelineServer.register_model("ar/dec", ps.InferenceModel(decoder, (32, 32)))
+    rng = np.random.default_rng(77)
+    W, H = 160, 90
+    n_frames = [18 + (7 * s) % 13 for s in range(S)]
+    batches = [1 + s % 4 for s in range(S)]
+    frames = [[O.random_frame(rng, O.NV12, W, H) for _ in range(n_frames[s])] for s in range(S)]
+    c = O.COracle()
+    ref = {}
+    for s in range(S):
+        r = np.zeros((n_frames[s], 3, 32, 32), np.float32)
+        for t, f in enumerate(frames[s]):
+            c.preprocess_item(f, None, r, t, mode=2, lut=O.np_norm_lut(0))
+        ref[s] = r
+    by_bytes = {ref[s][t].tobytes(): (s, t) for s in range(S) for t in range(n_frames[s])}
+    assert len(by_bytes) == sum(n_frames)
+    qs, pipes = [], []
+    for s in range(S):
+        q = queue.Queue()
+        for f in frames[s]:
+            q.put(evam.Image.from_host(f.fourcc, f.width, f.height, f.planes, device="cuda:0"))
+        q.put(None)
+        p = ps.PipelineServer.pipeline("action", "general")
+        p.start(source={"type": "application", "input": q}, destination={},
+                parameters={"ar-properties": {"batch-size": batches[s]}})
+        pipes.append(p)
+    for p in pipes:
+        assert p.wait(120)["state"] == "COMPLETED"
+    # every written slot, as the encoder read it: each (stream, frame) exactly once, bit-exact, in stream order
+    got = torch.cat(enc_in).cpu().numpy()
+    ids = [by_bytes.get(g.tobytes()) for g in got]
+    assert None not in ids, "a pre-processed frame matches no oracle frame"
+    assert sorted(ids) == sorted((s, t) for s in range(S) for t in range(n_frames[s]))
+    for s in range(S):
+        assert [t for s2, t in ids if s2 == s] == list(range(n_frames[s]))
+    assert len(enc_in) < sum(n_frames) / 2  # launches are shared across streams
+    # every decoder window: one stream's frames c-16 .. c-1, oldest first
+    emb = torch.cat(enc_out).cpu().numpy()
+    row_of = {emb[i].tobytes(): ids[i] for i in range(len(ids))}
+    wins = {s: [] for s in range(S)}
+    for w in dec_in:
+        ws = [row_of[r.tobytes()] for r in w.cpu().numpy()]
+        s = ws[0][0]
+        assert all(x[0] == s for x in ws) and [x[1] for x in ws] == list(range(ws[0][1], ws[0][1] + 16))
+        wins[s].append(ws[-1][1])
+    for s in range(S):
+        assert wins[s] == list(range(15, n_frames[s]))
+    # the rows' final contents: slot t % 16 holds frame t for the last 16 frames of every stream
+    rows = set()
+    for s, p in enumerate(pipes):
+        st = p.stages[0]
+        rows.add(st.last_row)
+        row = st.ring_row().cpu().numpy()
+        for t in range(n_frames[s] - 16, n_frames[s]):
+            assert np.array_equal(row[t % 16].view(np.uint32), ref[s][t].view(np.uint32)), (s, t)
+    assert len(rows) == S
     ps.PipelineServer.stop()
 
 

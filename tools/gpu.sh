@@ -9,7 +9,7 @@
 #   smoke             __graft_entry__.smoke()                          -> gpurun_out/smoke_TAG.txt
 #   driver[:N]        the driver's own bench command (C2, CPU baseline), N times -> gpurun_out/bench_TAG_driver[_k].json
 #   feed:c2,c4        bench.py --feed host (PCIe-inclusive) lines -> gpurun_out/bench_TAG_feed_<cfg>.json
-#   pipe              bench.py --via pipeline (C2 through PipelineServer) + its own rocprof kernel stats
+#   pipe[:c2,c5]      bench.py --via pipeline per config (default c2, + its rocprof kernel stats); HUB, PIPE_ARGS
 #   bench:c1,c2,...   one bench line per config (BENCH_STEPS, default 1000; CPU baseline unless CPU=0)
 #   prof:c1,c2,...    rocprofv3 --kernel-trace --stats per config (tools/prof_configs.sh, 200 steps, bench default:
 #                     two launches in flight)
@@ -61,11 +61,17 @@ for st in "$@"; do
         tail -1 "$OUT/bench_${TAG}_feed_$c.json"
       done ;;
     pipe)
-      # C2 frames through PipelineServer (device runner, 256-frame hub launches, null detector): a throughput line
-      timeout -k 10 300 python3 bench.py --via pipeline --steps 400 --warmup 40 --hub-batch 256 \
-        > "$OUT/bench_${TAG}_pipeline.json" 2> "$OUT/bench_${TAG}_pipeline.err" || { tail -20 "$OUT/bench_${TAG}_pipeline.err"; exit 1; }
-      tail -1 "$OUT/bench_${TAG}_pipeline.json"
-      PROF_ARGS="--via pipeline --hub-batch 256" STEPS=200 bash tools/prof_configs.sh "${TAG}_pipeline" c2 ;;
+      # frames through PipelineServer (device runner, null detector / no action decoder): a throughput line per config
+      # (default c2, with its rocprof kernel stats); HUB (hub batch, default 256) and PIPE_ARGS pass on to bench.py
+      [ "$arg" = "$st" ] && cfgs=c2
+      for c in $cfgs; do
+        timeout -k 10 300 python3 bench.py --via pipeline --config "$c" --hub-batch "${HUB:-256}" ${PIPE_ARGS:-} \
+          > "$OUT/bench_${TAG}_pipeline_$c.json" 2> "$OUT/bench_${TAG}_pipeline_$c.err" || { tail -20 "$OUT/bench_${TAG}_pipeline_$c.err"; exit 1; }
+        tail -1 "$OUT/bench_${TAG}_pipeline_$c.json"
+        if [ "$c" = c2 ] && [ -z "${PIPE_ARGS:-}" ]; then
+          PROF_ARGS="--via pipeline --hub-batch ${HUB:-256}" STEPS=200 bash tools/prof_configs.sh "${TAG}_pipeline" c2
+        fi
+      done ;;
     bench)
       for c in $cfgs; do
         timeout -k 10 300 python3 bench.py --config "$c" --steps "${BENCH_STEPS:-1000}" --warmup 100 $CPUARG \
