@@ -14,6 +14,7 @@ postproc maps the results to JSON.
 import json
 import os
 import queue
+import time
 
 import numpy as np
 import pytest
@@ -368,13 +369,21 @@ def test_action_streams_batched_staggered(ps, evam, model_dir, gpu, O, runner):
     qs, pipes = [], []
     for s in range(S):
         q = queue.Queue()
-        for f in frames[s]:
-            q.put(evam.Image.from_host(f.fourcc, f.width, f.height, f.planes, device="cuda:0"))
-        q.put(None)
         p = ps.PipelineServer.pipeline("action", "general")
         p.start(source={"type": "application", "input": q}, destination={},
                 parameters={"ar-properties": {"batch-size": batches[s]}})
+        qs.append(q)
         pipes.append(p)
+    for s in range(S):
+        for f in frames[s]:
+            qs[s].put(evam.Image.from_host(f.fourcc, f.width, f.height, f.planes, device="cuda:0"))
+    # end of stream only once every stream holds its ring row (an ended stream's row goes back to the free list),
+    # so every row's final contents below belong to its own stream
+    deadline = time.time() + 60
+    while any(p.stages[0]._row is None for p in pipes) and time.time() < deadline:
+        time.sleep(0.01)
+    for q in qs:
+        q.put(None)
     for p in pipes:
         assert p.wait(120)["state"] == "COMPLETED"
     # every written slot, as the encoder read it: each (stream, frame) exactly once, bit-exact, in stream order
