@@ -304,4 +304,103 @@ inline int roi_tail_tiles(int n, int n_cu, int64_t slots, int roi_tail, int DH, 
     return ts;
 }
 
+// The ROI kernel's launch order of one format group in one-unit-per-ROI plans, in four passes over the ROIs with no
+// intermediate unit list (round 6; the host call was 30+ us at 1,600 ROIs, half of it in the multi-pass planning):
+//   1. row-group cost per ROI (rg(cw): R | groups << 16, memoised by the caller) and the largest work estimate;
+//   2. the bytes bucket of every ROI (roi_largest_first's 64 buckets; all 0 without `sort`) and its histogram;
+//   3. the tail split (roi_tail_tiles: the last nsplit ROIs of the bytes order, i.e. the highest buckets, the last
+//      ones of the threshold bucket) and one histogram over (cost descending, split, bucket);
+//   4. every unit's position from that histogram, then the snake deal (every other band of n_cu positions reversed),
+//      handed to emit(position, item, row0, row1) — the caller writes the record straight into its slot.
+// The order equals the multi-pass plan it replaced (roi_largest_first, units in that order with the tail split, a stable
+// counting sort by row groups, the snake deal): tests/native/planner_check.cpp compares both on random groups.
+// sc: scratch. Returns the number of units.
+template <class RgFn, class EmitFn>
+inline int roi_launch_order(const int* idx, int n, const evam::Geom* geo, int DH, int n_cu, int64_t slots, int roi_tail,
+                            bool sort, bool snake, RgFn&& rg, std::vector<uint32_t>& sc, EmitFn&& emit) {
+    if (n <= 0) return 0;
+    sc.resize(2 * (size_t)n);
+    uint32_t* e_of = sc.data();       // per ROI: R | groups << 16
+    uint32_t* b_of = sc.data() + n;   // per ROI: bytes bucket | split flag << 8
+    int maxcost = 1;
+    int64_t maxw = 1;
+    for (int m = 0; m < n; m++) {
+        const evam::Geom& g = geo[idx[m]];
+        const uint32_t e = rg(g.cw);
+        e_of[m] = e;
+        maxcost = std::max(maxcost, (int)(e >> 16));
+        if (sort) maxw = std::max(maxw, (int64_t)g.cw * std::min(g.ch, 2 * DH));
+    }
+    int hist64[64] = {0};
+    if (sort) {
+        const double to_bucket = 63.0 / (double)maxw;
+        for (int m = 0; m < n; m++) {
+            const evam::Geom& g = geo[idx[m]];
+            const int64_t w = (int64_t)g.cw * std::min(g.ch, 2 * DH);
+            const uint32_t b = 63u - (uint32_t)std::min(63, (int)((double)w * to_bucket));  // 0 = largest
+            b_of[m] = b;
+            hist64[b]++;
+        }
+    } else {
+        std::fill(b_of, b_of + n, 0u);
+        hist64[0] = n;
+    }
+    int nsplit = 0;
+    const int ts = roi_tail_tiles(n, n_cu, slots, roi_tail, DH, nsplit);
+    // the split ROIs: every ROI of the buckets above bt, and the last kt (in call order) of bucket bt
+    int bt = 64, kt = 0;
+    for (int left = nsplit, b = 63; left > 0 && b >= 0; b--) {
+        bt = b;
+        kt = std::min(left, hist64[b]);
+        left -= kt;
+    }
+    const int nb = (maxcost + 1) * 128;  // bin = (maxcost - cost) * 128 + split * 64 + bucket
+    sc.resize(2 * (size_t)n + (size_t)nb + 1);
+    e_of = sc.data();
+    b_of = sc.data() + n;
+    uint32_t* start = sc.data() + 2 * (size_t)n;
+    std::fill(start, start + nb + 1, 0u);
+    int seen_bt = 0;
+    for (int m = 0; m < n; m++) {
+        const uint32_t b = b_of[m];
+        bool split = (int)b > bt;
+        if ((int)b == bt && ts > 1) split = seen_bt++ >= hist64[bt] - kt;
+        if (!split || ts <= 1) {
+            start[(size_t)(maxcost - (int)(e_of[m] >> 16)) * 128 + b + 1]++;
+            continue;
+        }
+        b_of[m] = b | 0x100u;
+        const int R = (int)(e_of[m] & 0xFFFF);
+        for (int t = 0; t < ts; t++) {
+            const int y0 = DH * t / ts, y1 = DH * (t + 1) / ts;
+            start[(size_t)(maxcost - (y1 - y0 + R - 1) / R) * 128 + 64 + b + 1]++;
+        }
+    }
+    for (int k = 0; k < nb; k++) start[k + 1] += start[k];
+    const int nu = (int)start[nb];
+    const int band = std::max(1, n_cu);
+    const int band_shift = (band & (band - 1)) == 0 ? __builtin_ctz((unsigned)band) : -1;  // 256 CUs: a shift
+    auto deal = [&](int p) {  // snake: positions of odd bands reversed within their band
+        if (!snake) return p;
+        const int b = band_shift >= 0 ? p >> band_shift : p / band;
+        if (!(b & 1)) return p;
+        const int lo = b * band, hi = std::min(nu, lo + band);
+        return lo + hi - 1 - p;
+    };
+    for (int m = 0; m < n; m++) {
+        const uint32_t b = b_of[m];
+        if (!(b & 0x100u)) {
+            emit(deal((int)start[(size_t)(maxcost - (int)(e_of[m] >> 16)) * 128 + b]++), idx[m], 0, DH);
+            continue;
+        }
+        const int R = (int)(e_of[m] & 0xFFFF);
+        const uint32_t bb = b & 0xFFu;
+        for (int t = 0; t < ts; t++) {
+            const int y0 = DH * t / ts, y1 = DH * (t + 1) / ts;
+            emit(deal((int)start[(size_t)(maxcost - (y1 - y0 + R - 1) / R) * 128 + 64 + bb]++), idx[m], y0, y1);
+        }
+    }
+    return nu;
+}
+
 #endif  // EVAM_GEOM_H

@@ -3718,6 +3718,7 @@ struct evam_pp {
     std::vector<int> sc_start;     // ROI unit counting sort: bucket starts
     std::vector<int> sc_slot;      // ROI units in launch order
     std::vector<uint8_t> sc_seen;  // evam_pp_run_slots: output slots taken
+    std::vector<uint32_t> sc_plan; // roi_launch_order scratch
     int memo_key[4] = {-1, -1, -1, -1};  // (format, staging buffer, row cap, DH) of memo_rg
     std::vector<uint32_t> memo_rg;       // per crop width: rows per group | groups of the whole height << 16
     TParams sc_tparams;            // strip-kernel arguments (3.5 KB: kept off the stack)
@@ -4175,14 +4176,29 @@ int run_impl(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* ite
         // bytes, crop width x touched rows). Workgroups are dispatched in order as slots free, so
         // the long ROIs start first and the short ones fill the tail.
         const bool sort = kn.roi_sort != 0;
-        std::vector<int>& bucket = h->sc_bucket;
-        bucket.resize(n_items);
         for (int f = 0; f < 4; f++) {
             if (path[f] != kPathRoi) continue;
             RoiRec* rr = reinterpret_cast<RoiRec*>(dyn + rec_off[f]);
-            std::vector<int>& ord = h->sc_order;
-            roi_largest_first(members.data() + mfirst[f], count[f], geo.data(), DH, sort, bucket.data(), ord);
-            HP(6);
+            // One record per work unit, built in registers and written as one 64-byte line into its launch slot.
+            auto put_rec = [&](int pos, int i, int row0, int row1) {
+                const evam_image& sim = srcs[items ? items[i].src_index : i];
+                RoiRec r;
+                r.plane[0] = sim.planes[0]; r.plane[1] = sim.planes[1]; r.plane[2] = sim.planes[2];
+                r.pitch[0] = sim.pitch[0]; r.pitch[1] = sim.pitch[1]; r.pitch[2] = sim.pitch[2];
+                r.width = (uint16_t)sim.width; r.height = (uint16_t)sim.height;
+                if (items) { r.x = items[i].x; r.y = items[i].y; r.w = items[i].w; r.h = items[i].h; }
+                else { r.x = r.y = r.w = r.h = 0; }  // w <= 0: the full frame
+                r.item = slots ? slots[i] : i;
+                r.row0 = (uint16_t)row0;
+                r.row1 = (uint16_t)row1;
+                if (dyn_wc) {  // write-combined device memory: the 64-byte line as four streaming stores
+                    const __m128i* src = reinterpret_cast<const __m128i*>(&r);
+                    __m128i* dst = reinterpret_cast<__m128i*>(&rr[pos]);
+                    for (int k = 0; k < 4; k++) _mm_stream_si128(dst + k, _mm_load_si128(src + k));
+                } else {
+                    memcpy(&rr[pos], &r, sizeof(RoiRec));
+                }
+            };
             // Work units (one workgroup each): one per ROI, or per row tile of TH rows for outputs taller than one
             // tile. Units launch largest first; beyond the resident workgroups the dispatcher starts each remaining
             // unit as a slot frees up. (Row tiles of a few row groups per ROI, EVAM_PP_ROI_UNIT, measured slower for
@@ -4191,113 +4207,89 @@ int run_impl(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* ite
             const int base = qbase[f];
             const int pxr = (kn.roi_px == 4 || kn.roi_px == 2) && DW % kn.roi_px == 0 ? kn.roi_px : 1;
             const int rcap = std::max(1, ((kRoiK / pxr) * kThreads) / (DW / pxr));
-            std::vector<int>& un = h->sc_units;  // (item, row0, row1, cost) per unit
-            un.clear();
-            int maxcost = 1;
+            int nu = 0;
             if (base == 1) {
-                // one unit per ROI (the default): no row split, no 64-bit divisions (this loop runs per ROI
-                // on the host for every call: 1,600 ROIs in C3)
+                // One unit per ROI (the default), planned in four passes over the ROIs with no unit list
+                // (roi_launch_order, evam_geom.h): row groups per ROI, the bytes pre-order, the tail split, one
+                // counting sort by (row groups, bytes), the snake deal, and each record written into its slot.
                 // Tail split: every ROI does the same pixel work (DW x DH), so when the ROIs do not divide
                 // evenly over the CUs the last `tail` ROIs in launch order land as one extra workgroup on
                 // `tail` CUs, whose SIMDs then convert 1 / floor(count / n_cu) more pixels than the others and
                 // end the launch (profiles/r03s_c3_roi_timeline_lut_dma.json: the last workgroups to finish
                 // are those narrow, compute-dense crops). Splitting those ROIs into kn.roi_tail row tiles —
                 // as long as every unit stays resident — gives each of the CUs a fraction of an ROI instead.
-                const int n = (int)ord.size();
-                int nsplit = 0;
-                const int ts = roi_tail_tiles(n, h->n_cu, qslots[f], kn.roi_tail, DH, nsplit);
-                un.resize(4 * ((size_t)n + (size_t)nsplit * (ts - 1)));
-                int* u4 = un.data();
-                // rows per group and groups per ROI depend on an ROI only through its crop width: memoised per
-                // handle for this launch's (format, staging buffer, row cap, DH), the divisions run once per
-                // distinct width instead of per ROI and call
+                // Snake deal: workgroup p starts on XCD p % 8 and within it on CU (p / 8) % 32, so each band of n_cu
+                // consecutive positions puts one unit on every CU; reversing every other band gives each CU one large
+                // and one small unit per two bands instead of always the k-th largest of every band (per-CU work
+                // balance is what bounds a one-round launch: profiles/r05ze_c3_head_split_ab.txt,
+                // r05zd_c3_xcd_frames_devrec_ab.txt).
+                // Rows per group and groups per ROI depend on an ROI only through its crop width: memoised per
+                // handle for this launch's (format, staging buffer, row cap, DH).
                 const int mkey[4] = {f, q.buf_bytes, rcap, DH};
                 if (memcmp(mkey, h->memo_key, sizeof(mkey)) != 0) {
                     memcpy(h->memo_key, mkey, sizeof(mkey));
                     h->memo_rg.clear();
                 }
                 if ((int)h->memo_rg.size() <= max_cw[f]) h->memo_rg.resize((size_t)max_cw[f] + 1, 0u);
-                uint32_t* rg = h->memo_rg.data();  // R | groups of the whole height << 16 (0: not yet known)
-                for (int p = 0; p < n; p++) {
-                    const int i = ord[p];
-                    uint32_t& e = rg[geo[i].cw];
+                uint32_t* rgm = h->memo_rg.data();  // R | groups of the whole height << 16 (0: not yet known)
+                auto rg = [&](int cw) {
+                    uint32_t& e = rgm[cw];
                     if (!e) {
-                        const int R = std::max(1, std::min(std::min(q.buf_bytes / row_bytes_bound(f, geo[i].cw), rcap), DH));
+                        const int R = std::max(1, std::min(std::min(q.buf_bytes / row_bytes_bound(f, cw), rcap), DH));
                         e = (uint32_t)R | ((uint32_t)((DH + R - 1) / R) << 16);
                     }
-                    if (p < n - nsplit) {
-                        const int cost = (int)(e >> 16);
-                        maxcost = std::max(maxcost, cost);
-                        u4[0] = i; u4[1] = 0; u4[2] = DH; u4[3] = cost;
-                        u4 += 4;
-                        continue;
-                    }
-                    const int R = (int)(e & 0xFFFF), nt = ts;
-                    for (int t = 0; t < nt; t++, u4 += 4) {
-                        const int y0 = DH * t / nt, y1 = DH * (t + 1) / nt;
+                    return e;
+                };
+                HP(6);
+                nu = roi_launch_order(members.data() + mfirst[f], count[f], geo.data(), DH, h->n_cu, qslots[f],
+                                      kn.roi_tail, sort, kn.roi_snake != 0, rg, h->sc_plan, put_rec);
+                HP(7);
+            } else {
+                // outputs taller than one tile (DH > TH): row tiles of TH rows per ROI, the same order rules
+                std::vector<int>& bucket = h->sc_bucket;
+                bucket.resize(n_items);
+                std::vector<int>& ord = h->sc_order;
+                roi_largest_first(members.data() + mfirst[f], count[f], geo.data(), DH, sort, bucket.data(), ord);
+                HP(6);
+                std::vector<int>& un = h->sc_units;  // (item, row0, row1, cost) per unit
+                un.clear();
+                int maxcost = 1;
+                for (size_t p = 0; p < ord.size(); p++) {
+                    const int i = ord[p];
+                    const int R = std::max(1, std::min(std::min(q.buf_bytes / row_bytes_bound(f, geo[i].cw), rcap), DH));
+                    for (int t = 0; t < base; t++) {
+                        const int y0 = t * q.TH;
+                        const int y1 = std::min(DH, (t + 1) * q.TH);
                         const int cost = (y1 - y0 + R - 1) / R;
                         maxcost = std::max(maxcost, cost);
-                        u4[0] = i; u4[1] = y0; u4[2] = y1; u4[3] = cost;
+                        un.insert(un.end(), {i, y0, y1, cost});
                     }
                 }
-            } else
-            for (size_t p = 0; p < ord.size(); p++) {
-                const int i = ord[p];
-                const int R = std::max(1, std::min(std::min(q.buf_bytes / row_bytes_bound(f, geo[i].cw), rcap), DH));
-                for (int t = 0; t < base; t++) {
-                    const int y0 = t * q.TH;
-                    const int y1 = std::min(DH, (t + 1) * q.TH);
-                    const int cost = (y1 - y0 + R - 1) / R;
-                    maxcost = std::max(maxcost, cost);
-                    un.insert(un.end(), {i, y0, y1, cost});
+                HP(7);
+                // stable counting sort of the units by cost, largest first, then the snake deal
+                nu = (int)(un.size() / 4);
+                std::vector<int>& start = h->sc_start;
+                start.assign((size_t)maxcost + 2, 0);
+                for (int u = 0; u < nu; u++) start[maxcost - un[4 * u + 3] + 1]++;
+                for (int c = 0; c <= maxcost; c++) start[c + 1] += start[c];
+                std::vector<int>& order = h->sc_slot;
+                order.resize(nu);
+                for (int u = 0; u < nu; u++) order[start[maxcost - un[4 * u + 3]]++] = u;
+                if (kn.roi_snake) {
+                    const int band = std::max(1, h->n_cu);
+                    for (int b0 = band; b0 < nu; b0 += 2 * band) std::reverse(order.begin() + b0, order.begin() + std::min(nu, b0 + band));
                 }
-            }
-            HP(7);
-            // stable counting sort of the units by cost, largest first; the records then go out in launch order,
-            // one sequential pass over the pinned (write-combined) slot instead of scattered 64-byte writes
-            const int nu = (int)(un.size() / 4);
-            std::vector<int>& start = h->sc_start;
-            start.assign((size_t)maxcost + 2, 0);
-            for (int u = 0; u < nu; u++) start[maxcost - un[4 * u + 3] + 1]++;
-            for (int c = 0; c <= maxcost; c++) start[c + 1] += start[c];
-            std::vector<int>& order = h->sc_slot;
-            order.resize(nu);
-            for (int u = 0; u < nu; u++) order[start[maxcost - un[4 * u + 3]]++] = u;
-            // Snake deal: workgroup p starts on XCD p % 8 and within it on CU (p / 8) % 32, so each band of n_cu
-            // consecutive positions puts one unit on every CU; reversing every other band gives each CU one large and
-            // one small unit per two bands instead of always the k-th largest of every band (per-CU work balance is
-            // what bounds a one-round launch: profiles/r05ze_c3_head_split_ab.txt, r05zd_c3_xcd_frames_devrec_ab.txt)
-            if (kn.roi_snake) {
-                const int band = std::max(1, h->n_cu);
-                for (int b0 = band; b0 < nu; b0 += 2 * band) std::reverse(order.begin() + b0, order.begin() + std::min(nu, b0 + band));
-            }
-            for (int pos = 0; pos < nu; pos++) {
-                const int u = order[pos];
-                const int i = un[4 * u];
-                const evam_image& sim = srcs[items ? items[i].src_index : i];
-                RoiRec r;  // built in registers, then one 64-byte copy into the write-combined slot
-                r.plane[0] = sim.planes[0]; r.plane[1] = sim.planes[1]; r.plane[2] = sim.planes[2];
-                r.pitch[0] = sim.pitch[0]; r.pitch[1] = sim.pitch[1]; r.pitch[2] = sim.pitch[2];
-                r.width = (uint16_t)sim.width; r.height = (uint16_t)sim.height;
-                if (items) { r.x = items[i].x; r.y = items[i].y; r.w = items[i].w; r.h = items[i].h; }
-                else { r.x = r.y = r.w = r.h = 0; }  // w <= 0: the full frame
-                r.item = slots ? slots[i] : i;
-                r.row0 = (uint16_t)un[4 * u + 1];
-                r.row1 = (uint16_t)un[4 * u + 2];
-                if (dyn_wc) {  // write-combined device memory: the 64-byte line as four streaming stores
-                    const __m128i* src = reinterpret_cast<const __m128i*>(&r);
-                    __m128i* dst = reinterpret_cast<__m128i*>(&rr[pos]);
-                    for (int k = 0; k < 4; k++) _mm_stream_si128(dst + k, _mm_load_si128(src + k));
-                } else {
-                    memcpy(&rr[pos], &r, sizeof(RoiRec));
+                for (int pos = 0; pos < nu; pos++) {
+                    const int u = order[pos];
+                    put_rec(pos, un[4 * u], un[4 * u + 1], un[4 * u + 2]);
                 }
             }
             if (dyn_wc && nu > 0) {
                 // The records reach device memory before the launch's doorbell. The fence only drains this core's
-                // write-combining buffers into the PCIe posted-write stream; a read of the last written line cannot
-                // complete ahead of those posted writes, so once it returns every record is in device memory (the
-                // HIP runtime publishes host-written device kernel arguments the same way: a read-back of the last
-                // byte after the fence).
+                // write-combining buffers into the PCIe posted-write stream; a read from the slot cannot complete
+                // ahead of those posted writes (PCIe ordering: a read does not pass posted writes), so once it
+                // returns every record is in device memory (the HIP runtime publishes host-written device kernel
+                // arguments the same way: a read-back of the last byte after the fence).
                 _mm_sfence();
                 _mm_mfence();
                 (void)*reinterpret_cast<const volatile uint32_t*>(reinterpret_cast<const uint8_t*>(&rr[nu - 1]) +

@@ -43,14 +43,16 @@ struct PinRingT {
     int cur = -1;
 
     // Next slot with at least n bytes. Blocks only while a kernel of up to N calls ago may still read it:
-    // the fence of the slot's run was recorded after the run's last call of the previous lap.
+    // the fence of the slot's run was recorded after the run's last call of the previous lap. One wait per run,
+    // on entering it: the run's fence is not recorded again before the run's last slot is used, so it still
+    // covers the run's other slots (a synchronize per call cost ~1 us of host time even on a passed event).
     int acquire(B& b, size_t n, uint8_t** h, const uint8_t** d, bool* is_wc = nullptr) {
         const int k = (cur + 1) % N;
         const int fk = k | (kFence - 1);
         if (!used[fk]) {
             if (int rc = b.event_create(&used[fk])) return rc;
         }
-        if (used_rec[fk]) {
+        if (used_rec[fk] && (k & (kFence - 1)) == 0) {
             if (int rc = b.event_sync(used[fk])) return rc;
         }
         if (cap[k] < n) {

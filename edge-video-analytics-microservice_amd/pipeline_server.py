@@ -1008,6 +1008,9 @@ class ClassifyStage(_InferenceStage):
                 r.tensors.append(t)
 
 
+_SECOND = operator.itemgetter(1)  # the Image of a (frame_index, Image, FrameResult) work item
+
+
 class ClipRing:
     """The clip ring of one action model on one device, shared by every action stream the device serves
     (BASELINE configs[4]: 16-frame 224x224 clip stacking, batched across streams).
@@ -1030,16 +1033,35 @@ class ClipRing:
     def acquire(self):
         """A free (page, row); a new page when every row is taken."""
         if not self.free:
-            import torch
-
             p = len(self.pages)
-            self.pages.append(torch.zeros((self.ROWS * ActionRecognitionStage.CLIP, 3, self.H, self.W),
-                                          dtype=torch.float32, device=f"cuda:{self.device}"))
+            self.pages.append(self._page())
             self.free = [(p, r) for r in range(self.ROWS - 1, -1, -1)]
         return self.free.pop()
 
+    def _page(self):
+        import torch
+
+        return torch.zeros((self.ROWS * ActionRecognitionStage.CLIP, 3, self.H, self.W), dtype=torch.float32,
+                           device=f"cuda:{self.device}")
+
     def release(self, pr):
         self.free.append(pr)
+
+    def enter(self):
+        """Order this tick's launches (on the current stream) behind the last tick that used the ring."""
+        if self.event is not None:
+            import torch
+
+            torch.cuda.current_stream(self.device).wait_event(self.event)
+
+    def leave(self):
+        """Mark the end of this tick's use of the ring on the current stream."""
+        if self.pages and self.pages[0].is_cuda:
+            import torch
+
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(self.device))
+            self.event = ev
 
 
 class ActionRecognitionStage(_InferenceStage):
@@ -1115,9 +1137,7 @@ class ActionRecognitionStage(_InferenceStage):
         for r in reqs:
             if r.stage._row is None:
                 r.stage._row = ring.acquire()
-        stream = torch.cuda.current_stream(self.device)
-        if ring.event is not None:
-            stream.wait_event(ring.event)
+        ring.enter()
         dec = self.decoder
         lens = [len(r.items) for r in reqs]
         kmax = max(lens)
@@ -1138,11 +1158,14 @@ class ActionRecognitionStage(_InferenceStage):
                 st = r.stage
                 p, row = st._row
                 imgs, sl, owners = by_page.setdefault(p, ([], [], []))
-                imgs.extend(it[1] for it in r.items[pos:j1])
-                sl.append(row * C + (st.t + np.arange(pos, j1)) % C)
+                imgs.extend(map(_SECOND, r.items[pos:j1]))
+                sl.append((row * C, st.t + pos, j1 - pos))
                 owners.append((r, pos, j1))
             for p, (imgs, sl, owners) in by_page.items():
-                slots = np.concatenate(sl).astype(np.int32)
+                # slot of frame j of a request: row * 16 + (t + j) % 16, for all requests in a few array operations
+                base, ph, k = np.array(sl, dtype=np.int64).T
+                first = np.repeat(np.cumsum(k) - k, k)
+                slots = (np.repeat(base, k) + (np.repeat(ph, k) + np.arange(len(imgs)) - first) % C).astype(np.int32)
                 page = ring.pages[p]
                 pp.convert(imgs, page, self.info, slots=slots)
                 if dec is None:
@@ -1159,9 +1182,7 @@ class ActionRecognitionStage(_InferenceStage):
             pos = end
         for r, n in zip(reqs, lens):
             r.stage.t += n
-        ev = torch.cuda.Event()
-        ev.record(stream)
-        ring.event = ev
+        ring.leave()
 
         def complete():
             if not windows:

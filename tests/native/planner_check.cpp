@@ -386,10 +386,85 @@ static void check_six_columns() {
     printf("six-column lanes: %d of 4000 tables admitted, every admitted lane exact\n", admitted);
 }
 
+// The fused four-pass ROI launch order (roi_launch_order, evam_pp_run since round 6) against the multi-pass plan it
+// replaced, restated here: roi_largest_first, one unit per ROI in that order with the tail split's row tiles for the
+// last nsplit, a stable counting sort of the units by row groups (largest first), then the snake deal. Same units at
+// the same positions, for the C3 shape and random groups (sorted or call order, snake on or off, odd CU counts).
+static void check_roi_launch_order() {
+    struct U { int item, r0, r1; bool operator==(const U& o) const { return item == o.item && r0 == o.r0 && r1 == o.r1; } };
+    int cases = 0;
+    for (int it = 0; it < 3000; it++) {
+        const bool c3 = it < 50;
+        const int f = c3 ? kNV12 : uni(0, 3);
+        const int n = c3 ? 1600 : uni(1, 2500), DH = c3 ? 72 : uni(1, 200);
+        const int n_cu = c3 ? 256 : (it % 3 ? 256 : uni(1, 300));
+        const int64_t slots = c3 ? 1792 : (int64_t)n_cu * uni(1, 8);
+        const int roi_tail = c3 ? 4 : uni(0, 8), buf = c3 ? 12 * 1024 : uni(1, 32) * 512;
+        const int rcap = c3 ? 42 : uni(1, 64);
+        const bool sort = c3 || it % 7 != 0, snake = c3 || it % 5 != 0;
+        std::vector<Geom> geo(n);
+        std::vector<int> idx(n);
+        for (int i = 0; i < n; i++) {
+            geo[i] = Geom{0, 0, c3 ? uni(24, 400) & ~1 : uni(1, 3000), c3 ? uni(24, 300) & ~1 : uni(1, 2000), 1, 1, 0, 0};
+            idx[i] = i;
+        }
+        auto rg = [&](int cw) {
+            const int R = std::max(1, std::min(std::min(buf / row_bytes_bound(f, cw), rcap), DH));
+            return (uint32_t)R | ((uint32_t)((DH + R - 1) / R) << 16);
+        };
+        // the multi-pass reference
+        std::vector<int> bucket(n), ord;
+        roi_largest_first(idx.data(), n, geo.data(), DH, sort, bucket.data(), ord);
+        int nsplit = 0;
+        const int ts = roi_tail_tiles(n, n_cu, slots, roi_tail, DH, nsplit);
+        std::vector<U> un;
+        std::vector<int> cost;
+        for (int p = 0; p < n; p++) {
+            const int i = ord[p];
+            const uint32_t e = rg(geo[i].cw);
+            if (p < n - nsplit) {
+                un.push_back({i, 0, DH});
+                cost.push_back((int)(e >> 16));
+                continue;
+            }
+            const int R = (int)(e & 0xFFFF);
+            for (int t = 0; t < ts; t++) {
+                const int y0 = DH * t / ts, y1 = DH * (t + 1) / ts;
+                un.push_back({i, y0, y1});
+                cost.push_back((y1 - y0 + R - 1) / R);
+            }
+        }
+        std::vector<int> order(un.size());
+        for (size_t u = 0; u < un.size(); u++) order[u] = (int)u;
+        std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return cost[a] > cost[b]; });
+        const int nu = (int)order.size(), band = std::max(1, n_cu);
+        if (snake)
+            for (int b0 = band; b0 < nu; b0 += 2 * band) std::reverse(order.begin() + b0, order.begin() + std::min(nu, b0 + band));
+        // the fused planner
+        std::vector<uint32_t> sc;
+        std::vector<U> got(nu, U{-1, -1, -1});
+        std::vector<int> hits(nu, 0);
+        const int nu2 = roi_launch_order(idx.data(), n, geo.data(), DH, n_cu, slots, roi_tail, sort, snake, rg, sc,
+                                         [&](int q, int item, int r0, int r1) {
+                                             if (q >= 0 && q < nu) { got[q] = U{item, r0, r1}; hits[q]++; }
+                                         });
+        CHECK(nu2 == nu, "launch order: %d units, expected %d (case %d)", nu2, nu, it);
+        for (int q = 0; q < nu && failures < 20; q++) {
+            CHECK(hits[q] == 1, "launch order: position %d written %d times (case %d)", q, hits[q], it);
+            const U& w = un[order[q]];
+            CHECK(got[q] == w, "launch order case %d pos %d: (%d,%d,%d) expected (%d,%d,%d)", it, q, got[q].item,
+                  got[q].r0, got[q].r1, w.item, w.r0, w.r1);
+        }
+        cases++;
+    }
+    printf("ROI launch order: fused planner equals the multi-pass plan on %d groups\n", cases);
+}
+
 int main() {
     check_six_columns();
     check_clip_simd();
     check_roi_tail();
+    check_roi_launch_order();
     check_geometry();
     check_linear_tables();
     check_footprints();

@@ -5,6 +5,7 @@ stage across pipelines bounded by batch_max, per-stream stage order, destination
 `"device"` runner and, for the same scenario, the `"threads"` runner (per-pipeline threads + BatchHub)."""
 import json
 import queue
+import time
 
 import pytest
 import torch
@@ -16,14 +17,17 @@ class StubPP:
     """Records every convert call; returns lazily built identity transforms like HipPreProcessor."""
 
     calls = []
+    slot_calls = []
 
     def __init__(self, device=0, stream=None):
         pass
 
-    def convert(self, srcs, out, info=None, rois=None, slot_offset=0, slot_stride=1, want_transform=False):
+    def convert(self, srcs, out, info=None, rois=None, slot_offset=0, slot_stride=1, want_transform=False, slots=None):
         n_src = len(srcs)
         n_roi = None if rois is None else len(rois)
         StubPP.calls.append((n_src, n_roi, tuple(out.shape)))
+        if slots is not None:
+            StubPP.slot_calls.append([int(v) for v in slots])
         if want_transform:
             return [None] * n_src
 
@@ -39,6 +43,7 @@ def stubbed(evam, monkeypatch, tmp_path):
     monkeypatch.setattr(ps._InferenceStage, "_tensor",
                         lambda self, n: torch.zeros((n, 3, self.model.input_size[1], self.model.input_size[0])))
     StubPP.calls = []
+    StubPP.slot_calls = []
     mdir = make_model_tree(str(tmp_path / "models"), {
         "det_alias": {"det_ver": (64, 64, {"input_preproc": [], "output_postproc": [{"labels": ["bg", "car"]}]})},
         "cls_alias": {"cls_ver": (24, 24, {"input_preproc": [],
@@ -531,3 +536,59 @@ def test_runner_death_with_held_back_results(stubbed, monkeypatch):
     st = p.wait(30)
     assert p._done.is_set(), "wait() timed out behind a dead runner"
     assert st["state"] == "ERROR" and "runner bug" in st["message"] and "undelivered" in st["message"], st
+
+
+@pytest.mark.parametrize("runner", ["device", "threads"])
+def test_action_stage_shared_ring_slots(stubbed, runner, monkeypatch):
+    """gvaactionrecognitionbin batched across streams (CPU, stubbed pre-processor, ring pages on the host): each launch
+    gives every item its own slot (evam_pp_run_slots), each stream's frames go to row * 16 + t % 16 in frame order,
+    launches are shared by the streams, a launch ends at the first frame whose window is due, and every frame from a
+    stream's 16th on gets its action."""
+    ps, pre, _ = stubbed
+    monkeypatch.setattr(ps.ClipRing, "_page", lambda self: torch.zeros((self.ROWS * 16, 3, self.H, self.W)))
+    mdir = make_model_tree(str(stubbed[2]) + "_ar", {
+        "ar": {"enc": (32, 32, None),
+               "dec": (32, 32, {"input_preproc": [{"format": "image", "params": {"resize": "aspect-ratio",
+                                                                                 "crop": "central"}}],
+                                "output_postproc": [{"attribute_name": "action", "method": "softmax",
+                                                     "labels": ["a", "b", "c"]}]})}})
+    ps.PipelineServer.start({"pipeline_dir": PIPES, "model_dir": mdir, "runner": runner, "batch_max": 64,
+                             "batch_wait_ms": 50, "batch_target": 64})
+    ps.PipelineServer.register_model("ar/enc", ps.InferenceModel(lambda x: x.mean(dim=(2, 3)), (32, 32)))
+    ps.PipelineServer.register_model("ar/dec", ps.InferenceModel(lambda w: w.mean(0, keepdim=True), (32, 32)))
+    counts, batches = [20, 17, 33, 16, 5], [1, 2, 3, 4, 1]
+    pipes, outs, ins = [], [], []
+    for n, b in zip(counts, batches):
+        qin, qout = queue.Queue(), queue.Queue()
+        for f in frames(pre, n):
+            qin.put(f)
+        p = ps.PipelineServer.pipeline("action", "general")
+        p.start(source={"type": "application", "input": qin}, destination={"metadata": {"output": qout, "mode": "json"}},
+                parameters={"ar-properties": {"batch-size": b}})
+        pipes.append(p)
+        outs.append(qout)
+        ins.append(qin)
+    deadline = time.time() + 30  # end of stream once every stream holds its ring row: rows are not reused below
+    while any(p.stages[0]._row is None for p in pipes) and time.time() < deadline:
+        time.sleep(0.005)
+    for q in ins:
+        q.put(None)
+    for p in pipes:
+        assert p.wait(30)["state"] == "COMPLETED"
+    for call in StubPP.slot_calls:
+        assert len(set(call)) == len(call)  # no two items of a launch share a slot
+    seq = {}
+    for call in StubPP.slot_calls:
+        for v in call:
+            seq.setdefault(v // 16, []).append(v % 16)
+    rows = [p.stages[0].last_row[1] for p in pipes]
+    assert len(set(rows)) == len(rows)
+    for n, row in zip(counts, rows):
+        assert seq[row] == [t % 16 for t in range(n)]
+    assert len(StubPP.slot_calls) < sum(counts)
+    for n, q in zip(counts, outs):
+        res = []
+        while (x := q.get(timeout=5)) is not None:
+            res.append(json.loads(x))
+        assert len(res) == n
+        assert all("tensors" not in d for d in res[:15]) and all("tensors" in d for d in res[15:])

@@ -17,7 +17,8 @@
 #   pmc:c2,c3,...     FETCH_SIZE / WRITE_SIZE passes per config (tools/pmc.sh) -> pmc_traffic_TAG_<cfg>.json
 #   valu:c1,...       SQ_INSTS_VALU pass per config (tools/pmc.sh)
 #   stall:c1,...      stall-attribution passes per config (tools/pmc.sh, two SQ groups)
-#   ab:CFG:SET1|SET2  same-box alternating env A/B (tools/gpu_env_ab.sh)
+#   hostprof:c3       host time per evam_pp_run section (needs ab/libevam_pp_hostprof.so) -> hostprof_TAG.txt
+#   ab:CFG:SET1|SET2  same-box alternating env / option A/B (tools/gpu_env_ab.sh)
 #   dist              bench.py under torch.distributed.run, 2 ranks sharing the GPU over gloo
 #
 # Every output is stamped with EVAM_SHA (pass `EVAM_SHA=$(git rev-parse HEAD)` from the container: the box has
@@ -102,6 +103,16 @@ PY
       for c in $cfgs; do
         PMC_GROUPS="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU;SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_LDS SQ_INSTS_LDS SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VMEM SQ_INSTS_VMEM_RD" \
           bash tools/pmc.sh "${TAG}_stall_$c" "$c"
+      done ;;
+    hostprof)
+      # host time per section of evam_pp_run (a -DEVAM_PP_HOST_PROF build: tools/build_variant.sh hostprof
+      # -DEVAM_PP_HOST_PROF before the call), one launch at a time, plus the bench's own host_us_per_call
+      for c in $cfgs; do
+        EVAM_PP_LIB=ab/libevam_pp_hostprof.so timeout -k 10 200 python3 bench.py --config "$c" --steps 1000 --warmup 100 \
+          --no-cpu-baseline --inflight 1 > "$OUT/hostprof_${TAG}_$c.json" 2> "$OUT/hostprof_${TAG}_$c.err" \
+          || { tail -20 "$OUT/hostprof_${TAG}_$c.err"; exit 1; }
+        echo "$c $(grep 'host prof' "$OUT/hostprof_${TAG}_$c.err") host_us_per_call $(python3 -c "import json; print(json.loads(open('$OUT/hostprof_${TAG}_$c.json').read().splitlines()[-1])['host_us_per_call'])")" \
+          | tee -a "$OUT/hostprof_$TAG.txt"
       done ;;
     ab)
       c="${arg%%:*}"; sets="${arg#*:}"

@@ -14,6 +14,6 @@ for pass in 1 2; do
     for w in $s; do case "$w" in --*) opts+=("$w") ;; *) envs+=("$w") ;; esac; done
     env "${envs[@]}" timeout -k 10 120 python bench.py --config $CFG --steps ${AB_STEPS:-1000} --warmup 100 --no-cpu-baseline \
       --resident-steps 0 "${opts[@]}" > $f 2>/dev/null
-    python -c "import json; d=json.load(open('$f')); print('$CFG [$s]', d['value'], d['ms_per_step'], d['roofline']['frac'])" | tee -a gpurun_out/envab_$TAG.txt
+    python -c "import json; d=json.load(open('$f')); print('$CFG [$s]', d['value'], d['ms_per_step'], d['roofline']['frac'], 'single', d['roofline']['single_launch']['frac'], 'host_us', d['host_us_per_call'], 'submit_ms', d['host_submit_ms_per_step'])" | tee -a gpurun_out/envab_$TAG.txt
   done
 done
