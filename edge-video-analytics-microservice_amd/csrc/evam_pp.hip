@@ -1637,6 +1637,33 @@ static_assert(sizeof(TParams) <= 4000, "strip / band kernel arguments must fit t
 // bytes), the copy floor of those bytes on the same box (profiles/r03c_strip_bw.txt).
 // Letterbox rows are plain fill stores outside the ring; letterbox columns are a per-lane select in the
 // strips that have any. D = ring depth (rows of DMA in flight).
+// Progress-based priority (EVAM_PP_PRIO): s_setprio 3 at the start, one level lower at each quarter of a wave's n
+// steps (rows or row groups), so the waves behind get the issue slot when several are ready. One scalar compare per
+// step against the next threshold; the level change sits in the rarely taken branch (the three-way compare chain it
+// replaces cost six scalar instructions per step).
+struct ProgressPrio {
+    int next, q2, q3, level;
+    __device__ __forceinline__ ProgressPrio(bool on, int n) : next(on ? n / 4 : -1), q2(n / 2), q3((3 * n) / 4), level(3) {
+        if (on) __builtin_amdgcn_s_setprio(3);
+    }
+    __device__ __forceinline__ void step(int i) {
+        if (__builtin_expect(i != next, 1)) return;
+        if (level == 3) {
+            __builtin_amdgcn_s_setprio(2);
+            level = 2;
+            next = q2;
+        } else if (level == 2) {
+            __builtin_amdgcn_s_setprio(1);
+            level = 1;
+            next = q3;
+        } else {
+            __builtin_amdgcn_s_setprio(0);
+            level = 0;
+            next = -1;
+        }
+    }
+};
+
 template <int FMT, int OUT, int D, int PX, int PR>
 __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
     // the LUT at a static LDS address (folds into the reads' immediate offsets); the rings after it
@@ -1918,8 +1945,7 @@ __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
     // Progress-based priority (EVAM_PP_PRIO): waves of a SIMD otherwise share issue by age, so the youngest
     // workgroups' waves lag and end the launch alone; a wave lowers its priority as it passes each quarter of its
     // rows, so the ones behind get the issue slots when several are ready.
-    const int pq1 = P.prio ? n / 4 : -1, pq2 = P.prio ? n / 2 : -1, pq3 = P.prio ? (3 * n) / 4 : -1;
-    if (P.prio) __builtin_amdgcn_s_setprio(3);
+    ProgressPrio prio(P.prio != 0, n);
     const int nst = full ? 3 * PX : 3;
     // one output row: row i of the tile's visible rows, ring entry kk (compile-time after unrolling)
     auto row = [&](int i, int kk, auto has_pad) {
@@ -1938,9 +1964,7 @@ __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
 #ifdef EVAM_PP_TRACE
         if (i == 0) EVAM_WSTAMP(3);
 #endif
-        if (i == pq1) __builtin_amdgcn_s_setprio(2);
-        else if (i == pq2) __builtin_amdgcn_s_setprio(1);
-        else if (i == pq3) __builtin_amdgcn_s_setprio(0);
+        prio.step(i);
         const int Y = vr0 + i;
         const uint32_t wb0 = (uint32_t)__builtin_amdgcn_readlane(lb0, i), wb1 = (uint32_t)__builtin_amdgcn_readlane(lb1, i);
         const int ya = __builtin_amdgcn_readlane(lr0, i), yb = __builtin_amdgcn_readlane(lr1, i);
@@ -2372,12 +2396,9 @@ __global__ __launch_bounds__(256) void evam_pp_band(const TParams P) {
     int pa = -1, pb = -1;
     const int nst = 3;  // stores per output row (one PX-wide store per channel)
     // progress-based priority (EVAM_PP_PRIO), as in the strip kernel
-    const int pq1 = P.prio ? n / 4 : -1, pq2 = P.prio ? n / 2 : -1, pq3 = P.prio ? (3 * n) / 4 : -1;
-    if (P.prio) __builtin_amdgcn_s_setprio(3);
+    ProgressPrio prio(P.prio != 0, n);
     for (int i = 0; i < n; i++) {
-        if (i == pq1) __builtin_amdgcn_s_setprio(2);
-        else if (i == pq2) __builtin_amdgcn_s_setprio(1);
-        else if (i == pq3) __builtin_amdgcn_s_setprio(0);
+        prio.step(i);
         const int ra = __builtin_amdgcn_readlane(lr0, i), rb = __builtin_amdgcn_readlane(lr1, i);
         issue_to(rb);  // (issued already unless `ahead` is 0)
         vmcnt_le(pos - __builtin_amdgcn_readlane(dpos, rb - rlo));  // rows up to rb landed
@@ -2831,15 +2852,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(96))) void
 
 
     // progress-based priority (EVAM_PP_PRIO): 3 -> 0 over the quarters of the workgroup's row groups
-    const int pg1 = P.prio ? ngroups / 4 : -1, pg2 = P.prio ? ngroups / 2 : -1, pg3 = P.prio ? (3 * ngroups) / 4 : -1;
-    if (P.prio) __builtin_amdgcn_s_setprio(3);
-    auto step_prio = [&](int grp) {
-        if (grp == pg1) __builtin_amdgcn_s_setprio(2);
-        else if (grp == pg2) __builtin_amdgcn_s_setprio(1);
-        else if (grp == pg3) __builtin_amdgcn_s_setprio(0);
-    };
+    ProgressPrio prio(P.prio != 0, ngroups);
     for (int grp = 0; grp < ngroups; grp++) {
-        step_prio(grp);
+        prio.step(grp);
         // Wait for this wave's share of group grp's DMA. Group grp-1 was full (only the last group can
         // be partial), so this wave issued at least 3 stores for each of its nk_w store steps after
         // that DMA: those may stay in flight.

@@ -1,11 +1,14 @@
 #!/bin/bash
-# One parameterised GPU session (replaces the per-round one-off scripts). Every GPU step runs under its own
-# time limit and the first failure ends the script.
+# One parameterised GPU session: every round-5 one-off session script was a composition of these steps
+# (testk + ab, prof + ablate, pmc) and is gone; a profile's header records the steps that made it. Every GPU step runs
+# under its own time limit and the first failure ends the script.
 #
 #   tools/gpu.sh TAG STEP [STEP ...]
 #
 # Steps:
 #   test              pytest -m gpu (one process)                      -> gpurun_out/pytest_gpu_TAG.log
+#   testk:a,b         pytest -m gpu -k "a or b" (a subset before an A/B of the knob it covers)
+#   ablate:CFG:B1,B2  rocprof of stage-removal builds (EVAM_PP_ABLATE bits, tools/prof_ablate.sh)
 #   smoke             __graft_entry__.smoke()                          -> gpurun_out/smoke_TAG.txt
 #   driver[:N]        the driver's own bench command (C2, CPU baseline), N times -> gpurun_out/bench_TAG_driver[_k].json
 #   feed:c2,c4        bench.py --feed host (PCIe-inclusive) lines -> gpurun_out/bench_TAG_feed_<cfg>.json
@@ -41,6 +44,16 @@ for st in "$@"; do
       timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
         > "$OUT/pytest_gpu_$TAG.log" 2>&1 || { tail -40 "$OUT/pytest_gpu_$TAG.log"; exit 1; }
       tail -1 "$OUT/pytest_gpu_$TAG.log" ;;
+    testk)
+      # a subset of the GPU suite: testk:c3,roi -> pytest -m gpu -k "c3 or roi" (env knobs apply: VAR=... gpu.sh ...)
+      k="${arg//,/ or }"
+      timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "$k" \
+        > "$OUT/pytest_gpu_${TAG}_k.log" 2>&1 || { tail -40 "$OUT/pytest_gpu_${TAG}_k.log"; exit 1; }
+      tail -1 "$OUT/pytest_gpu_${TAG}_k.log" ;;
+    ablate)
+      # stage-removal rocprof of one config: ablate:c2:0,2,4,16 (EVAM_PP_ABLATE bit sets, tools/prof_ablate.sh)
+      c="${arg%%:*}"; bits="${arg#*:}"
+      bash tools/prof_ablate.sh "$TAG" "$c" "${bits//,/ }" ;;
     smoke)
       timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke_$TAG.txt" 2>&1 \
         || { tail -20 "$OUT/smoke_$TAG.txt"; exit 1; }
