@@ -403,4 +403,50 @@ inline int roi_launch_order(const int* idx, int n, const evam::Geom* geo, int DH
     return nu;
 }
 
+// Frame-to-XCD deal of a sorted unit list (EVAM_PP_ROI_XCD=1, round 6 experiment for C3's 1.5x read over-fetch):
+// workgroup p of a launch starts on XCD p % n_xcd and, within it, on CU (p / n_xcd) % (n_cu / n_xcd). Frames go to XCDs
+// largest total cost first onto the least loaded XCD, so the overlapping crops of one frame share one L2; each XCD keeps
+// its units in the sorted (largest-first) order, dealt over its CUs snake-wise (every other band of its CUs reversed);
+// position n_xcd * j + x holds XCD x's j-th unit. Units beyond the smallest XCD's count (the smallest units) fill the
+// positions after the interleave, in sorted order. unit[q] = (frame, cost) of sorted position q; pos[q] = its slot.
+inline void roi_xcd_deal(const int* frame, const int* cost, int nu, int n_frames, int n_cu, int n_xcd,
+                         std::vector<int>& pos, std::vector<int>& scratch) {
+    pos.assign((size_t)nu, 0);
+    if (nu <= 0) return;
+    n_xcd = std::max(1, n_xcd);
+    const int cus = std::max(1, n_cu / n_xcd);
+    scratch.assign((size_t)n_frames * 2 + (size_t)nu + 2 * (size_t)n_xcd, 0);
+    int* fcost = scratch.data();                       // per frame: summed unit cost
+    int* fxcd = fcost + n_frames;                      // per frame: its XCD
+    int* local = fxcd + n_frames;                      // per unit: index within its XCD
+    int* cnt = local + nu;                             // per XCD: units
+    int* load = cnt + n_xcd;                           // per XCD: summed cost
+    for (int q = 0; q < nu; q++) fcost[frame[q]] += cost[q];
+    std::vector<int> order((size_t)n_frames);
+    for (int f = 0; f < n_frames; f++) order[f] = f;
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return fcost[a] > fcost[b]; });
+    for (int f : order) {
+        int best = 0;
+        for (int x = 1; x < n_xcd; x++)
+            if (load[x] < load[best]) best = x;
+        fxcd[f] = best;
+        load[best] += fcost[f];
+    }
+    for (int q = 0; q < nu; q++) local[q] = cnt[fxcd[frame[q]]]++;
+    int n_min = cnt[0];
+    for (int x = 1; x < n_xcd; x++) n_min = std::min(n_min, cnt[x]);
+    int rest = n_xcd * n_min;
+    for (int q = 0; q < nu; q++) {
+        const int x = fxcd[frame[q]], j = local[q];
+        if (j >= n_min) {
+            pos[q] = rest++;
+            continue;
+        }
+        const int b = j / cus;
+        const int lo = b * cus, hi = std::min(n_min, lo + cus);
+        const int jj = (b & 1) ? lo + hi - 1 - j : j;
+        pos[q] = n_xcd * jj + x;
+    }
+}
+
 #endif  // EVAM_GEOM_H

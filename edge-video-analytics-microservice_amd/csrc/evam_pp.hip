@@ -2952,6 +2952,7 @@ struct Knobs {
                        // profiles/r05zf_c3_snake_ab.txt)
     int roi_tail = 4;                              // row tiles per ROI of the uneven tail over the CUs (1: no split)
     int roi_snake = 1;                             // snake deal of the sorted units over the CUs (0: bands in one direction)
+    int roi_xcd = 0;                               // 1: each frame's ROIs on one XCD, snake-dealt over its CUs (experiment)
     int strip = 1, strip_th = -1, strip_nw = -1, strip_px = 0;  // strip kernel: allowed (2: forced), rows per
                                                                 // tile, waves, px
     int strip_pair = 1;                            // strip kernel: paired-tap DMA where the footprints allow it
@@ -2985,6 +2986,7 @@ struct Knobs {
         roi_th = env_int("EVAM_PP_ROI_TH", roi_th); roi_buf = env_int("EVAM_PP_ROI_BUF", roi_buf);
         roi_px = env_int("EVAM_PP_ROI_PX", roi_px); roi_sort = env_int("EVAM_PP_ROI_SORT", roi_sort);
         roi_tail = env_int("EVAM_PP_ROI_TAIL", roi_tail); roi_snake = env_int("EVAM_PP_ROI_SNAKE", roi_snake);
+        roi_xcd = env_int("EVAM_PP_ROI_XCD", roi_xcd);
     }
 };
 
@@ -4256,8 +4258,27 @@ int run_impl(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* ite
                     return e;
                 };
                 HP(6);
-                nu = roi_launch_order(members.data() + mfirst[f], count[f], geo.data(), DH, h->n_cu, qslots[f],
-                                      kn.roi_tail, sort, kn.roi_snake != 0, rg, h->sc_plan, put_rec);
+                if (kn.roi_xcd && items && h->n_cu >= 8) {
+                    // experiment (EVAM_PP_ROI_XCD=1): the sorted units, then each frame's units on one XCD
+                    std::vector<int>& un = h->sc_units;  // per sorted position: item, row0, row1, cost
+                    un.assign(4 * ((size_t)count[f] * (size_t)std::max(1, kn.roi_tail) + 1), -1);
+                    nu = roi_launch_order(members.data() + mfirst[f], count[f], geo.data(), DH, h->n_cu, qslots[f],
+                                          kn.roi_tail, sort, false, rg, h->sc_plan, [&](int q, int i, int r0, int r1) {
+                                              const int R = (int)(rg(geo[i].cw) & 0xFFFF);
+                                              int* u = &un[4 * (size_t)q];
+                                              u[0] = i; u[1] = r0; u[2] = r1; u[3] = (r1 - r0 + R - 1) / R;
+                                          });
+                    std::vector<int>& fr = h->sc_start;
+                    std::vector<int>& co = h->sc_bucket;
+                    fr.resize(nu);
+                    co.resize(nu);
+                    for (int q = 0; q < nu; q++) { fr[q] = items[un[4 * q]].src_index; co[q] = un[4 * q + 3]; }
+                    roi_xcd_deal(fr.data(), co.data(), nu, n_srcs, h->n_cu, 8, h->sc_slot, h->sc_order);
+                    for (int q = 0; q < nu; q++) put_rec(h->sc_slot[q], un[4 * q], un[4 * q + 1], un[4 * q + 2]);
+                } else {
+                    nu = roi_launch_order(members.data() + mfirst[f], count[f], geo.data(), DH, h->n_cu, qslots[f],
+                                          kn.roi_tail, sort, kn.roi_snake != 0, rg, h->sc_plan, put_rec);
+                }
                 HP(7);
             } else {
                 // outputs taller than one tile (DH > TH): row tiles of TH rows per ROI, the same order rules

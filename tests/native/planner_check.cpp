@@ -460,11 +460,43 @@ static void check_roi_launch_order() {
     printf("ROI launch order: fused planner equals the multi-pass plan on %d groups\n", cases);
 }
 
+// The frame-to-XCD deal (EVAM_PP_ROI_XCD=1): a permutation of the launch positions; every unit inside the interleave
+// (positions below 8 x the smallest XCD's unit count) sits on its frame's XCD (position % 8); the XCDs' summed costs
+// differ by at most the largest frame's cost (LPT).
+static void check_roi_xcd_deal() {
+    int cases = 0;
+    for (int it = 0; it < 2000; it++) {
+        const int n_frames = uni(1, 64), nu = uni(1, 3000), n_cu = it % 3 ? 256 : 8 * uni(1, 40);
+        std::vector<int> frame(nu), cost(nu), pos, scr;
+        for (int q = 0; q < nu; q++) { frame[q] = uni(0, n_frames - 1); cost[q] = uni(1, 16); }
+        std::sort(cost.begin(), cost.end(), [](int a, int b) { return a > b; });
+        roi_xcd_deal(frame.data(), cost.data(), nu, n_frames, n_cu, 8, pos, scr);
+        std::vector<int> hit(nu, 0);
+        for (int q = 0; q < nu; q++) {
+            CHECK(pos[q] >= 0 && pos[q] < nu, "xcd deal: position %d of %d (case %d)", pos[q], nu, it);
+            if (pos[q] >= 0 && pos[q] < nu) hit[pos[q]]++;
+        }
+        for (int p = 0; p < nu; p++) CHECK(hit[p] == 1, "xcd deal: position %d used %d times (case %d)", p, hit[p], it);
+        const int* fxcd = scr.data() + n_frames;  // the frame -> XCD map the deal leaves in its scratch
+        std::vector<int64_t> cnt(8, 0), load(8, 0), fcost(n_frames, 0);
+        for (int q = 0; q < nu; q++) { cnt[fxcd[frame[q]]]++; load[fxcd[frame[q]]] += cost[q]; fcost[frame[q]] += cost[q]; }
+        const int64_t n_min = *std::min_element(cnt.begin(), cnt.end());
+        for (int q = 0; q < nu; q++)
+            if (pos[q] < 8 * n_min) CHECK(pos[q] % 8 == fxcd[frame[q]], "xcd deal: unit %d off its frame's XCD (case %d)", q, it);
+        const int64_t spread = *std::max_element(load.begin(), load.end()) - *std::min_element(load.begin(), load.end());
+        CHECK(spread <= *std::max_element(fcost.begin(), fcost.end()), "xcd deal: XCD loads spread %lld (case %d)",
+              (long long)spread, it);
+        cases++;
+    }
+    printf("ROI XCD deal: %d random unit lists, permutations, frames on their XCDs, LPT-balanced\n", cases);
+}
+
 int main() {
     check_six_columns();
     check_clip_simd();
     check_roi_tail();
     check_roi_launch_order();
+    check_roi_xcd_deal();
     check_geometry();
     check_linear_tables();
     check_footprints();

@@ -113,18 +113,22 @@ def test_c2_bench_batch(evam, O, coracle, gpu, shape, monkeypatch):
     pp.close()
 
 
-@pytest.mark.parametrize("kernel", ["roi_tail1", "roi", "roi_noprio", "roi_unsorted", "roi_pinned"])
+@pytest.mark.parametrize("kernel", ["roi_tail1", "roi", "roi_noprio", "roi_unsorted", "roi_pinned", "roi_xcd"])
 @pytest.mark.parametrize("seed", [0, 3])
 def test_c3_bench_roi_set(evam, O, coracle, gpu, seed, kernel, monkeypatch):
     """C3: bench.py's seeded ROI set (50 per frame, w 24..400, h 24..300) on 32 bench 1080p NV12 frames ->
     1600x3x72x72 fp32 through the ROI kernel, with and without its tail split (EVAM_PP_ROI_TAIL: the 64 ROIs beyond 6
     per CU as row tiles), without progress-based priority (EVAM_PP_PRIO=0), without the largest-bytes pre-order and
-    the snake deal over the CUs (EVAM_PP_ROI_SORT=0 EVAM_PP_ROI_SNAKE=0) and with the records in pinned host memory
-    instead of host-written device memory (EVAM_PP_REC_DEVICE=0)."""
+    the snake deal over the CUs (EVAM_PP_ROI_SORT=0 EVAM_PP_ROI_SNAKE=0), with the records in pinned host memory
+    instead of host-written device memory (EVAM_PP_REC_DEVICE=0) and with each frame's ROIs dealt to one XCD
+    (EVAM_PP_ROI_XCD=1)."""
     import torch
 
     if kernel == "roi_pinned":
         monkeypatch.setenv("EVAM_PP_REC_DEVICE", "0")
+        kernel = "roi"
+    if kernel == "roi_xcd":  # each frame's ROIs dealt to one XCD (EVAM_PP_ROI_XCD=1)
+        monkeypatch.setenv("EVAM_PP_ROI_XCD", "1")
         kernel = "roi"
     if kernel.endswith("_noprio"):
         monkeypatch.setenv("EVAM_PP_PRIO", "0")
