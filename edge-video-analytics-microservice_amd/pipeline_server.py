@@ -515,7 +515,7 @@ class DeviceRunner:
         self._pipes: list = []
         self._draining: list = []  # ended pipelines whose destination still holds back results (queue full)
         self._ticks = 0            # ticks run; tick t uses the hub's slot t mod hub.inflight
-        self._pending = None       # the last tick, launched but not completed (hub.inflight > 1)
+        self._pending = collections.deque()  # ticks launched, not completed (at most hub.inflight - 1, oldest first)
         self._cv = threading.Condition()
         self._stop = False
         self._thread = threading.Thread(target=self._guarded_loop, name=f"evam-runner-{hub.device}", daemon=True)
@@ -675,10 +675,10 @@ class DeviceRunner:
     def _tick(self, work):
         """Run the stage chains of `work` [(pipeline, frames)] stage by stage, batched across pipelines, on the
         hub's next slot (handle and stream). With ``hub.inflight`` > 1 a batch whose stage ends every chain in it
-        and can launch without completing (``launch_batch``: detection) is only enqueued here; its completion,
-        the pipelines' bookkeeping and the tick's results wait until the next tick has been launched, so the
-        next tick's kernels overlap this one's tail. Ticks complete in launch order, so every stream's results
-        keep their order."""
+        and can launch without completing (``launch_batch``: detection, action recognition) is only enqueued here;
+        its completion, the pipelines' bookkeeping and the tick's results wait until ``hub.inflight`` - 1 later ticks
+        have been launched, so the next ticks' kernels overlap this one's tail. Ticks complete in launch order, so
+        every stream's results keep their order."""
         hub = self.hub
         slot = self._ticks % hub.inflight
         self._ticks += 1
@@ -741,17 +741,21 @@ class DeviceRunner:
                         if not defer:
                             self._finish_batch(chunk, failed, fail)
         tick = (slot, deferred, work, failed)
-        prev, self._pending = self._pending, None
-        if prev is not None:
-            self._complete(prev)
-        for p, e in errors:  # a stream's earlier results (the previous tick) precede its error
+        if errors or not deferred:
+            # a stream's earlier results (the pending ticks) precede its error and this tick's results
+            self._complete_pending()
+        for p, e in errors:
             self._finish(p, e)
         if errors:
             # out of the runner now, not when this tick completes: a deferred tick may stay pending, and the
             # loop must not ingest or schedule a stream whose end-of-stream marker is already out
             self._drop({p for p, _ in errors})
         if deferred:
-            self._pending = tick
+            # up to hub.inflight ticks launched: complete the oldest beyond inflight - 1 pending (in launch order), so
+            # the next tick's launch goes out while the others still run
+            self._pending.append(tick)
+            while len(self._pending) > max(1, hub.inflight - 1):
+                self._complete(self._pending.popleft())
         else:
             self._complete(tick)
 
@@ -797,9 +801,8 @@ class DeviceRunner:
             self._pipes = [p for p in self._pipes if p not in pipes]
 
     def _complete_pending(self):
-        if self._pending is not None:
-            tick, self._pending = self._pending, None
-            self._complete(tick)
+        while self._pending:
+            self._complete(self._pending.popleft())
 
 
 class _InferenceStage:

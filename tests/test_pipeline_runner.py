@@ -403,13 +403,13 @@ def test_runner_keeps_two_ticks_in_flight(stubbed, monkeypatch):
 
     monkeypatch.setattr(ps.DetectStage, "launch_batch", launch)
 
-    def run(inflight):
+    def run(inflight, counts=(9, 6, 11)):
         events.clear()
         ps.PipelineServer.start({"pipeline_dir": PIPES, "model_dir": mdir, "batch_max": 4, "batch_target": 4,
                                  "batch_wait_ms": 200, "inflight": inflight})
         register(ps, det_every=1)  # a car in every frame: the results do not depend on how ticks group frames
         outs, pipes = [], []
-        for k, n in enumerate([9, 6, 11]):
+        for k, n in enumerate(counts):
             qin, qout = queue.Queue(), queue.Queue()
             for im in frames(pre, n):
                 qin.put(im)
@@ -440,6 +440,19 @@ def test_runner_keeps_two_ticks_in_flight(stubbed, monkeypatch):
     assert any(pos[("launch", t + 1)] < pos[("complete", t)] for t in range(len(order) - 1))
     handles = [e[2] for e in ev2 if e[0] == "launch"]
     assert len(set(handles)) == 2
+    # inflight 3: three ticks launched before the oldest completes (two pending), on three handles, same results
+    long_counts = (40, 30, 50)
+    three, ev3 = run(3, long_counts)
+    assert three == run(1, long_counts)[0] and [len(g) for g in three] == list(long_counts)
+    three, ev3 = run(3, long_counts)
+    order = [e[1] for e in ev3 if e[0] == "complete"]
+    assert order == sorted(order) and len(order) == len([e for e in ev3 if e[0] == "launch"])
+    pos = {(e[0], e[1]): i for i, e in enumerate(ev3)}
+    # a batch still pending while batches on both other handles were launched after it
+    hid = {e[1]: e[2] for e in ev3 if e[0] == "launch"}
+    assert any(len({hid[u] for u in hid if u > t and pos[("launch", u)] < pos[("complete", t)]} - {hid[t]}) == 2
+               for t in order)
+    assert len(set(hid.values())) == 3
 
 
 @pytest.mark.parametrize("inflight", [1, 2])
