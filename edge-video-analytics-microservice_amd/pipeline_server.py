@@ -546,16 +546,28 @@ class DeviceRunner:
                 draining, self._draining = list(self._draining), []
                 self._stop = True
             for p in pipes + draining:
-                try:
-                    p._fail(e)
-                except Exception:  # noqa: BLE001 — the destination's own error; the pipeline ends either way
-                    pass
+                ended = p in draining  # already ended (COMPLETED / ABORTED), only handing over held-back results
+                if not ended:
+                    try:
+                        p._fail(e)
+                    except Exception:  # noqa: BLE001 — the destination's own error; the pipeline ends either way
+                        pass
                 if p._out_backlog:
-                    # no thread is left to hand the held-back results over: report them, never block wait()
-                    n = len(p._out_backlog)
-                    p.error = f"{p.error or type(e).__name__ + ': ' + str(e)}; {n} result(s) undelivered"
-                    p.state = p.ERROR
+                    # no thread is left to hand the held-back results over: report them, never block wait(). The
+                    # end-of-stream marker queued behind them is offered once more, so a consumer reading until None
+                    # still ends when its queue has room; a pipeline that had ended keeps its state.
+                    n = sum(1 for x in p._out_backlog if x is not None)
                     p._out_backlog.clear()
+                    dst = p.destination.get("metadata", p.destination)
+                    out = dst.get("output")
+                    try:
+                        if out is not None and hasattr(out, "put_nowait"):
+                            out.put_nowait(None)
+                    except Exception:  # noqa: BLE001 — a full queue: the marker cannot be delivered either
+                        pass
+                    p.error = f"{p.error or type(e).__name__ + ': ' + str(e)}; {n} result(s) undelivered"
+                    if not ended:
+                        p.state = p.ERROR
                 p._done.set()
 
     def _drain(self):

@@ -551,6 +551,33 @@ def test_runner_death_with_held_back_results(stubbed, monkeypatch):
     assert st["state"] == "ERROR" and "runner bug" in st["message"] and "undelivered" in st["message"], st
 
 
+def test_runner_death_while_draining_keeps_state(stubbed, monkeypatch):
+    """a pipeline that had already ended (COMPLETED) and was only handing held-back results to a full
+    destination keeps its state when the runner thread dies; it reports the undelivered results (the end-of-stream
+    marker not counted) and wait() returns."""
+    import time
+
+    ps, pre, mdir = stubbed
+    ps.PipelineServer.start({"pipeline_dir": PIPES, "model_dir": mdir, "batch_max": 64, "batch_target": 12})
+    register(ps)
+    q = queue.Queue(maxsize=1)
+    p = _start(ps, pre, 12, q, batch=12)  # one tick runs the whole stream, then its end of stream
+    t0 = time.time()
+    while p.state != "COMPLETED" and time.time() - t0 < 30:
+        time.sleep(0.01)
+    assert p.state == "COMPLETED" and p._out_backlog and not p._done.is_set()
+
+    def boom(self):
+        raise RuntimeError("runner bug")
+
+    monkeypatch.setattr(ps.DeviceRunner, "_drain", boom)
+    st = p.wait(30)
+    assert p._done.is_set(), "wait() timed out behind a dead runner"
+    assert st["state"] == "COMPLETED" and "runner bug" in st["message"] and "undelivered" in st["message"], st
+    n = int(st["message"].split("; ")[-1].split()[0])
+    assert n == 12 - 1  # twelve results, one of them delivered (the queue holds it); the marker is not a result
+
+
 @pytest.mark.parametrize("runner", ["device", "threads"])
 def test_action_stage_shared_ring_slots(stubbed, runner, monkeypatch):
     """gvaactionrecognitionbin batched across streams (CPU, stubbed pre-processor, ring pages on the host): each launch
