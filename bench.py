@@ -3,7 +3,7 @@
 
 Default workload (BASELINE.json configs[1], "C2"): a batch of 32 synthetic 1920x1080 NV12 frames,
 device-resident, -> 32x3x512x512 fp32 NCHW normalised (range [0,1], ImageNet mean/std in BGR order),
-one fused kernel launch per step, two steps in flight on two handles / HIP streams (the shape
+one fused kernel launch per step, three steps in flight on three handles / HIP streams (the shape
 PipelineServer's device runner runs by default; `--inflight 1` times one launch at a time, and every
 line carries that one-at-a-time kernel figure as roofline.single_launch). Other configs (--config
 c1|c3|c4|c5) are the remaining BASELINE workloads; the driver's headline line is c2.
@@ -381,12 +381,12 @@ def main():
     ap.add_argument("--frames-per-stream", type=int, default=16384, help="--via pipeline: frames per stream")
     ap.add_argument("--stream-batch", type=int, default=16, help="--via pipeline: gvadetect batch-size per stream")
     ap.add_argument("--hub-batch", type=int, default=256, help="--via pipeline: max frames per hub launch")
-    ap.add_argument("--inflight", type=int, default=2,
-                    help="launches in flight: step t runs on handle/stream t mod N (independent outputs), so launch "
-                         "t+1's ramp overlaps launch t's tail, timed by wall clock. The default 2 is the shape the "
-                         "product runs (PipelineServer's device runner, server option inflight=2); the one-launch-at-"
+    ap.add_argument("--inflight", type=int, default=3,
+                    help="launches in flight: step t runs on handle/stream t mod N (independent outputs), so the next "
+                         "launches' ramps overlap launch t's tail, timed by wall clock. The default 3 is the shape the "
+                         "product runs (PipelineServer's device runner, server option inflight=3); the one-launch-at-"
                          "a-time kernel figure is reported next to it as roofline.single_launch either way")
-    ap.add_argument("--runner-inflight", type=int, default=2,
+    ap.add_argument("--runner-inflight", type=int, default=3,
                     help="--via pipeline: ticks the device runner keeps in flight (server option inflight)")
     ap.add_argument("--runner", choices=["device", "threads"], default="device",
                     help="--via pipeline: one runner thread per device (default) or one thread per pipeline")

@@ -360,8 +360,9 @@ class BatchHub:
     def __init__(self, device: int, max_batch: int = 64, max_wait_s: float = 0.002, target: int | None = None,
                  drain_timeout_s: float = 2.0, inflight: int = 1):
         self.device = int(device)
-        # ticks the device runner keeps in flight: tick t runs on handle / stream t mod inflight, so tick t+1's
-        # launch ramp overlaps tick t's tail (bench.py --inflight: C5 +30 %, C2 +14 % at the launch level)
+        # ticks the device runner keeps in flight: tick t runs on handle / stream t mod inflight, so the next ticks'
+        # launch ramps overlap tick t's tail (server default 3: C2 through the runner 865 k -> 920 k f/s against 2,
+        # 4 slower, C1 / C4 / C5 equal within noise; profiles/r06f_pipeline_inflight.txt)
         self.inflight = max(1, int(inflight))
         self.drain_timeout_s = float(drain_timeout_s)  # runner shutdown: how long held-back results may wait
         self.max_batch = max(1, int(max_batch))
@@ -1580,7 +1581,7 @@ class _Server:
                                                 max_wait_s=float(o.get("batch_wait_ms", 2.0)) / 1e3,
                                                 target=o.get("batch_target"),
                                                 drain_timeout_s=float(o.get("drain_timeout_ms", 2000.0)) / 1e3,
-                                                inflight=int(o.get("inflight", 2)))
+                                                inflight=int(o.get("inflight", 3)))
             return h
 
     def runner(self, slot: int = 0) -> DeviceRunner:

@@ -231,10 +231,11 @@ def test_c5_bgrx_ring_step(evam, O, coracle, gpu, variant, monkeypatch):
     pp.close()
 
 
+@pytest.mark.parametrize("n_streams", [2, 3])
 @pytest.mark.parametrize("config", ["c5", "c2"])
-def test_inflight_two_streams_bit_equal(evam, gpu, config):
-    """bench.py --inflight 2: successive launches alternate between two handles bound to two HIP streams (their
-    outputs are independent, so launch t+1's ramp overlaps launch t's tail). The tensors equal one-at-a-time
+def test_inflight_two_streams_bit_equal(evam, gpu, config, n_streams):
+    """bench.py --inflight N (default 3): successive launches rotate over N handles bound to N HIP streams (their
+    outputs are independent, so the next launches' ramps overlap launch t's tail). The tensors equal one-at-a-time
     launches on one stream bit for bit (C5: four ring steps into one [32,16,...] clip ring; C2: four batches)."""
     import torch
 
@@ -257,7 +258,7 @@ def test_inflight_two_streams_bit_equal(evam, gpu, config):
         return [o.cpu() for o in outs]
 
     serial = run([evam.HipPreProcessor(device=0)], [torch.cuda.current_stream(gpu)])
-    streams = [torch.cuda.Stream(gpu) for _ in range(2)]
+    streams = [torch.cuda.Stream(gpu) for _ in range(n_streams)]
     pps = [evam.HipPreProcessor(device=0, stream=s) for s in streams]
     two = run(pps, streams)
     for a, b in zip(serial, two):

@@ -384,7 +384,8 @@ def test_runner_survives_an_internal_error(stubbed, monkeypatch):
 
 
 def test_runner_keeps_two_ticks_in_flight(stubbed, monkeypatch):
-    """with inflight 2 (the default) the device runner launches tick t+1 before it completes tick t
+    """with inflight 2 (3 is the default since round 6) the device runner launches tick t+1 before it
+    completes tick t
     (model output to the host, detections, results), on the hub's alternate slot; ticks still complete in launch
     order and every stream's results are those of inflight 1, in order, end-of-stream marker last."""
     ps, pre, mdir = stubbed

@@ -20,6 +20,7 @@
 #   pmc:c2,c3,...     FETCH_SIZE / WRITE_SIZE passes per config (tools/pmc.sh) -> pmc_traffic_TAG_<cfg>.json
 #   valu:c1,...       SQ_INSTS_VALU pass per config (tools/pmc.sh)
 #   stall:c1,...      stall-attribution passes per config (tools/pmc.sh, two SQ groups)
+#   scalar:c1,...     scalar-issue passes (SALU counts and cycles, SALUBusy / VALUBusy)
 #   hostprof:c3       host time per evam_pp_run section (needs ab/libevam_pp_hostprof.so) -> hostprof_TAG.txt
 #   ab:CFG:SET1|SET2  same-box alternating env / option A/B (tools/gpu_env_ab.sh)
 #   dist              bench.py under torch.distributed.run, 2 ranks sharing the GPU over gloo
@@ -109,6 +110,13 @@ PY
     valu)
       for c in $cfgs; do
         PMC_GROUPS="SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVES" bash tools/pmc.sh "${TAG}_valu_$c" "$c"
+      done ;;
+    scalar)
+      # scalar issue: SALU instructions and cycles, scalar-active wave cycles next to VALU, then the
+      # derived SALUBusy / VALUBusy percentages (one launch at a time)
+      for c in $cfgs; do
+        PMC_GROUPS="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_SALU SQ_INST_CYCLES_SALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_VALU SQ_INSTS_VALU GRBM_GUI_ACTIVE;SALUBusy VALUBusy" \
+          bash tools/pmc.sh "${TAG}_scalar_$c" "$c"
       done ;;
     stall)
       # Stall attribution: WAIT_ANY (parked on s_waitcnt / barrier) + WAIT_INST_ANY (issue stall; WAIT_INST_LDS is
