@@ -321,26 +321,28 @@ inline int roi_launch_order(const int* idx, int n, const evam::Geom* geo, int DH
     if (n <= 0) return 0;
     sc.resize(2 * (size_t)n);
     uint32_t* e_of = sc.data();       // per ROI: R | groups << 16
-    uint32_t* b_of = sc.data() + n;   // per ROI: bytes bucket | split flag << 8
+    uint32_t* b_of = sc.data() + n;   // per ROI: work estimate (pass 1), then bytes bucket | split flag << 8
     int maxcost = 1;
-    int64_t maxw = 1;
+    uint32_t maxw = 1;
+    const int dh2 = 2 * DH;
     for (int m = 0; m < n; m++) {
         const evam::Geom& g = geo[idx[m]];
         const uint32_t e = rg(g.cw);
         e_of[m] = e;
         maxcost = std::max(maxcost, (int)(e >> 16));
-        if (sort) maxw = std::max(maxw, (int64_t)g.cw * std::min(g.ch, 2 * DH));
+        // crop width x touched rows: < 2^30 (frames are at most 32,768 on a side, validated by the caller)
+        const uint32_t w = (uint32_t)g.cw * (uint32_t)std::min(g.ch, dh2);
+        b_of[m] = w;
+        maxw = std::max(maxw, w);
     }
     int hist64[64] = {0};
     if (sort) {
+        // roi_largest_first's buckets from the stored estimates: a sequential pass the compiler vectorises, then the
+        // histogram (the geometry is not gathered twice)
         const double to_bucket = 63.0 / (double)maxw;
-        for (int m = 0; m < n; m++) {
-            const evam::Geom& g = geo[idx[m]];
-            const int64_t w = (int64_t)g.cw * std::min(g.ch, 2 * DH);
-            const uint32_t b = 63u - (uint32_t)std::min(63, (int)((double)w * to_bucket));  // 0 = largest
-            b_of[m] = b;
-            hist64[b]++;
-        }
+        for (int m = 0; m < n; m++)
+            b_of[m] = 63u - (uint32_t)std::min(63, (int)((double)b_of[m] * to_bucket));  // 0 = largest
+        for (int m = 0; m < n; m++) hist64[b_of[m]]++;
     } else {
         std::fill(b_of, b_of + n, 0u);
         hist64[0] = n;

@@ -25,6 +25,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdarg>
+#include <cstddef>
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
@@ -1582,6 +1583,11 @@ struct alignas(64) RoiRec {  // 64 B
     uint16_t row0, row1;      // output rows [row0, row1) of this tile (DH <= 65535 for split tiles)
 };
 static_assert(sizeof(RoiRec) == 64, "RoiRec layout");
+// The host builds a record as four 16-byte lines: the frame's first 40 bytes (planes, pitches, size; prepared once per
+// source and call), the caller's rect (evam_roi x, y, w, h: 16 contiguous bytes), then the output index and rows.
+static_assert(offsetof(RoiRec, x) == 40 && offsetof(RoiRec, item) == 56 && offsetof(RoiRec, row0) == 60, "RoiRec lines");
+static_assert(offsetof(evam_roi, h) == offsetof(evam_roi, x) + 12, "evam_roi rect");
+struct RecFrame { __m128i l[3]; };  // a record's bytes 0-47 for one source (bytes 40-47 zero)
 
 // ------------------------------------------------------------------------------------------------
 // strip kernel (uniform geometry, 4:2:0 sources, no shared source rows between output rows)
@@ -3736,6 +3742,7 @@ struct evam_pp {
     std::vector<int> sc_slot;      // ROI units in launch order
     std::vector<uint8_t> sc_seen;  // evam_pp_run_slots: output slots taken
     std::vector<uint32_t> sc_plan; // roi_launch_order scratch
+    std::vector<RecFrame> sc_frames;  // per source: the frame half of its ROI records
     int memo_key[4] = {-1, -1, -1, -1};  // (format, staging buffer, row cap, DH) of memo_rg
     std::vector<uint32_t> memo_rg;       // per crop width: rows per group | groups of the whole height << 16
     TParams sc_tparams;            // strip-kernel arguments (3.5 KB: kept off the stack)
@@ -4193,27 +4200,42 @@ int run_impl(evam_pp* h, const evam_image* srcs, int n_srcs, const evam_roi* ite
         // bytes, crop width x touched rows). Workgroups are dispatched in order as slots free, so
         // the long ROIs start first and the short ones fill the tail.
         const bool sort = kn.roi_sort != 0;
+        // the frame half of the records, once per source (a record then takes three of its lines from here)
+        std::vector<RecFrame>& rfr = h->sc_frames;
+        rfr.resize((size_t)n_srcs);
+        for (int s = 0; s < n_srcs; s++) {
+            RoiRec r;
+            memset(&r, 0, sizeof(r));
+            r.plane[0] = srcs[s].planes[0]; r.plane[1] = srcs[s].planes[1]; r.plane[2] = srcs[s].planes[2];
+            r.pitch[0] = srcs[s].pitch[0]; r.pitch[1] = srcs[s].pitch[1]; r.pitch[2] = srcs[s].pitch[2];
+            r.width = (uint16_t)srcs[s].width; r.height = (uint16_t)srcs[s].height;
+            memcpy(&rfr[s], &r, sizeof(RecFrame));
+        }
         for (int f = 0; f < 4; f++) {
             if (path[f] != kPathRoi) continue;
             RoiRec* rr = reinterpret_cast<RoiRec*>(dyn + rec_off[f]);
-            // One record per work unit, built in registers and written as one 64-byte line into its launch slot.
+            // One record per work unit, assembled in four XMM registers and written as one 64-byte line into its
+            // launch slot: the frame's lines, the caller's rect (w <= 0 without items: the full frame), the output
+            // index and the tile's rows.
+            const RecFrame* rf = rfr.data();
             auto put_rec = [&](int pos, int i, int row0, int row1) {
-                const evam_image& sim = srcs[items ? items[i].src_index : i];
-                RoiRec r;
-                r.plane[0] = sim.planes[0]; r.plane[1] = sim.planes[1]; r.plane[2] = sim.planes[2];
-                r.pitch[0] = sim.pitch[0]; r.pitch[1] = sim.pitch[1]; r.pitch[2] = sim.pitch[2];
-                r.width = (uint16_t)sim.width; r.height = (uint16_t)sim.height;
-                if (items) { r.x = items[i].x; r.y = items[i].y; r.w = items[i].w; r.h = items[i].h; }
-                else { r.x = r.y = r.w = r.h = 0; }  // w <= 0: the full frame
-                r.item = slots ? slots[i] : i;
-                r.row0 = (uint16_t)row0;
-                r.row1 = (uint16_t)row1;
+                const RecFrame& F = rf[items ? items[i].src_index : i];
+                const __m128i rect = items ? _mm_loadu_si128(reinterpret_cast<const __m128i*>(&items[i].x)) : _mm_setzero_si128();
+                const uint64_t tail = (uint64_t)(uint32_t)(slots ? slots[i] : i) |
+                                      ((uint64_t)((uint32_t)(uint16_t)row0 | ((uint32_t)(uint16_t)row1 << 16)) << 32);
+                const __m128i l2 = _mm_unpacklo_epi64(F.l[2], rect);
+                const __m128i l3 = _mm_unpackhi_epi64(rect, _mm_set_epi64x((long long)tail, 0));
+                __m128i* dst = reinterpret_cast<__m128i*>(&rr[pos]);
                 if (dyn_wc) {  // write-combined device memory: the 64-byte line as four streaming stores
-                    const __m128i* src = reinterpret_cast<const __m128i*>(&r);
-                    __m128i* dst = reinterpret_cast<__m128i*>(&rr[pos]);
-                    for (int k = 0; k < 4; k++) _mm_stream_si128(dst + k, _mm_load_si128(src + k));
+                    _mm_stream_si128(dst + 0, F.l[0]);
+                    _mm_stream_si128(dst + 1, F.l[1]);
+                    _mm_stream_si128(dst + 2, l2);
+                    _mm_stream_si128(dst + 3, l3);
                 } else {
-                    memcpy(&rr[pos], &r, sizeof(RoiRec));
+                    _mm_store_si128(dst + 0, F.l[0]);
+                    _mm_store_si128(dst + 1, F.l[1]);
+                    _mm_store_si128(dst + 2, l2);
+                    _mm_store_si128(dst + 3, l3);
                 }
             };
             // Work units (one workgroup each): one per ROI, or per row tile of TH rows for outputs taller than one

@@ -130,3 +130,64 @@ def test_library_has_no_undefined_kernel_symbols():
     out = subprocess.run(["nm", "-D", "--undefined-only", lib], capture_output=True, text=True, check=True).stdout
     bad = [ln.split()[-1] for ln in out.splitlines() if "evam" in ln]
     assert not bad, bad
+
+
+def test_convert_host_caches_follow_changes(evam):
+    """HipPreProcessor.convert's per-call caches (no GPU: a recording stand-in for evam_pp_run, and the device check
+    of the output tensor skipped): the evam_tensor of an output tensor is reused only while the tensor object, its
+    version and storage are unchanged (resize_ re-validates), each of several output tensors keeps its own, and the
+    C config follows every change of the PreProcInfo, in-place list edits included."""
+    import torch
+
+    native = evam.native
+    P = evam.HipPreProcessor
+    calls = []
+
+    class Rec(P):
+        def _tensor_entry(self, out):  # as the product's, minus the cuda-device check (CPU tensors here)
+            t = native.EvamTensor()
+            t.data = out.data_ptr()
+            t.n, t.c, t.h, t.w = (int(v) for v in out.shape)
+            dt = native.DTYPE_F32
+            import weakref
+
+            e = (weakref.ref(out), out._version, t.data, t, dt, ctypes.byref(t))
+            self._tdesc[id(out)] = e
+            return e
+
+    def fake_run(h, arr, n_srcs, items, n_items, cfg, tref, xf):
+        c, t = cfg._obj, tref._obj
+        calls.append({"n": t.n, "data": t.data, "off": t.slot_offset, "stride": t.slot_stride,
+                      "mean": tuple(c.mean), "t": id(t)})
+        return 0
+
+    pp = Rec.__new__(Rec)
+    pp._torch, pp.device, pp._h = torch, 0, None
+    pp._tdesc, pp._cfg_cache, pp._last_cfg = {}, {}, None
+    pp._default_info = evam.PreProcInfo()
+    pp._run, pp._bind_stream = fake_run, lambda: None
+    batch = evam.ImageBatch.__new__(evam.ImageBatch)
+    batch.images, batch.c_array = [None], (native.EvamImage * 1)()
+
+    a, b = torch.empty(4, 3, 8, 8), torch.empty(6, 3, 8, 8)
+    info = evam.PreProcInfo(mean=(1.0, 2.0, 3.0), std=(1.0, 1.0, 1.0))
+    pp.convert(batch, a, info)
+    pp.convert(batch, a, info, slot_offset=2)
+    assert calls[-1]["t"] == calls[-2]["t"] and calls[-1]["off"] == 2 and calls[-1]["n"] == 4
+    pp.convert(batch, b, info)
+    pp.convert(batch, a, info)
+    assert (calls[-2]["n"], calls[-1]["n"]) == (6, 4) and calls[-1]["data"] == a.data_ptr()
+    a.resize_(2, 3, 8, 8)
+    pp.convert(batch, a, info)
+    assert calls[-1]["n"] == 2
+    info.mean = (4.0, 5.0, 6.0)
+    pp.convert(batch, a, info)
+    assert calls[-1]["mean"] == (4.0, 5.0, 6.0)
+    info.mean = [7.0, 8.0, 9.0]
+    pp.convert(batch, a, info)
+    info.mean[0] = 10.0
+    pp.convert(batch, a, info)
+    assert calls[-2]["mean"] == (7.0, 8.0, 9.0) and calls[-1]["mean"] == (10.0, 8.0, 9.0)
+    other = evam.PreProcInfo(mean=(10.0, 8.0, 9.0), std=(1.0, 1.0, 1.0))
+    pp.convert(batch, a, other)
+    assert calls[-1]["mean"] == (10.0, 8.0, 9.0)

@@ -15,7 +15,7 @@
 #   pipe[:c2,c5]      bench.py --via pipeline per config (default c2, + its rocprof kernel stats); HUB, PIPE_ARGS
 #   bench:c1,c2,...   one bench line per config (BENCH_STEPS, default 1000; CPU baseline unless CPU=0)
 #   prof:c1,c2,...    rocprofv3 --kernel-trace --stats per config (tools/prof_configs.sh, 200 steps, bench default:
-#                     two launches in flight)
+#                     three launches in flight)
 #   prof1:c1,c2,...   the same, one launch at a time (--inflight 1: the kernel-quality average) -> prof_TAG_single_*
 #   pmc:c2,c3,...     FETCH_SIZE / WRITE_SIZE passes per config (tools/pmc.sh) -> pmc_traffic_TAG_<cfg>.json
 #   valu:c1,...       SQ_INSTS_VALU pass per config (tools/pmc.sh)
