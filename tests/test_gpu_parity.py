@@ -5,6 +5,7 @@ through a host-built LUT computed in the reference's operation order, so the bar
 1e-6 relative — is met with zero error). Sizes are small enough for the oracle to finish in seconds, plus
 the full BASELINE configs through size-independent properties.
 """
+import os
 import zlib
 
 import numpy as np
@@ -740,3 +741,81 @@ def test_run_slots_explicit_output_slots(evam, O, coracle, gpu, kind, monkeypatc
     with pytest.raises(evam.PreProcError):
         pp.convert(imgs, out, info, rois=[evam.Roi(*r) for r in rois] if rois else None, slots=slots[:-1])
     pp.close()
+
+
+@pytest.fixture(scope="module")
+def fuzz_pp(evam, gpu):
+    """One handle for every fuzz case: descriptor-block, LUT, record-ring and convert-side caches all see churn."""
+    pp = evam.HipPreProcessor(device=0)
+    yield pp
+    pp.close()
+
+
+@pytest.mark.parametrize("seed", range(int(os.environ.get("EVAM_FUZZ_CASES", "96"))))
+def test_random_configurations(evam, O, coracle, gpu, fuzz_pp, seed):
+    """Seeded random calls over the whole input space the boundary accepts, each bit-exact against the oracle: any
+    source format, frame sizes from 2 to ~1,300 (odd widths for packed formats), pitch padding, tensor sizes from 1 to
+    ~700 (up- and downscales), the three resize modes and two placements, BGR / RGB order, fill values, u8 or fp32
+    with random range / mean / std, full frames or ROI lists (partly outside the frame, slivers, whole frames) over
+    several sources of mixed sizes, and slot offsets / strides; one handle for all cases."""
+    import torch
+
+    rng = np.random.default_rng(1000 + seed)
+    fmt = FORMATS[int(rng.integers(0, len(FORMATS)))]
+    yuv = fmt in ("NV12", "I420")
+    n_src = int(rng.integers(1, 4))
+    frames = []
+    for k in range(n_src):
+        big = rng.random() < 0.25
+        W = int(rng.integers(2, 1300 if big else 400))
+        H = int(rng.integers(2, 760 if big else 300))
+        if yuv:
+            W, H = W + (W & 1), H + (H & 1)
+        frames.append(O.random_frame(rng, fc(O, fmt), W, H, pitch_align=int(rng.choice([16, 64, 256])),
+                                     pattern="gradient" if rng.random() < 0.3 else "uniform"))
+    DW, DH = int(rng.integers(1, 700)), int(rng.integers(1, 500))
+    if rng.random() < 0.3:
+        DW = DH = int(rng.choice([72, 224, 256, 512]))
+    dtype = "f32" if rng.random() < 0.6 else "u8"
+    mode = ["no-aspect-ratio", "aspect-ratio", "crop"][int(rng.integers(0, 3))]
+    kw = {"resize": "aspect-ratio", "crop": "central"} if mode == "crop" else {"resize": mode}
+    kw["placement"] = "center" if rng.random() < 0.5 else "top_left"
+    kw["color_space"] = "RGB" if rng.random() < 0.5 else "BGR"
+    kw["fill"] = tuple(int(v) for v in rng.integers(0, 256, 3))
+    if dtype == "f32":
+        if rng.random() < 0.7:
+            kw["range"] = (0.0, float(rng.choice([1.0, 255.0])))
+        if rng.random() < 0.6:
+            kw["mean"] = tuple(float(v) for v in rng.uniform(0, 1, 3))
+            kw["std"] = tuple(float(v) for v in rng.uniform(0.1, 1, 3))
+    info = evam.PreProcInfo(**kw)
+    rois = None
+    if rng.random() < 0.6:
+        rois = []
+        for _ in range(int(rng.integers(1, 41))):
+            si = int(rng.integers(0, n_src))
+            W, H = frames[si].width, frames[si].height
+            r = rng.random()
+            if r < 0.1:
+                rois.append((si, 0, 0, W, H))
+            elif r < 0.15:
+                rois.append((si, 0, 0, 0, 0))  # w <= 0: the full frame
+            else:
+                x, y = int(rng.integers(-W // 4 - 1, W)), int(rng.integers(-H // 4 - 1, H))
+                w = int(rng.integers(1, max(2, W + W // 4)))
+                h = int(rng.integers(1, max(2, H + H // 4)))
+                rois.append((si, x, y, max(w, 1 - x), max(h, 1 - y)))  # at least one pixel inside
+        n_items = len(rois)
+    else:
+        n_items = n_src
+    stride = int(rng.integers(1, 3))
+    offset = int(rng.integers(0, 3))
+    shape = (offset + (n_items - 1) * stride + 1 + int(rng.integers(0, 2)), 3, DH, DW)
+    tdt = torch.float32 if dtype == "f32" else torch.uint8
+    what = f"seed {seed}: {fmt} {[(f.width, f.height) for f in frames]} -> {DW}x{DH} {dtype} {kw} " \
+           f"{'%d rois' % n_items if rois else 'frames'} offset {offset} stride {stride}"
+    got, _ = run_hip(evam, torch, upload(evam, frames, gpu), shape, tdt, info,
+                     rois=[evam.Roi(*r) for r in rois] if rois else None, slot_offset=offset, slot_stride=stride,
+                     pp=fuzz_pp)
+    ref, _ = run_oracle(O, coracle, frames, shape, dtype, info, rois=rois, slot_offset=offset, slot_stride=stride)
+    assert_same(got, ref, what)
