@@ -713,6 +713,9 @@ __global__ __launch_bounds__(kThreads) void evam_pp_rows(const RParams P) {
                         asm volatile("" :: "v"(v[0]), "v"(v[1]), "v"(v[2]));
                     } else {
                         if (P.color_rgb) { const int tmp = v[0]; v[0] = v[2]; v[2] = tmp; }
+                        if (wa[j] == 0) {  // letterbox padding column (zero weights): the fill, in output plane order
+                            v[0] = f0; v[1] = f1; v[2] = f2;
+                        }
                         const uint32_t vo = xo[j] * (uint32_t)esz;
                         if constexpr (OUT == 1) {
                             __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lut_s[v[0]]), rsD0, vo, sO, EVAM_PP_STORE_AUX);

@@ -184,6 +184,29 @@ def test_letterbox(evam, O, coracle, gpu, placement, fill):
         assert (t.crop_x, t.crop_y, t.crop_w, t.crop_h, t.resized_w, t.resized_h, t.pad_x, t.pad_y) == g
 
 
+@pytest.mark.parametrize("fmt", FORMATS)
+@pytest.mark.parametrize("dtype", ["u8", "f32"])
+@pytest.mark.parametrize("placement", ["top_left", "center"])
+def test_letterbox_strong_downscale(evam, O, coracle, gpu, fmt, dtype, placement):
+    """Letterbox columns and rows at > 15x downscales, where the kernel choice falls to the direct-tap row kernel
+    (evam_pp_rows): its padding columns carry the fill (round 6: found by test_random_calls_in_flight, the row kernel
+    wrote 0 there)."""
+    import torch
+
+    rng = np.random.default_rng(zlib.crc32(repr((fmt, dtype, placement)).encode()))
+    info = evam.PreProcInfo(resize="aspect-ratio", placement=placement, fill=(241, 17, 99), color_space="RGB",
+                            **({"range": (0.0, 1.0), "mean": (0.1, 0.2, 0.3), "std": (0.3, 0.2, 0.1)}
+                               if dtype == "f32" else {}))
+    for (W, H), (DW, DH) in (((1178, 566), (433, 26)), ((566, 1178), (26, 433)), ((1178, 566), (40, 40)),
+                             ((566, 1178), (40, 40))):
+        frames = [O.random_frame(rng, fc(O, fmt), W, H) for _ in range(2)]  # one size: a uniform-geometry launch
+        shape = (3, 3, DH, DW)
+        got, _ = run_hip(evam, torch, upload(evam, frames, gpu), shape, torch.float32 if dtype == "f32" else torch.uint8,
+                         info, slot_offset=1)
+        ref, _ = run_oracle(O, coracle, frames, shape, dtype, info, slot_offset=1)
+        assert_same(got, ref, f"strong downscale letterbox {fmt} {dtype} {placement} -> {DW}x{DH}")
+
+
 @pytest.mark.parametrize("fmt,src", [("NV12", (1920, 1080)), ("BGRX", (768, 432)), ("I420", (640, 480))])
 def test_aspect_central_crop(evam, O, coracle, gpu, fmt, src):
     """action-recognition-0001 model-proc: BGR, resize aspect-ratio, crop central, 224x224."""
@@ -365,14 +388,15 @@ def test_stats_and_timing(evam, O, gpu):
 @pytest.mark.parametrize("variant", ["auto", "wave", "px1", "px2", "noreuse", "staged", "staged_xcd", "staged_r1",
                                      "strip", "strip_unpaired", "strip_th5", "strip_nw8", "strip_px1", "strip_px2",
                                      "strip_px1_unpaired", "strip_px2_unpaired_th7", "strip_noprio", "band", "band_px1",
-                                     "band_px2", "band_th5", "band_th64", "band_ahead64", "band_noprio"])
+                                     "band_px2", "band_th5", "band_th64", "band_ahead64", "band_noprio", "rows"])
 def test_wave_kernel_variants(evam, O, coracle, gpu, fmt, src, dst, resize, variant, monkeypatch):
     """Uniform-geometry batches through the default kernel choice, the wave-row kernel forced
     (EVAM_PP_WAVE=2; every PX / REUSE choice), the staged kernel (EVAM_PP_WAVE=0 EVAM_PP_STRIP=0; with the
     XCD-contiguous tile order forced on small, non-multiple-of-8 grids: EVAM_PP_XCD=1) and the strip kernel
     (EVAM_PP_STRIP=2: forced even where output rows share source rows; every ring depth, an odd tile height,
     8 waves per workgroup, XCD order, 1 and 2 pixels per lane) and the band kernel (EVAM_PP_BAND=2: forced
-    on downscales too, every PX, short and 64-row bands), RGB order, fp32 with normalisation and u8."""
+    on downscales too, every PX, short and 64-row bands), the direct-tap row kernel (every other family off), RGB
+    order, fp32 with normalisation and u8."""
     import torch
 
     env = {"wave": {"EVAM_PP_WAVE": "2"}, "px1": {"EVAM_PP_WAVE": "2", "EVAM_PP_PX": "1"},
@@ -393,8 +417,9 @@ def test_wave_kernel_variants(evam, O, coracle, gpu, fmt, src, dst, resize, vari
            "band_th64": {"EVAM_PP_BAND": "2", "EVAM_PP_STRIP_TH": "64"},
            "strip_noprio": {"EVAM_PP_STRIP": "2", "EVAM_PP_PRIO": "0"},
            "band_ahead64": {"EVAM_PP_BAND": "2", "EVAM_PP_BAND_AHEAD": "64", "EVAM_PP_STRIP_TH": "20"},
-           "band_noprio": {"EVAM_PP_BAND": "2", "EVAM_PP_PRIO": "0"}}.get(variant, {})
-    if variant.startswith(("staged", "band")):
+           "band_noprio": {"EVAM_PP_BAND": "2", "EVAM_PP_PRIO": "0"},
+           "rows": {"EVAM_PP_WAVE": "0", "EVAM_PP_STAGED": "0", "EVAM_PP_BAND": "0"}}.get(variant, {})
+    if variant.startswith(("staged", "band", "rows")):
         env["EVAM_PP_STRIP"] = "0"
     for k, v in env.items():
         monkeypatch.setenv(k, v)
@@ -751,19 +776,13 @@ def fuzz_pp(evam, gpu):
     pp.close()
 
 
-@pytest.mark.parametrize("seed", range(int(os.environ.get("EVAM_FUZZ_CASES", "96"))))
-def test_random_configurations(evam, O, coracle, gpu, fuzz_pp, seed):
-    """Seeded random calls over the whole input space the boundary accepts, each bit-exact against the oracle: any
-    source format, frame sizes from 2 to ~1,300 (odd widths for packed formats), pitch padding, tensor sizes from 1 to
-    ~700 (up- and downscales), the three resize modes and two placements, BGR / RGB order, fill values, u8 or fp32
-    with random range / mean / std, full frames or ROI lists (partly outside the frame, slivers, whole frames) over
-    several sources of mixed sizes, and slot offsets / strides; one handle for all cases."""
-    import torch
-
-    rng = np.random.default_rng(1000 + seed)
+def random_case(evam, O, rng):
+    """One seeded random call over the whole input space the boundary accepts (test_random_configurations):
+    returns (fmt, frames, shape, dtype, info, rois or None, slot offset, slot stride)."""
     fmt = FORMATS[int(rng.integers(0, len(FORMATS)))]
     yuv = fmt in ("NV12", "I420")
     n_src = int(rng.integers(1, 4))
+    one_size = rng.random() < 0.4  # every source one size: full-frame calls take the uniform-geometry kernels
     frames = []
     for k in range(n_src):
         big = rng.random() < 0.25
@@ -771,6 +790,8 @@ def test_random_configurations(evam, O, coracle, gpu, fuzz_pp, seed):
         H = int(rng.integers(2, 760 if big else 300))
         if yuv:
             W, H = W + (W & 1), H + (H & 1)
+        if one_size and k:
+            W, H = frames[0].width, frames[0].height
         frames.append(O.random_frame(rng, fc(O, fmt), W, H, pitch_align=int(rng.choice([16, 64, 256])),
                                      pattern="gradient" if rng.random() < 0.3 else "uniform"))
     DW, DH = int(rng.integers(1, 700)), int(rng.integers(1, 500))
@@ -811,11 +832,64 @@ def test_random_configurations(evam, O, coracle, gpu, fuzz_pp, seed):
     stride = int(rng.integers(1, 3))
     offset = int(rng.integers(0, 3))
     shape = (offset + (n_items - 1) * stride + 1 + int(rng.integers(0, 2)), 3, DH, DW)
+    return fmt, frames, shape, dtype, info, rois, offset, stride
+
+
+@pytest.mark.parametrize("seed", range(int(os.environ.get("EVAM_FUZZ_CASES", "96"))))
+def test_random_configurations(evam, O, coracle, gpu, fuzz_pp, seed):
+    """Seeded random calls over the whole input space the boundary accepts, each bit-exact against the oracle: any
+    source format, frame sizes from 2 to ~1,300 (odd widths for packed formats), pitch padding, tensor sizes from 1 to
+    ~700 (up- and downscales), the three resize modes and two placements, BGR / RGB order, fill values, u8 or fp32
+    with random range / mean / std, full frames or ROI lists (partly outside the frame, slivers, whole frames) over
+    several sources of mixed sizes, and slot offsets / strides; one handle for all cases."""
+    import torch
+
+    fmt, frames, shape, dtype, info, rois, offset, stride = random_case(evam, O, np.random.default_rng(1000 + seed))
     tdt = torch.float32 if dtype == "f32" else torch.uint8
-    what = f"seed {seed}: {fmt} {[(f.width, f.height) for f in frames]} -> {DW}x{DH} {dtype} {kw} " \
-           f"{'%d rois' % n_items if rois else 'frames'} offset {offset} stride {stride}"
+    what = f"seed {seed}: {fmt} {[(f.width, f.height) for f in frames]} -> {shape} {dtype} {info} " \
+           f"{'%d rois' % len(rois) if rois else 'frames'} offset {offset} stride {stride}"
     got, _ = run_hip(evam, torch, upload(evam, frames, gpu), shape, tdt, info,
                      rois=[evam.Roi(*r) for r in rois] if rois else None, slot_offset=offset, slot_stride=stride,
                      pp=fuzz_pp)
     ref, _ = run_oracle(O, coracle, frames, shape, dtype, info, rois=rois, slot_offset=offset, slot_stride=stride)
     assert_same(got, ref, what)
+
+
+@pytest.mark.parametrize("n_handles", [1, 3])
+def test_random_calls_in_flight(evam, O, coracle, gpu, n_handles):
+    """40 random calls (random_case) enqueued back to back with no synchronisation, round-robin over handles bound to
+    their own HIP streams (the device runner's shape), each into its own output: the descriptor-block ring, the ROI
+    record ring and the LUT are reused while earlier kernels still run. After one synchronize every output equals the
+    oracle bit for bit."""
+    import torch
+
+    streams = [torch.cuda.Stream(device=gpu) for _ in range(n_handles)]
+    pps = [evam.HipPreProcessor(device=0, stream=s) for s in streams]
+    rng = np.random.default_rng(77 + n_handles)
+    cases = [random_case(evam, O, rng) for _ in range(int(os.environ.get("EVAM_FUZZ_INFLIGHT_CALLS", "40")))]
+    try:
+        # inputs and outputs first (default stream), then one synchronize: the calls below go out back to back
+        imgs = [upload(evam, c[1], gpu) for c in cases]
+        outs = [torch.full(c[2], 7, dtype=torch.float32 if c[3] == "f32" else torch.uint8, device=gpu) for c in cases]
+        torch.cuda.synchronize()
+        first = int(os.environ.get("EVAM_FUZZ_INFLIGHT_FIRST", "0"))  # (diagnostics: a sub-range of the calls,
+        sync_each = os.environ.get("EVAM_FUZZ_INFLIGHT_SYNC") == "1"    # or a synchronize after every call)
+        for k, (case, im, out) in enumerate(zip(cases, imgs, outs)):
+            if k < first:
+                continue
+            fmt, frames, shape, dtype, info, rois, offset, stride = case
+            pps[k % n_handles].convert(im, out, info, rois=[evam.Roi(*r) for r in rois] if rois else None,
+                                       slot_offset=offset, slot_stride=stride)
+            if sync_each:
+                torch.cuda.synchronize()
+        torch.cuda.synchronize()
+        for k, (case, out) in enumerate(zip(cases, outs)):
+            if k < first:
+                continue
+            fmt, frames, shape, dtype, info, rois, offset, stride = case
+            ref, _ = run_oracle(O, coracle, frames, shape, dtype, info, rois=rois, slot_offset=offset,
+                                slot_stride=stride)
+            assert_same(out.cpu().numpy(), ref, f"call {k} on handle {k % n_handles}: {fmt} -> {shape} {dtype}")
+    finally:
+        for pp in pps:
+            pp.close()
