@@ -893,3 +893,99 @@ def test_random_calls_in_flight(evam, O, coracle, gpu, n_handles):
     finally:
         for pp in pps:
             pp.close()
+
+
+# Kernel families switched off (the planner then chooses among the rest by its own feasibility rules) and the ROI
+# path's options: random calls through every family the product can reach, not only the one the default plan picks.
+FAMILY_ENVS = {
+    "no_strip": {"EVAM_PP_STRIP": "0"},
+    "no_strip_band": {"EVAM_PP_STRIP": "0", "EVAM_PP_BAND": "0"},
+    "staged_rows": {"EVAM_PP_STRIP": "0", "EVAM_PP_BAND": "0", "EVAM_PP_WAVE": "0"},
+    "rows_only": {"EVAM_PP_STRIP": "0", "EVAM_PP_BAND": "0", "EVAM_PP_WAVE": "0", "EVAM_PP_STAGED": "0"},
+    "no_uniform": {"EVAM_PP_ROWS": "0"},
+    "generic_only": {"EVAM_PP_ROWS": "0", "EVAM_PP_ROI": "0"},
+    "roi_px1": {"EVAM_PP_ROI_PX": "1"},
+    "roi_px4": {"EVAM_PP_ROI_PX": "4"},
+    "roi_unsorted": {"EVAM_PP_ROI_SORT": "0", "EVAM_PP_ROI_SNAKE": "0"},
+    "roi_no_tail": {"EVAM_PP_ROI_TAIL": "1"},
+    "roi_xcd": {"EVAM_PP_ROI_XCD": "1"},
+    "rec_host": {"EVAM_PP_REC_DEVICE": "0"},
+    "host_scalar": {"EVAM_PP_HOST_SIMD": "0"},
+}
+
+
+@pytest.mark.parametrize("family", sorted(FAMILY_ENVS))
+def test_random_kernel_families(evam, O, coracle, gpu, family, monkeypatch):
+    """random_case calls (EVAM_FUZZ_FAMILY_CASES each, default 12) on a handle created with one family switched off or
+    one ROI-path option set: every output bit-exact against the oracle."""
+    import torch
+
+    for k, v in FAMILY_ENVS[family].items():
+        monkeypatch.setenv(k, v)
+    pp = evam.HipPreProcessor(device=0)  # knobs are read when the handle is created
+    try:
+        rng = np.random.default_rng(zlib.crc32(family.encode()))
+        for n in range(int(os.environ.get("EVAM_FUZZ_FAMILY_CASES", "12"))):
+            fmt, frames, shape, dtype, info, rois, offset, stride = random_case(evam, O, rng)
+            tdt = torch.float32 if dtype == "f32" else torch.uint8
+            got, _ = run_hip(evam, torch, upload(evam, frames, gpu), shape, tdt, info,
+                             rois=[evam.Roi(*r) for r in rois] if rois else None, slot_offset=offset,
+                             slot_stride=stride, pp=pp)
+            ref, _ = run_oracle(O, coracle, frames, shape, dtype, info, rois=rois, slot_offset=offset,
+                                slot_stride=stride)
+            assert_same(got, ref, f"{family} case {n}: {fmt} {[(f.width, f.height) for f in frames]} -> {shape} "
+                                  f"{dtype} {info} {'%d rois' % len(rois) if rois else 'frames'}")
+    finally:
+        pp.close()
+
+
+@pytest.mark.parametrize("seed", range(int(os.environ.get("EVAM_FUZZ_SLOT_CASES", "24"))))
+def test_random_slots_and_large_batches(evam, O, coracle, gpu, fuzz_pp, seed):
+    """Random calls with an explicit output slot per item (evam_pp_run_slots: a random injective table into a larger
+    tensor) and batches past one launch's 64 kernel-argument items: up to 70 one-size frames, or up to 150 ROIs over a
+    few sources. Every written slot bit-exact against the oracle; every other slot untouched."""
+    import torch
+
+    rng = np.random.default_rng(50000 + seed)
+    fmt = FORMATS[int(rng.integers(0, len(FORMATS)))]
+    yuv = fmt in ("NV12", "I420")
+    W, H = int(rng.integers(8, 500)), int(rng.integers(8, 300))
+    if yuv:
+        W, H = W + (W & 1), H + (H & 1)
+    use_rois = rng.random() < 0.5
+    n_src = int(rng.integers(1, 5)) if use_rois else int(rng.integers(60, 71))
+    frames = [O.random_frame(rng, fc(O, fmt), W, H) for _ in range(n_src)]
+    if use_rois:
+        rois = []
+        for _ in range(int(rng.integers(65, 151))):
+            si = int(rng.integers(0, n_src))
+            x, y = int(rng.integers(-10, W - 1)), int(rng.integers(-10, H - 1))
+            w, h = int(rng.integers(1, W)), int(rng.integers(1, H))
+            rois.append((si, x, y, max(w, 1 - x), max(h, 1 - y)))
+        n_items = len(rois)
+    else:
+        rois, n_items = None, n_src
+    DW, DH = int(rng.integers(1, 160)), int(rng.integers(1, 160))
+    dtype = "f32" if rng.random() < 0.5 else "u8"
+    kw = {"resize": ["no-aspect-ratio", "aspect-ratio"][int(rng.integers(0, 2))],
+          "placement": "center" if rng.random() < 0.5 else "top_left", "fill": tuple(int(v) for v in rng.integers(0, 256, 3))}
+    if dtype == "f32":
+        kw["range"] = (0.0, 1.0)
+    info = evam.PreProcInfo(**kw)
+    batch = n_items + int(rng.integers(0, 40))
+    slots = rng.permutation(batch)[:n_items].astype(np.int32)
+    tdt = torch.float32 if dtype == "f32" else torch.uint8
+    out = torch.full((batch, 3, DH, DW), 7, dtype=tdt, device=gpu)
+    fuzz_pp.convert(upload(evam, frames, gpu), out, info, rois=[evam.Roi(*r) for r in rois] if rois else None,
+                    slots=slots)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy()
+    # the oracle writes item i at slot_offset + i: one item at a time into its slot
+    ref = np.full(got.shape, 7, dtype=got.dtype)
+    items = rois if rois else [(i, 0, 0, 0, 0) for i in range(n_items)]
+    one = (1, 3, DH, DW)
+    for i, r in enumerate(items):
+        part, _ = run_oracle(O, coracle, frames, one, dtype, info, rois=[r])
+        ref[slots[i]] = part[0]
+    assert_same(got, ref, f"seed {seed}: {fmt} {W}x{H} x{n_src} -> {DW}x{DH} {dtype} {kw} "
+                          f"{'%d rois' % n_items if rois else '%d frames' % n_items} batch {batch}")
