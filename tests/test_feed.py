@@ -1,4 +1,6 @@
 """Host->device feed: pinned ring + copy stream, parity with the oracle per batch."""
+import os
+
 import numpy as np
 import pytest
 
@@ -85,3 +87,52 @@ def test_feed_touched_rows_only(evam, O, coracle, gpu, fmt, resize, src, dst):
             coracle.preprocess_item(f, None, ref, i, mode=mode, lut=lut)
         assert np.array_equal(out.cpu().numpy().view(np.uint32), ref.view(np.uint32)), f"step {step}"
     pp.close()
+
+
+@pytest.mark.parametrize("seed", range(int(os.environ.get("EVAM_FUZZ_FEED_CASES", "12"))))
+def test_feed_touched_rows_random(evam, O, coracle, gpu, seed):
+    """Random geometries through set_geometry's touched-row feed: format, frame and tensor sizes, the three resize
+    modes, placement, batch; the device slots start poisoned (0xA5), so a row the plan skipped but a kernel reads
+    breaks parity with the oracle."""
+    import torch
+
+    rng = np.random.default_rng(9000 + seed)
+    fmt = ["NV12", "I420", "BGRX"][int(rng.integers(0, 3))]
+    fc = {"NV12": O.NV12, "I420": O.I420, "BGRX": O.BGRX}[fmt]
+    W, H = int(rng.integers(8, 900)), int(rng.integers(8, 700))
+    if fmt != "BGRX":
+        W, H = W + (W & 1), H + (H & 1)
+    DW, DH, B = int(rng.integers(1, 300)), int(rng.integers(1, 300)), int(rng.integers(1, 5))
+    mode = ["no-aspect-ratio", "aspect-ratio", "crop"][int(rng.integers(0, 3))]
+    kw = {"resize": "aspect-ratio", "crop": "central"} if mode == "crop" else {"resize": mode}
+    info = evam.PreProcInfo(range=(0.0, 1.0), placement="center" if rng.random() < 0.5 else "top_left",
+                            fill=(3, 130, 250), **kw)
+    feed = evam.feed.HostFeed(fc, W, H, batch=B, depth=2)
+    feed.set_geometry(DW, DH, info)
+    for d in feed.dev:
+        d.fill_(0xA5)
+    pp = evam.HipPreProcessor(device=0)
+    try:
+        for step in range(2):
+            frames = [O.random_frame(rng, fc, W, H) for _ in range(B)]
+            k = feed.acquire()
+            feed.fill(k, frames)
+            feed.submit(k)
+            out = torch.empty((B, 3, DH, DW), dtype=torch.float32, device=gpu)
+            pp.convert(feed.batch(k), out, info)
+            feed.release(k)
+            torch.cuda.synchronize()
+            ref, _ = _oracle_batch(O, coracle, frames, (B, 3, DH, DW), info)
+            assert np.array_equal(out.cpu().numpy().view(np.uint32), ref.view(np.uint32)), \
+                f"seed {seed} step {step}: {fmt} {W}x{H} -> {DW}x{DH} {kw} B {B}"
+    finally:
+        pp.close()
+
+
+def _oracle_batch(O, coracle, frames, shape, info):
+    ref = np.zeros(shape, np.float32)
+    lut = O.np_norm_lut(1, (0.0, 1.0))
+    geoms = [coracle.preprocess_item(f, None, ref, i, mode=info.resize_mode(),
+                                     placement=1 if info.placement == "center" else 0, lut=lut, fill=info.fill)
+             for i, f in enumerate(frames)]
+    return ref, geoms

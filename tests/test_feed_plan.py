@@ -58,3 +58,21 @@ def test_resized_height_matches_oracle_geometry(evam, O, src, dst, mode):
     assert rh == g["rh"] and top == (-g["oy"] if mode == 2 else 0)
     if src == (192, 320):
         assert top == 16  # 320 * 48/192 = 80 resized rows, the middle 48 visible
+
+
+@pytest.mark.parametrize("seed", range(40))
+def test_touched_rows_random_geometries(evam, O, coracle, seed):
+    """Random frame / tensor sizes and the three resize modes: resized_height against the oracle's item geometry, and
+    touched_rows against both clamped taps of every visible row of the oracle's own row table (luma and 4:2:0 chroma
+    rows)."""
+    F = evam.feed
+    rng = np.random.default_rng(700 + seed)
+    W, H = 2 * int(rng.integers(1, 1200)), 2 * int(rng.integers(1, 1200))
+    DW, DH, mode = int(rng.integers(1, 700)), int(rng.integers(1, 700)), int(rng.integers(0, 3))
+    g = O.item_geometry(O.NV12, W, H, 0, 0, 0, 0, mode, 0, DW, DH)
+    rh, top = F.resized_height(W, H, DW, DH, mode)
+    assert rh == g["rh"] and top == (-g["oy"] if mode == 2 else 0), (W, H, DW, DH, mode)
+    ofs, _, _ = coracle.linear_table(H, rh, False)
+    want = sorted({min(max(int(s) + d, 0), H - 1) for s in ofs[top:top + DH] for d in (0, 1)})
+    rows = F.touched_rows(O.NV12, W, H, DW, DH, mode)
+    assert rows[0] == want and rows[1] == sorted({r >> 1 for r in want}), (W, H, DW, DH, mode)
