@@ -755,10 +755,6 @@ struct LaneRows {
     __device__ __forceinline__ int B1(int i) const { return __builtin_amdgcn_readlane(b1, i); }
 };
 
-// Wait until at most n vector-memory operations of this wave are outstanding (n wave-uniform). s_waitcnt
-// takes an immediate, so n is rounded DOWN to one of a few levels (always safe: it only waits longer) by
-// a short ladder of scalar compares; a full 64-way switch cost more SALU and branch issue per row group
-// than it saved.
 // Workgroup barrier for data written to LDS by ds_write only: lgkmcnt(0) and a raw s_barrier. __syncthreads()
 // also waits vmcnt(0), which drains every LDS-DMA in flight (cdna_hip_programming.md, Pipelining across barriers).
 __device__ __forceinline__ void lds_barrier() {
@@ -2091,28 +2087,63 @@ __global__ __launch_bounds__(512) void evam_pp_strip(const TParams P) {
 }
 
 // Wait until at most n (>= 0, wave-uniform) vector-memory operations of this wave are outstanding, rounded down to
-// 0-4, 6, 8, 12, 16 or 32: waiting for a few more operations than needed is always safe, and the four-level branch
-// tree costs a third of the scalar instructions of an exact 64-case jump. Same box (profiles/r04k2_vmcnt_coarse_ab.txt):
-// C1 +2 %, C1/I420 +3 % against the exact jump.
+// 0-4, 6, 8, 12, 16 or 32: waiting for a few more operations than needed is always safe. A binary tree of scalar
+// compares and branches in one asm block: 4-5 compares, one wait and one branch on every path. (The same tree in C was
+// structurised by the compiler into flag registers carried through every level, ~25 scalar instructions per wait;
+// same box, one launch at a time: C1 equal, C1 / I420 +2.2 %, profiles/r06n_vmcnt_asm_ab.txt. The tree itself costs a
+// third of the scalar instructions of an exact 64-case jump, C1 +2 % against it: profiles/r04k2_vmcnt_coarse_ab.txt.)
 __device__ __forceinline__ void vmcnt_le(int n) {
     n = __builtin_amdgcn_readfirstlane(n);
-    if (n >= 16) {
-        if (n >= 32) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-    } else if (n >= 8) {
-        if (n >= 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    } else if (n >= 4) {
-        if (n >= 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    } else if (n >= 2) {
-        if (n >= 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-    } else if (n == 1) {
-        asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
-    } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    asm volatile(
+        "s_cmp_lt_i32 %0, 8\n\t"
+        "s_cbranch_scc1 5f\n\t"
+        "s_cmp_lt_i32 %0, 16\n\t"
+        "s_cbranch_scc1 2f\n\t"
+        "s_cmp_lt_i32 %0, 32\n\t"
+        "s_cbranch_scc1 1f\n\t"
+        "s_waitcnt vmcnt(32)\n\t"
+        "s_branch 9f\n"
+        "1:\n\t"
+        "s_waitcnt vmcnt(16)\n\t"
+        "s_branch 9f\n"
+        "2:\n\t"
+        "s_cmp_lt_i32 %0, 12\n\t"
+        "s_cbranch_scc1 3f\n\t"
+        "s_waitcnt vmcnt(12)\n\t"
+        "s_branch 9f\n"
+        "3:\n\t"
+        "s_waitcnt vmcnt(8)\n\t"
+        "s_branch 9f\n"
+        "5:\n\t"
+        "s_cmp_lt_i32 %0, 4\n\t"
+        "s_cbranch_scc1 7f\n\t"
+        "s_cmp_lt_i32 %0, 6\n\t"
+        "s_cbranch_scc1 6f\n\t"
+        "s_waitcnt vmcnt(6)\n\t"
+        "s_branch 9f\n"
+        "6:\n\t"
+        "s_waitcnt vmcnt(4)\n\t"
+        "s_branch 9f\n"
+        "7:\n\t"
+        "s_cmp_lt_i32 %0, 2\n\t"
+        "s_cbranch_scc1 8f\n\t"
+        "s_cmp_lt_i32 %0, 3\n\t"
+        "s_cbranch_scc1 4f\n\t"
+        "s_waitcnt vmcnt(3)\n\t"
+        "s_branch 9f\n"
+        "4:\n\t"
+        "s_waitcnt vmcnt(2)\n\t"
+        "s_branch 9f\n"
+        "8:\n\t"
+        "s_cmp_lt_i32 %0, 1\n\t"
+        "s_cbranch_scc1 10f\n\t"
+        "s_waitcnt vmcnt(1)\n\t"
+        "s_branch 9f\n"
+        "10:\n\t"
+        "s_waitcnt vmcnt(0)\n"
+        "9:"
+        ::"s"(n)
+        : "scc", "memory");
 }
 
 // Band kernel for uniform 4:2:0 batches whose consecutive output rows share source rows (vertical
