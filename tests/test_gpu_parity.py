@@ -989,3 +989,45 @@ def test_random_slots_and_large_batches(evam, O, coracle, gpu, fuzz_pp, seed):
         ref[slots[i]] = part[0]
     assert_same(got, ref, f"seed {seed}: {fmt} {W}x{H} x{n_src} -> {DW}x{DH} {dtype} {kw} "
                           f"{'%d rois' % n_items if rois else '%d frames' % n_items} batch {batch}")
+
+
+@pytest.mark.parametrize("seed", range(int(os.environ.get("EVAM_FUZZ_MIXED_CASES", "24"))))
+def test_random_mixed_format_calls(evam, O, coracle, gpu, fuzz_pp, seed):
+    """Random calls whose sources differ in format (one launch per format group, each group's ROI records in its own
+    region of the call's record slot): 2-5 sources of random formats and sizes, full frames or up to 60 ROIs over all
+    of them, every output bit-exact against the oracle."""
+    import torch
+
+    rng = np.random.default_rng(80000 + seed)
+    frames = []
+    for _ in range(int(rng.integers(2, 6))):
+        fmt = FORMATS[int(rng.integers(0, len(FORMATS)))]
+        W, H = int(rng.integers(2, 700)), int(rng.integers(2, 500))
+        if fmt in ("NV12", "I420"):
+            W, H = W + (W & 1), H + (H & 1)
+        frames.append(O.random_frame(rng, fc(O, fmt), W, H))
+    rois = None
+    if rng.random() < 0.6:
+        rois = []
+        for _ in range(int(rng.integers(1, 61))):
+            si = int(rng.integers(0, len(frames)))
+            W, H = frames[si].width, frames[si].height
+            x, y = int(rng.integers(-W // 4 - 1, W)), int(rng.integers(-H // 4 - 1, H))
+            w, h = int(rng.integers(1, W + W // 4 + 1)), int(rng.integers(1, H + H // 4 + 1))
+            rois.append((si, x, y, max(w, 1 - x), max(h, 1 - y)))
+    n_items = len(rois) if rois else len(frames)
+    DW, DH = int(rng.integers(1, 400)), int(rng.integers(1, 300))
+    dtype = "f32" if rng.random() < 0.5 else "u8"
+    mode = ["no-aspect-ratio", "aspect-ratio", "crop"][int(rng.integers(0, 3))]
+    kw = {"resize": "aspect-ratio", "crop": "central"} if mode == "crop" else {"resize": mode}
+    info = evam.PreProcInfo(placement="center" if rng.random() < 0.5 else "top_left",
+                            color_space="RGB" if rng.random() < 0.5 else "BGR",
+                            fill=tuple(int(v) for v in rng.integers(0, 256, 3)),
+                            **({"range": (0.0, 1.0), "mean": (0.2, 0.3, 0.4), "std": (0.5, 0.6, 0.7)}
+                               if dtype == "f32" else {}), **kw)
+    shape = (n_items, 3, DH, DW)
+    got, _ = run_hip(evam, torch, upload(evam, frames, gpu), shape, torch.float32 if dtype == "f32" else torch.uint8,
+                     info, rois=[evam.Roi(*r) for r in rois] if rois else None, pp=fuzz_pp)
+    ref, _ = run_oracle(O, coracle, frames, shape, dtype, info, rois=rois)
+    assert_same(got, ref, f"seed {seed}: {[(f.fourcc, f.width, f.height) for f in frames]} -> {DW}x{DH} {dtype} {kw} "
+                          f"{'%d rois' % n_items if rois else 'frames'}")
