@@ -670,3 +670,89 @@ def test_parse_ssd_batch_matches_per_item(evam):
     got = P.parse_ssd_batch(raw, 0.5)
     assert got == [P.parse_ssd(raw[i], 0.5) for i in range(9)]
     assert got[3] == [] and got[5] == []
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(3))
+@pytest.mark.parametrize("runner", ["device", "threads"])
+def test_end_to_end_random_detections_bit_exact(ps, evam, model_dir, gpu, O, coracle, runner, seed):
+    """detect -> classify with random detections: every tensor the two models receive is checked bit for bit against
+    the oracle. The detector's input is each full frame (64x64, BGR, no normalisation); the classifier's rows are the
+    crops of the `car` detections, as the JSON reports them (x, y, w, h after the box mapping), in frame and object
+    order (24x24, RGB, range [0, 1])."""
+    import torch
+
+    rng = np.random.default_rng(17 + 2 * seed + (runner == "threads"))
+    n_frames, W, H = 24, 352, 198
+    frames = [O.random_frame(rng, O.NV12, W, H, pattern="gradient" if k % 3 == 0 else "uniform")
+              for k in range(n_frames)]
+    boxes = []  # per frame: [label, conf, x0, y0, x1, y1] rows (normalised)
+    for _ in range(n_frames):
+        rows = []
+        for _ in range(int(rng.integers(0, 9))):
+            x0, y0 = rng.uniform(-0.1, 0.9, 2)
+            x1, y1 = x0 + rng.uniform(0.01, 0.6), y0 + rng.uniform(0.01, 0.6)
+            rows.append([float(rng.integers(1, 3)), 0.9, x0, y0, x1, y1])
+        boxes.append(rows)
+    det_in, cls_in = [], []
+    seen = [0]
+
+    def detector(t):
+        det_in.append(t.detach().float().cpu().numpy().copy())
+        n = t.shape[0]
+        out = torch.full((n, 10, 7), -1.0)
+        for i in range(n):
+            for j, r in enumerate(boxes[seen[0] + i]):
+                out[i, j] = torch.tensor([0.0] + r)
+        seen[0] += n
+        return out
+
+    def classifier(t):
+        cls_in.append(t.detach().float().cpu().numpy().copy())
+        m = t.mean(dim=(1, 2, 3))
+        return {"color": torch.stack([1 - m, m], 1)}
+
+    ps.PipelineServer.start({"pipeline_dir": PIPES, "model_dir": model_dir, "runner": runner})
+    try:
+        ps.PipelineServer.register_model("det_alias/det_ver", ps.InferenceModel(detector, (64, 64), name="det"))
+        ps.PipelineServer.register_model("cls_alias/cls_ver", ps.InferenceModel(classifier, (24, 24), name="cls"))
+        qin, qout = queue.Queue(), queue.Queue()
+        for f in frames:
+            qin.put({"fourcc": f.fourcc, "width": f.width, "height": f.height, "planes": f.planes})
+        qin.put(None)
+        p = ps.PipelineServer.pipeline("detect_classify", "hip")
+        p.start(source={"type": "application", "input": qin},
+                destination={"metadata": {"type": "application", "output": qout, "mode": "json"}},
+                parameters={"detection-properties": {"pre-process-backend": "hip"}})
+        st = p.wait(60)
+        assert st["state"] == "COMPLETED", st
+        lines = []
+        while True:
+            x = qout.get(timeout=5)
+            if x is None:
+                break
+            lines.append(json.loads(x))
+    finally:
+        ps.PipelineServer.stop()
+    assert len(lines) == n_frames
+    # detector input: every frame, in order
+    got = np.concatenate(det_in)
+    assert got.shape == (n_frames, 3, 64, 64)
+    ref = np.zeros(got.shape, np.float32)
+    lut0 = O.np_norm_lut(0)
+    for i, f in enumerate(frames):
+        coracle.preprocess_item(f, None, ref, i, lut=lut0)
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), "detector input"
+    # classifier input: the car crops the JSON reports, frame by frame
+    crops = [(k, o["x"], o["y"], o["w"], o["h"]) for k, d in enumerate(lines) for o in d.get("objects", [])
+             if "color" in o]
+    n_car = sum(1 for rows in boxes for r in rows if r[0] == 1.0)
+    assert crops and len(crops) <= n_car
+    got = np.concatenate(cls_in) if cls_in else np.zeros((0, 3, 24, 24), np.float32)
+    assert got.shape == (len(crops), 3, 24, 24)
+    ref = np.zeros(got.shape, np.float32)
+    lut1 = O.np_norm_lut(1, (0.0, 1.0))
+    for i, (k, x, y, w, h) in enumerate(crops):
+        coracle.preprocess_item(frames[k], (x, y, w, h), ref, i, color_rgb=True, lut=lut1)
+    bad = [i for i in range(len(crops)) if not np.array_equal(got[i].view(np.uint32), ref[i].view(np.uint32))]
+    assert not bad, f"classifier rows differ: {[(i, crops[i]) for i in bad[:5]]}"
