@@ -1031,3 +1031,36 @@ def test_random_mixed_format_calls(evam, O, coracle, gpu, fuzz_pp, seed):
     ref, _ = run_oracle(O, coracle, frames, shape, dtype, info, rois=rois)
     assert_same(got, ref, f"seed {seed}: {[(f.fourcc, f.width, f.height) for f in frames]} -> {DW}x{DH} {dtype} {kw} "
                           f"{'%d rois' % n_items if rois else 'frames'}")
+
+
+@pytest.mark.parametrize("seed", range(int(os.environ.get("EVAM_FUZZ_LARGE_CASES", "6"))))
+def test_random_large_outputs(evam, O, coracle, gpu, fuzz_pp, seed):
+    """Tensors past the ranges the other random tests draw from: 700 - 4096 columns and rows (identity sizes, 4K
+    upscales, wide strips past the strip kernel's 2,048-column limit), full frames or a few ROIs, u8 or fp32."""
+    import torch
+
+    rng = np.random.default_rng(90000 + seed)
+    fmt = FORMATS[int(rng.integers(0, len(FORMATS)))]
+    W, H = int(rng.integers(64, 2000)), int(rng.integers(64, 1200))
+    if fmt in ("NV12", "I420"):
+        W, H = W + (W & 1), H + (H & 1)
+    frames = [O.random_frame(rng, fc(O, fmt), W, H) for _ in range(int(rng.integers(1, 3)))]
+    DW, DH = int(rng.integers(700, 4097)), int(rng.integers(700, 2200))
+    if seed % 3 == 0:
+        DW, DH = W, H  # identity size
+    rois = None
+    if rng.random() < 0.4:
+        rois = [(int(rng.integers(0, len(frames))), int(rng.integers(0, W // 2)), int(rng.integers(0, H // 2)),
+                 int(rng.integers(2, W // 2)), int(rng.integers(2, H // 2))) for _ in range(int(rng.integers(1, 4)))]
+    dtype = "f32" if rng.random() < 0.4 else "u8"
+    mode = ["no-aspect-ratio", "aspect-ratio", "crop"][int(rng.integers(0, 3))]
+    kw = {"resize": "aspect-ratio", "crop": "central"} if mode == "crop" else {"resize": mode}
+    info = evam.PreProcInfo(placement="center", fill=(1, 2, 3), **({"range": (0.0, 1.0)} if dtype == "f32" else {}),
+                            **kw)
+    n = len(rois) if rois else len(frames)
+    shape = (n, 3, DH, DW)
+    got, _ = run_hip(evam, torch, upload(evam, frames, gpu), shape, torch.float32 if dtype == "f32" else torch.uint8,
+                     info, rois=[evam.Roi(*r) for r in rois] if rois else None, pp=fuzz_pp)
+    ref, _ = run_oracle(O, coracle, frames, shape, dtype, info, rois=rois)
+    assert_same(got, ref, f"seed {seed}: {fmt} {W}x{H} x{len(frames)} -> {DW}x{DH} {dtype} {kw} "
+                          f"{'%d rois' % n if rois else 'frames'}")
