@@ -756,3 +756,93 @@ def test_end_to_end_random_detections_bit_exact(ps, evam, model_dir, gpu, O, cor
         coracle.preprocess_item(frames[k], (x, y, w, h), ref, i, color_rgb=True, lut=lut1)
     bad = [i for i in range(len(crops)) if not np.array_equal(got[i].view(np.uint32), ref[i].view(np.uint32))]
     assert not bad, f"classifier rows differ: {[(i, crops[i]) for i in bad[:5]]}"
+
+
+def _fingerprint(row):
+    """24-bit fingerprint of one model-input row (exact as a float32)."""
+    import zlib
+
+    return zlib.crc32(np.ascontiguousarray(row, dtype=np.float32).tobytes()) & 0xFFFFFF
+
+
+def _box_of(fp):
+    """A car box derived from a detector-input fingerprint (dyadic, so exact in float32)."""
+    x0, y0 = (fp & 0xFF) / 512.0, ((fp >> 8) & 0xFF) / 512.0
+    return x0, y0, x0 + 0.25 + ((fp >> 16) & 0x3F) / 256.0, y0 + 0.25
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("runner,inflight", [("device", 3), ("device", 1), ("device", 4), ("threads", 1)])
+def test_pipeline_soak_fingerprints(ps, evam, model_dir, gpu, O, coracle, runner, inflight):
+    """Many detect -> classify streams at once (EVAM_SOAK_STREAMS x EVAM_SOAK_FRAMES, default 4 x 24), each stream its
+    own frame size, batched across streams by the hub with 1, 3 (the default) or 4 ticks in flight. The detector answers each input row with a
+    car box derived from a fingerprint of that row; the classifier answers with a fingerprint of its crop as the
+    confidence. Every frame's JSON box must be the one its oracle detector input implies, and every crop's confidence
+    the fingerprint of the oracle crop of the JSON rect: a frame or crop from another stream, slot or tick fails."""
+    import torch
+
+    S = int(os.environ.get("EVAM_SOAK_STREAMS", "4"))
+    F = int(os.environ.get("EVAM_SOAK_FRAMES", "24"))
+    rng = np.random.default_rng(31 + inflight + (runner == "threads"))
+    sizes = [(2 * int(rng.integers(60, 400)), 2 * int(rng.integers(40, 250))) for _ in range(S)]
+    frames = [[O.random_frame(rng, O.NV12, *sizes[s]) for _ in range(F)] for s in range(S)]
+
+    def detector(t):
+        a = t.detach().float().cpu().numpy()
+        out = torch.full((a.shape[0], 2, 7), -1.0)
+        for i in range(a.shape[0]):
+            out[i, 0] = torch.tensor([0.0, 1.0, 0.9, *_box_of(_fingerprint(a[i]))])
+        return out
+
+    def classifier(t):
+        a = t.detach().float().cpu().numpy()
+        return {"color": torch.tensor([[float(_fingerprint(a[i])), -1.0] for i in range(a.shape[0])])}
+
+    ps.PipelineServer.start({"pipeline_dir": PIPES, "model_dir": model_dir, "runner": runner, "inflight": inflight})
+    outs = []
+    try:
+        ps.PipelineServer.register_model("det_alias/det_ver", ps.InferenceModel(detector, (64, 64), name="det"))
+        ps.PipelineServer.register_model("cls_alias/cls_ver", ps.InferenceModel(classifier, (24, 24), name="cls"))
+        pipes = []
+        for s in range(S):
+            qin, qout = queue.Queue(), queue.Queue()
+            for f in frames[s]:
+                qin.put({"fourcc": f.fourcc, "width": f.width, "height": f.height, "planes": f.planes})
+            qin.put(None)
+            p = ps.PipelineServer.pipeline("detect_classify", "hip")
+            p.start(source={"type": "application", "input": qin},
+                    destination={"metadata": {"type": "application", "output": qout, "mode": "json"}},
+                    parameters={"detection-properties": {"pre-process-backend": "hip"}})
+            pipes.append(p)
+            outs.append(qout)
+        for p in pipes:
+            st = p.wait(120)
+            assert st["state"] == "COMPLETED", st
+    finally:
+        ps.PipelineServer.stop()
+    lut0, lut1 = O.np_norm_lut(0), O.np_norm_lut(1, (0.0, 1.0))
+    n_crops = 0
+    for s in range(S):
+        lines = []
+        while True:
+            x = outs[s].get(timeout=5)
+            if x is None:
+                break
+            lines.append(json.loads(x))
+        assert len(lines) == F, (s, len(lines))
+        for k, d in enumerate(lines):
+            f = frames[s][k]
+            det = np.zeros((1, 3, 64, 64), np.float32)
+            coracle.preprocess_item(f, None, det, 0, lut=lut0)
+            want = _box_of(_fingerprint(det[0]))
+            (obj,) = d["objects"]
+            bb = obj["detection"]["bounding_box"]
+            got = (bb["x_min"], bb["y_min"], bb["x_max"], bb["y_max"])
+            assert np.allclose(got, want, rtol=0, atol=1e-6), f"stream {s} frame {k}: detector input differs"
+            if "color" not in obj:
+                continue
+            crop = np.zeros((1, 3, 24, 24), np.float32)
+            coracle.preprocess_item(f, (obj["x"], obj["y"], obj["w"], obj["h"]), crop, 0, color_rgb=True, lut=lut1)
+            assert obj["color"]["confidence"] == float(_fingerprint(crop[0])), f"stream {s} frame {k}: crop differs"
+            n_crops += 1
+    assert n_crops > S * F // 2
