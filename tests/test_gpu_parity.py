@@ -1064,3 +1064,58 @@ def test_random_large_outputs(evam, O, coracle, gpu, fuzz_pp, seed):
     ref, _ = run_oracle(O, coracle, frames, shape, dtype, info, rois=rois)
     assert_same(got, ref, f"seed {seed}: {fmt} {W}x{H} x{len(frames)} -> {DW}x{DH} {dtype} {kw} "
                           f"{'%d rois' % n if rois else 'frames'}")
+
+
+@pytest.mark.parametrize("seed", range(int(os.environ.get("EVAM_FUZZ_INVALID_CASES", "24"))))
+def test_random_invalid_calls(evam, O, coracle, gpu, fuzz_pp, seed):
+    """A random valid call (random_case) broken in one way — an ROI outside its frame, a source index out of range, a
+    slot past the tensor, a repeated explicit slot, a misaligned plane pitch, an odd 4:2:0 size: the call fails with
+    the documented status before anything is written (the output keeps its fill), and the same handle then runs the
+    unbroken call bit-exact."""
+    import torch
+
+    rng = np.random.default_rng(60000 + seed)
+    fmt, frames, shape, dtype, info, rois, offset, stride = random_case(evam, O, rng)
+    imgs = upload(evam, frames, gpu)
+    n_items = len(rois) if rois else len(frames)
+    kinds = ["empty_roi", "src_index", "slot_past_end", "misaligned_pitch"]
+    if n_items >= 2:
+        kinds.append("repeated_slot")
+    if fmt in ("NV12", "I420"):
+        kinds.append("odd_420")
+    kind = kinds[int(rng.integers(0, len(kinds)))]
+    bad_imgs, bad_rois = list(imgs), list(rois) if rois else [(i, 0, 0, 0, 0) for i in range(len(frames))]
+    kw = {"slot_offset": offset, "slot_stride": stride}
+    if kind == "empty_roi":  # the last item replaced: the item count (and so every slot) stays valid
+        W, H = frames[0].width, frames[0].height
+        bad_rois[-1] = (0, W + 5, H + 5, 4, 4)
+    elif kind == "src_index":
+        bad_rois[-1] = (len(frames), 0, 0, 0, 0)
+    elif kind == "slot_past_end":
+        kw["slot_offset"] = shape[0] - (n_items - 1) * stride  # the last item one slot past the end
+    elif kind == "repeated_slot":
+        kw = {"slots": np.array([0] * n_items, dtype=np.int32)}
+    elif kind == "misaligned_pitch":
+        im = imgs[0]
+        p0 = im.planes[0]
+        pitch = p0.shape[1] + 8  # >= the row bytes, not a multiple of 16
+        q = torch.zeros((p0.shape[0], pitch), dtype=torch.uint8, device=gpu)
+        bad_imgs[0] = evam.Image(im.fourcc, im.width, im.height, [q] + list(im.planes[1:]))
+    elif kind == "odd_420":
+        im = imgs[0]
+        bad_imgs[0] = evam.Image(im.fourcc, im.width - 1, im.height, list(im.planes))
+    want = {"empty_roi": -4, "src_index": -1, "slot_past_end": -1, "repeated_slot": -1, "misaligned_pitch": -3,
+            "odd_420": -1}[kind]
+    tdt = torch.float32 if dtype == "f32" else torch.uint8
+    if kind in ("misaligned_pitch", "odd_420", "repeated_slot") and not rois:
+        bad_rois = None  # a frame-list call
+    out = torch.full(shape, 7, dtype=tdt, device=gpu)
+    with pytest.raises(evam.PreProcError) as ei:
+        fuzz_pp.convert(bad_imgs, out, info, rois=[evam.Roi(*r) for r in bad_rois] if bad_rois else None, **kw)
+    torch.cuda.synchronize()
+    assert ei.value.status == want, f"seed {seed} {kind}: {ei.value}"
+    assert bool((out == 7).all()), f"seed {seed} {kind}: the failed call wrote into the output"
+    got, _ = run_hip(evam, torch, imgs, shape, tdt, info, rois=[evam.Roi(*r) for r in rois] if rois else None,
+                     slot_offset=offset, slot_stride=stride, pp=fuzz_pp)
+    ref, _ = run_oracle(O, coracle, frames, shape, dtype, info, rois=rois, slot_offset=offset, slot_stride=stride)
+    assert_same(got, ref, f"seed {seed}: the call after a {kind} failure")
